@@ -1,0 +1,173 @@
+/*
+ * dcn.h — C-ABI of libdcn.so, the MI355X (gfx950) DeformConv2d operator.
+ *
+ * The reference (x-y20/jittor-dcn) has no FFI: its boundary is the Python module
+ * `DeformConv2d` in deform_conv.py. Each entry point below replaces one piece of
+ * that module's behaviour; the file:line it replaces is cited next to it. The
+ * Python drop-in (jittor-dcn_amd/deform_conv.py) binds these symbols with ctypes.
+ *
+ * Conventions
+ *  - Every function returns int: 0 = OK, < 0 = dcn_status error code. The
+ *    library never aborts; dcn_last_error() returns a thread-local message.
+ *  - Tensors are fp32, dense, NCHW (x, out, offsets) or the reference's own
+ *    parameter layouts (weights). All device pointers are caller-owned; the
+ *    library never frees or retains them.
+ *  - Calls are ordered on the handle's stream (dcn_set_stream). A handle is not
+ *    thread-safe: use one handle per device and per host thread.
+ *  - `*_host` variants take host pointers, move data over PCIe themselves and
+ *    synchronise before returning (the NumPy / Jittor-CPU caller's path).
+ *
+ * Semantics are exactly deform_conv.py:56-81 (see DESIGN.md §1 "quirks"):
+ * transposed sampling, coordinates normalised by the OUTPUT size, no per-tap
+ * base offsets, offset channels [Δx(0..N-1) | Δy(0..N-1)], weight read as
+ * W[o][n][c]. `dil_h/dil_w/deform_groups` are extensions (BASELINE config 5)
+ * that must be 1 for reference semantics.
+ */
+#ifndef DCN_H_
+#define DCN_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DCN_ABI_VERSION 1
+
+typedef enum {
+  DCN_OK = 0,
+  DCN_ERR_INVALID = -1,     /* bad descriptor / argument */
+  DCN_ERR_UNSUPPORTED = -2, /* shape or dtype outside what the build supports */
+  DCN_ERR_HIP = -3,         /* HIP runtime error (no device, OOM, launch) */
+  DCN_ERR_BLAS = -4,        /* rocBLAS error */
+  DCN_ERR_WORKSPACE = -5    /* caller workspace too small */
+} dcn_status;
+
+typedef enum { DCN_F32 = 0, DCN_BF16 = 1 } dcn_dtype;
+
+/* Geometry of one DeformConv2d call. Mirrors the constructor arguments of
+ * deform_conv.py:7 (in_channels=C, out_channels=O, kernel_size=(kh,kw),
+ * stride=(sh,sw), padding=(ph,pw), bias) plus the input batch shape. */
+typedef struct {
+  int B, C, H, W; /* input x[B][C][H][W] */
+  int O;          /* out_channels */
+  int kh, kw;     /* kernel_size, deform_conv.py:11 */
+  int sh, sw;     /* stride, deform_conv.py:12 */
+  int ph, pw;     /* padding, deform_conv.py:13 */
+  int dil_h, dil_w;  /* extension: offset-conv dilation (1 = reference) */
+  int deform_groups; /* extension: offset groups (1 = reference) */
+  int dtype;         /* dcn_dtype; only DCN_F32 in this build */
+  int has_bias;      /* deform_conv.py:25 */
+} dcn_desc;
+
+typedef struct dcn_handle dcn_handle;
+
+/* ---- library / device ---------------------------------------------------- */
+int dcn_abi_version(void);
+const char* dcn_last_error(void);
+int dcn_device_count(int* n);
+int dcn_create(int device, dcn_handle** out);
+int dcn_destroy(dcn_handle* h);
+/* Bind the handle to an existing hipStream_t (NULL = handle's own stream). */
+int dcn_set_stream(dcn_handle* h, void* hip_stream);
+int dcn_get_stream(dcn_handle* h, void** hip_stream);
+int dcn_synchronize(dcn_handle* h);
+
+/* ---- device memory helpers (ctypes callers without another runtime) -------- */
+int dcn_malloc(dcn_handle* h, size_t bytes, void** ptr);
+int dcn_free(dcn_handle* h, void* ptr);
+int dcn_memcpy_h2d(dcn_handle* h, void* dst, const void* src, size_t bytes);
+int dcn_memcpy_d2h(dcn_handle* h, void* dst, const void* src, size_t bytes);
+int dcn_memset_zero(dcn_handle* h, void* dst, size_t bytes);
+
+/* ---- shapes -------------------------------------------------------------- */
+/* Output size, deform_conv.py:34-35 (dilation-aware for the extension). */
+int dcn_out_shape(const dcn_desc* d, int* Ho, int* Wo);
+/* Device workspace needed by dcn_forward (with_backward=0) or by the pair
+ * dcn_forward + dcn_backward sharing one workspace (with_backward=1). */
+int dcn_workspace_bytes(const dcn_desc* d, int with_backward, size_t* bytes);
+
+/* ---- hot-path kernels (device pointers, stream-ordered) -------------------- */
+/* offset = offset_conv(x): replaces deform_conv.py:58 (nn.Conv from :16-21).
+ * w_off[2N·G][C][kh][kw], b_off[2N·G] -> off[B][2N·G][Ho][Wo]. */
+int dcn_offset_conv_fwd(dcn_handle* h, const dcn_desc* d, const float* x,
+                        const float* w_off, const float* b_off, float* off);
+/* Backward of the offset conv: grad_w_off = Σ, grad_b_off = Σ (overwritten);
+ * grad_x += conv_transpose(grad_off, w_off) (accumulated). */
+int dcn_offset_conv_bwd(dcn_handle* h, const dcn_desc* d, const float* x,
+                        const float* w_off, const float* grad_off,
+                        float* grad_x, float* grad_w_off, float* grad_b_off);
+/* Deformable bilinear im2col (K1): replaces deform_conv.py:30-54 and :62-73
+ * (grid build, normalisation, x_repeat, grid_sample, permutes).
+ * col[b][n·C + c][ho·Wo + wo] for images b in [b0, b0+nb). */
+int dcn_im2col_fwd(dcn_handle* h, const dcn_desc* d, const float* x,
+                   const float* off, float* col, int b0, int nb);
+/* Backward of K1 (K5): grad_x += Σ scatter(grad_col) (accumulated, atomics);
+ * grad_off[b][..][ho][wo] = coordinate gradient (overwritten), for images
+ * [b0, b0+nb). grad_col has the layout of dcn_im2col_fwd's col. */
+int dcn_col2im_coord_bwd(dcn_handle* h, const dcn_desc* d, const float* x,
+                         const float* off, const float* grad_col,
+                         float* grad_x, float* grad_off, int b0, int nb);
+
+/* ---- whole-op entry points ------------------------------------------------- */
+/* DeformConv2d.execute (deform_conv.py:56-81). Writes out[B][O][Ho][Wo] and the
+ * offsets off[B][2N·G][Ho][Wo] (kept by the caller for backward). ws must hold
+ * dcn_workspace_bytes(d, with_backward) bytes; when with_backward, the sampled
+ * columns stay in ws for dcn_backward (flag DCN_BWD_COL_IN_WS). */
+int dcn_forward(dcn_handle* h, const dcn_desc* d, const float* x,
+                const float* w_off, const float* b_off, const float* w,
+                const float* b, float* out, float* off, void* ws,
+                size_t ws_bytes);
+
+#define DCN_BWD_COL_IN_WS 1 /* ws still holds forward's columns */
+
+/* Autodiff of DeformConv2d.execute as triggered by optimizer.backward
+ * (train.py:414). Overwrites grad_x, grad_w, grad_b (if has_bias),
+ * grad_w_off, grad_b_off. grad_off_out (optional, may be NULL) receives
+ * ∂L/∂offset [B][2N·G][Ho][Wo]. */
+int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x,
+                 const float* off, const float* w_off, const float* w,
+                 const float* grad_out, float* grad_x, float* grad_w,
+                 float* grad_b, float* grad_w_off, float* grad_b_off,
+                 float* grad_off_out, void* ws, size_t ws_bytes, int flags);
+
+/* Host-pointer variants (NumPy / Jittor-CPU callers). Synchronous. */
+int dcn_forward_host(dcn_handle* h, const dcn_desc* d, const float* x,
+                     const float* w_off, const float* b_off, const float* w,
+                     const float* b, float* out, float* off);
+int dcn_backward_host(dcn_handle* h, const dcn_desc* d, const float* x,
+                      const float* off, const float* w_off, const float* w,
+                      const float* grad_out, float* grad_x, float* grad_w,
+                      float* grad_b, float* grad_w_off, float* grad_b_off,
+                      float* grad_off_out);
+
+/* ---- in-library kernel timing (HIP events on the handle's stream) ---------- */
+typedef enum {
+  DCN_K_OFFSET_FWD = 0,
+  DCN_K_IM2COL = 1,
+  DCN_K_GEMM_FWD = 2,
+  DCN_K_BIAS_FWD = 3,
+  DCN_K_BWD_BIAS = 4,
+  DCN_K_GEMM_DW = 5,
+  DCN_K_GEMM_DCOL = 6,
+  DCN_K_COL2IM = 7,
+  DCN_K_OFFSET_BWD = 8,
+  DCN_K_COUNT = 9
+} dcn_kernel_id;
+/* Record start/stop events around every launch of each kernel class, up to
+ * `capacity` launches per class (0 disables). */
+int dcn_prof_enable(dcn_handle* h, int capacity);
+/* Sum of elapsed ms and number of recorded launches (synchronises first). */
+int dcn_prof_read(dcn_handle* h, int kernel_id, double* total_ms, int* count);
+int dcn_prof_reset(dcn_handle* h);
+
+/* ---- testing ------------------------------------------------------------------ */
+/* 1 = route K1/K5 through the generic global-gather kernels (independent
+ * implementation used by the parity tests to cross-check the LDS-window ones). */
+int dcn_debug_force_generic(int on);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DCN_H_ */

@@ -1,0 +1,570 @@
+// dcn_api.cpp — C-ABI of libdcn.so (include/dcn.h): handles, workspace, the
+// DeformConv2d forward/backward pipelines and the three dense contractions on
+// rocBLAS (exact fp32 MFMA GEMMs on gfx950).
+//
+// Forward  = deform_conv.py:56-81:  K3 offset conv -> K1 deformable im2col ->
+//            GEMM (out_b = W[O][N*C] · col_b) -> bias.
+// Backward = Jittor autodiff of the same graph (train.py:414): ∂b, ∂W (per-image
+//            GEMM partials + deterministic sum), ∂col = Wᵀ·∂out, K5 col2im +
+//            coordinate gradient, offset-conv backward.
+#include <rocblas/rocblas.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "dcn_internal.h"
+
+using dcn::Geo;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+  do {                                                                                       \
+    hipError_t e_ = (expr);                                                                  \
+    if (e_ != hipSuccess)                                                                    \
+      return fail(DCN_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));           \
+  } while (0)
+
+#define BLAS_TRY(expr)                                                                       \
+  do {                                                                                       \
+    rocblas_status s_ = (expr);                                                              \
+    if (s_ != rocblas_status_success)                                                        \
+      return fail(DCN_ERR_BLAS, std::string(#expr) + ": " + rocblas_status_to_string(s_));   \
+  } while (0)
+
+#define DCN_TRY(expr)           \
+  do {                          \
+    int r_ = (expr);            \
+    if (r_ != DCN_OK) return r_; \
+  } while (0)
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// Validate a descriptor and derive the geometry (deform_conv.py:7-14, :34-35).
+int make_geo(const dcn_desc* d, Geo* g) {
+  if (!d || !g) return fail(DCN_ERR_INVALID, "null descriptor");
+  if (d->B <= 0 || d->C <= 0 || d->H <= 0 || d->W <= 0 || d->O <= 0)
+    return fail(DCN_ERR_INVALID, "B, C, H, W, O must be positive");
+  if (d->kh <= 0 || d->kw <= 0 || d->sh <= 0 || d->sw <= 0 || d->ph < 0 || d->pw < 0)
+    return fail(DCN_ERR_INVALID, "kernel/stride must be positive, padding >= 0");
+  if (d->dil_h <= 0 || d->dil_w <= 0 || d->deform_groups <= 0)
+    return fail(DCN_ERR_INVALID, "dilation and deform_groups must be >= 1");
+  if (d->C % d->deform_groups != 0)
+    return fail(DCN_ERR_INVALID, "in_channels must be divisible by deform_groups");
+  if (d->dtype != DCN_F32)
+    return fail(DCN_ERR_UNSUPPORTED, "only DCN_F32 is implemented in this build");
+  Geo& q = *g;
+  q.B = d->B; q.C = d->C; q.H = d->H; q.W = d->W; q.O = d->O;
+  q.kh = d->kh; q.kw = d->kw; q.sh = d->sh; q.sw = d->sw; q.ph = d->ph; q.pw = d->pw;
+  q.dh = d->dil_h; q.dw = d->dil_w; q.G = d->deform_groups;
+  q.Ho = (d->H + 2 * d->ph - d->dil_h * (d->kh - 1) - 1) / d->sh + 1;
+  q.Wo = (d->W + 2 * d->pw - d->dil_w * (d->kw - 1) - 1) / d->sw + 1;
+  if (q.Ho <= 0 || q.Wo <= 0) return fail(DCN_ERR_INVALID, "empty output (input too small)");
+  if (q.Ho < 2 || q.Wo < 2)
+    return fail(DCN_ERR_UNSUPPORTED,
+                "H_out or W_out == 1: the reference divides by (W_out-1)/(H_out-1) "
+                "(deform_conv.py:37-38)");
+  q.N = d->kh * d->kw;
+  q.K = q.N * d->C;
+  q.HW = q.Ho * q.Wo;
+  q.HWi = d->H * d->W;
+  q.Cg = d->C / d->deform_groups;
+  q.J = 2 * q.N * q.G;
+  if ((long long)q.K * q.HW > (1LL << 31) - 1 || (long long)q.HWi > (1LL << 30))
+    return fail(DCN_ERR_UNSUPPORTED, "per-image column block exceeds 2^31 elements");
+  if ((long long)q.O > (1 << 30) || (long long)q.K > (1 << 30))
+    return fail(DCN_ERR_UNSUPPORTED, "channel counts too large");
+  return DCN_OK;
+}
+
+struct WsLayout {
+  size_t col = 0, col_bytes = 0;    // [B][K][HW]
+  size_t parts = 0, parts_bytes = 0;  // [B][O*K] ∂W partials
+  size_t goff = 0, goff_bytes = 0;  // [B][J][HW] ∂offset (when caller passes none)
+  size_t total = 0;
+};
+
+WsLayout ws_layout(const Geo& g, bool bwd) {
+  WsLayout L;
+  L.col = 0;
+  L.col_bytes = (size_t)g.B * g.K * g.HW * sizeof(float);
+  size_t off = align_up(L.col_bytes, 256);
+  if (bwd) {
+    L.parts = off;
+    L.parts_bytes = (size_t)g.B * g.O * g.K * sizeof(float);
+    off = align_up(off + L.parts_bytes, 256);
+    L.goff = off;
+    L.goff_bytes = (size_t)g.B * g.J * g.HW * sizeof(float);
+    off = align_up(off + L.goff_bytes, 256);
+  }
+  L.total = off;
+  return L;
+}
+
+}  // namespace
+
+struct dcn_handle {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  rocblas_handle blas = nullptr;
+  // handle-owned workspace (host-pointer API)
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  // profiling: events per kernel class
+  int prof_cap = 0;
+  std::vector<hipEvent_t> ev[DCN_K_COUNT];  // pairs: [2*i] start, [2*i+1] stop
+  int prof_n[DCN_K_COUNT] = {0};
+};
+
+namespace {
+
+struct ProfScope {
+  dcn_handle* h;
+  int id;
+  bool on;
+  ProfScope(dcn_handle* hh, int k) : h(hh), id(k), on(hh->prof_cap > 0 && hh->prof_n[k] < hh->prof_cap) {
+    if (on) (void)hipEventRecord(h->ev[id][2 * h->prof_n[id]], h->stream);
+  }
+  ~ProfScope() {
+    if (on) {
+      (void)hipEventRecord(h->ev[id][2 * h->prof_n[id] + 1], h->stream);
+      ++h->prof_n[id];
+    }
+  }
+};
+
+int set_device(dcn_handle* h) {
+  if (!h) return fail(DCN_ERR_INVALID, "null handle");
+  HIP_TRY(hipSetDevice(h->device));
+  return DCN_OK;
+}
+
+// ---- forward core ------------------------------------------------------------
+int core_forward(dcn_handle* h, const Geo& g, const float* x, const float* off, const float* w,
+                 const float* b, bool has_bias, float* out, float* col) {
+  {
+    ProfScope ps(h, DCN_K_IM2COL);
+    HIP_TRY(dcn::launch_im2col(g, x, off, col, 0, g.B, h->stream));
+  }
+  {
+    // out_b[O][HW] = Wf[O][K] · col_b[K][HW]; column-major: C(HW×O) = col_b(HW×K) · Wf(K×O)
+    ProfScope ps(h, DCN_K_GEMM_FWD);
+    const float one = 1.f, zero = 0.f;
+    BLAS_TRY(rocblas_sgemm_strided_batched(h->blas, rocblas_operation_none, rocblas_operation_none,
+                                           g.HW, g.O, g.K, &one, col, g.HW, (rocblas_stride)g.K * g.HW,
+                                           w, g.K, 0, &zero, out, g.HW, (rocblas_stride)g.O * g.HW, g.B));
+  }
+  if (has_bias) {
+    ProfScope ps(h, DCN_K_BIAS_FWD);
+    HIP_TRY(dcn::launch_bias_add(g, out, b, 0, g.B, h->stream));
+  }
+  return DCN_OK;
+}
+
+int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off, const float* w,
+                  const float* gout, float* gx, float* gw, float* gb, bool has_bias, float* goff,
+                  float* col, float* parts, bool col_valid) {
+  if (!col_valid) {
+    ProfScope ps(h, DCN_K_IM2COL);
+    HIP_TRY(dcn::launch_im2col(g, x, off, col, 0, g.B, h->stream));
+  }
+  if (has_bias) {
+    ProfScope ps(h, DCN_K_BWD_BIAS);
+    HIP_TRY(dcn::launch_bias_grad(g, gout, gb, h->stream));
+  }
+  const float one = 1.f, zero = 0.f;
+  {
+    // ∂Wf[O][K] = Σ_b ∂out_b[O][HW] · col_bᵀ; column-major per image:
+    // P_b(K×O) = col_bᵀ (K×HW) · ∂out_b (HW×O); then deterministic Σ_b.
+    ProfScope ps(h, DCN_K_GEMM_DW);
+    BLAS_TRY(rocblas_sgemm_strided_batched(h->blas, rocblas_operation_transpose, rocblas_operation_none,
+                                           g.K, g.O, g.HW, &one, col, g.HW, (rocblas_stride)g.K * g.HW,
+                                           gout, g.HW, (rocblas_stride)g.O * g.HW, &zero, parts, g.K,
+                                           (rocblas_stride)g.K * g.O, g.B));
+    HIP_TRY(dcn::launch_sum_partials(parts, g.B, (size_t)g.K * g.O, gw, h->stream));
+  }
+  {
+    // ∂col_b[K][HW] = Wfᵀ · ∂out_b; column-major: C(HW×K) = ∂out_b(HW×O) · Wfᵀ(O×K)
+    ProfScope ps(h, DCN_K_GEMM_DCOL);
+    BLAS_TRY(rocblas_sgemm_strided_batched(h->blas, rocblas_operation_none, rocblas_operation_transpose,
+                                           g.HW, g.K, g.O, &one, gout, g.HW, (rocblas_stride)g.O * g.HW,
+                                           w, g.K, 0, &zero, col, g.HW, (rocblas_stride)g.K * g.HW, g.B));
+  }
+  HIP_TRY(hipMemsetAsync(gx, 0, (size_t)g.B * g.C * g.HWi * sizeof(float), h->stream));
+  {
+    ProfScope ps(h, DCN_K_COL2IM);
+    HIP_TRY(dcn::launch_col2im_coord(g, x, off, col, gx, goff, 0, g.B, h->stream));
+  }
+  return DCN_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dcn_abi_version(void) { return DCN_ABI_VERSION; }
+
+const char* dcn_last_error(void) { return g_err.c_str(); }
+
+int dcn_device_count(int* n) {
+  if (!n) return fail(DCN_ERR_INVALID, "null out pointer");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    *n = 0;
+    return fail(DCN_ERR_HIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+  }
+  *n = c;
+  return DCN_OK;
+}
+
+int dcn_create(int device, dcn_handle** out) {
+  if (!out) return fail(DCN_ERR_INVALID, "null out pointer");
+  *out = nullptr;
+  int n = 0;
+  DCN_TRY(dcn_device_count(&n));
+  if (device < 0 || device >= n) return fail(DCN_ERR_INVALID, "device index out of range");
+  dcn_handle* h = new dcn_handle();
+  h->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete h;
+    return fail(DCN_ERR_HIP, std::string("dcn_create: ") + hipGetErrorString(e));
+  }
+  h->stream = h->own;
+  if (rocblas_create_handle(&h->blas) != rocblas_status_success ||
+      rocblas_set_stream(h->blas, h->stream) != rocblas_status_success) {
+    (void)hipStreamDestroy(h->own);
+    delete h;
+    return fail(DCN_ERR_BLAS, "rocblas_create_handle failed");
+  }
+  *out = h;
+  return DCN_OK;
+}
+
+int dcn_destroy(dcn_handle* h) {
+  if (!h) return DCN_OK;
+  (void)hipSetDevice(h->device);
+  (void)hipStreamSynchronize(h->stream);
+  for (auto& v : h->ev)
+    for (hipEvent_t e : v) (void)hipEventDestroy(e);
+  if (h->ws) (void)hipFree(h->ws);
+  if (h->blas) (void)rocblas_destroy_handle(h->blas);
+  if (h->own) (void)hipStreamDestroy(h->own);
+  delete h;
+  return DCN_OK;
+}
+
+int dcn_set_stream(dcn_handle* h, void* s) {
+  DCN_TRY(set_device(h));
+  h->stream = s ? reinterpret_cast<hipStream_t>(s) : h->own;
+  BLAS_TRY(rocblas_set_stream(h->blas, h->stream));
+  return DCN_OK;
+}
+
+int dcn_get_stream(dcn_handle* h, void** s) {
+  if (!h || !s) return fail(DCN_ERR_INVALID, "null argument");
+  *s = h->stream;
+  return DCN_OK;
+}
+
+int dcn_synchronize(dcn_handle* h) {
+  DCN_TRY(set_device(h));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return DCN_OK;
+}
+
+int dcn_malloc(dcn_handle* h, size_t bytes, void** ptr) {
+  if (!ptr) return fail(DCN_ERR_INVALID, "null out pointer");
+  DCN_TRY(set_device(h));
+  HIP_TRY(hipMalloc(ptr, bytes ? bytes : 1));
+  return DCN_OK;
+}
+
+int dcn_free(dcn_handle* h, void* ptr) {
+  DCN_TRY(set_device(h));
+  if (ptr) HIP_TRY(hipFree(ptr));
+  return DCN_OK;
+}
+
+int dcn_memcpy_h2d(dcn_handle* h, void* dst, const void* src, size_t bytes) {
+  DCN_TRY(set_device(h));
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return DCN_OK;
+}
+
+int dcn_memcpy_d2h(dcn_handle* h, void* dst, const void* src, size_t bytes) {
+  DCN_TRY(set_device(h));
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return DCN_OK;
+}
+
+int dcn_memset_zero(dcn_handle* h, void* dst, size_t bytes) {
+  DCN_TRY(set_device(h));
+  HIP_TRY(hipMemsetAsync(dst, 0, bytes, h->stream));
+  return DCN_OK;
+}
+
+int dcn_out_shape(const dcn_desc* d, int* Ho, int* Wo) {
+  Geo g;
+  DCN_TRY(make_geo(d, &g));
+  if (Ho) *Ho = g.Ho;
+  if (Wo) *Wo = g.Wo;
+  return DCN_OK;
+}
+
+int dcn_workspace_bytes(const dcn_desc* d, int with_backward, size_t* bytes) {
+  if (!bytes) return fail(DCN_ERR_INVALID, "null out pointer");
+  Geo g;
+  DCN_TRY(make_geo(d, &g));
+  *bytes = ws_layout(g, with_backward != 0).total;
+  return DCN_OK;
+}
+
+int dcn_offset_conv_fwd(dcn_handle* h, const dcn_desc* d, const float* x, const float* w_off,
+                        const float* b_off, float* off) {
+  Geo g;
+  DCN_TRY(make_geo(d, &g));
+  DCN_TRY(set_device(h));
+  ProfScope ps(h, DCN_K_OFFSET_FWD);
+  HIP_TRY(dcn::launch_offset_conv_fwd(g, x, w_off, b_off, off, nullptr, h->stream));
+  return DCN_OK;
+}
+
+int dcn_offset_conv_bwd(dcn_handle* h, const dcn_desc* d, const float* x, const float* w_off,
+                        const float* grad_off, float* grad_x, float* grad_w_off,
+                        float* grad_b_off) {
+  Geo g;
+  DCN_TRY(make_geo(d, &g));
+  DCN_TRY(set_device(h));
+  ProfScope ps(h, DCN_K_OFFSET_BWD);
+  HIP_TRY(dcn::launch_offset_conv_bwd(g, x, w_off, grad_off, grad_x, grad_w_off, grad_b_off,
+                                      h->stream));
+  return DCN_OK;
+}
+
+int dcn_im2col_fwd(dcn_handle* h, const dcn_desc* d, const float* x, const float* off,
+                   float* col, int b0, int nb) {
+  Geo g;
+  DCN_TRY(make_geo(d, &g));
+  DCN_TRY(set_device(h));
+  if (b0 < 0 || nb < 0 || b0 + nb > g.B) return fail(DCN_ERR_INVALID, "image range out of bounds");
+  ProfScope ps(h, DCN_K_IM2COL);
+  HIP_TRY(dcn::launch_im2col(g, x, off, col, b0, nb, h->stream));
+  return DCN_OK;
+}
+
+int dcn_col2im_coord_bwd(dcn_handle* h, const dcn_desc* d, const float* x, const float* off,
+                         const float* grad_col, float* grad_x, float* grad_off, int b0, int nb) {
+  Geo g;
+  DCN_TRY(make_geo(d, &g));
+  DCN_TRY(set_device(h));
+  if (b0 < 0 || nb < 0 || b0 + nb > g.B) return fail(DCN_ERR_INVALID, "image range out of bounds");
+  ProfScope ps(h, DCN_K_COL2IM);
+  HIP_TRY(dcn::launch_col2im_coord(g, x, off, grad_col, grad_x, grad_off, b0, nb, h->stream));
+  return DCN_OK;
+}
+
+int dcn_forward(dcn_handle* h, const dcn_desc* d, const float* x, const float* w_off,
+                const float* b_off, const float* w, const float* b, float* out, float* off,
+                void* ws, size_t ws_bytes) {
+  Geo g;
+  DCN_TRY(make_geo(d, &g));
+  DCN_TRY(set_device(h));
+  const WsLayout L = ws_layout(g, false);
+  if (!ws || ws_bytes < L.total) return fail(DCN_ERR_WORKSPACE, "workspace too small for dcn_forward");
+  if (d->has_bias && !b) return fail(DCN_ERR_INVALID, "has_bias set but bias is NULL");
+  {
+    ProfScope ps(h, DCN_K_OFFSET_FWD);
+    HIP_TRY(dcn::launch_offset_conv_fwd(g, x, w_off, b_off, off, nullptr, h->stream));
+  }
+  float* col = reinterpret_cast<float*>(static_cast<char*>(ws) + L.col);
+  return core_forward(h, g, x, off, w, b, d->has_bias != 0, out, col);
+}
+
+int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* off,
+                 const float* w_off, const float* w, const float* grad_out, float* grad_x,
+                 float* grad_w, float* grad_b, float* grad_w_off, float* grad_b_off,
+                 float* grad_off_out, void* ws, size_t ws_bytes, int flags) {
+  Geo g;
+  DCN_TRY(make_geo(d, &g));
+  DCN_TRY(set_device(h));
+  const WsLayout L = ws_layout(g, true);
+  if (!ws || ws_bytes < L.total) return fail(DCN_ERR_WORKSPACE, "workspace too small for dcn_backward");
+  if (d->has_bias && !grad_b) return fail(DCN_ERR_INVALID, "has_bias set but grad_b is NULL");
+  char* base = static_cast<char*>(ws);
+  float* col = reinterpret_cast<float*>(base + L.col);
+  float* parts = reinterpret_cast<float*>(base + L.parts);
+  float* goff = grad_off_out ? grad_off_out : reinterpret_cast<float*>(base + L.goff);
+  DCN_TRY(core_backward(h, g, x, off, w, grad_out, grad_x, grad_w, grad_b, d->has_bias != 0, goff,
+                        col, parts, (flags & DCN_BWD_COL_IN_WS) != 0));
+  ProfScope ps(h, DCN_K_OFFSET_BWD);
+  HIP_TRY(dcn::launch_offset_conv_bwd(g, x, w_off, goff, grad_x, grad_w_off, grad_b_off, h->stream));
+  return DCN_OK;
+}
+
+// ---- host-pointer variants -----------------------------------------------------
+namespace {
+struct DevBufs {
+  std::vector<void*> ptrs;
+  ~DevBufs() {
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+  int alloc(size_t bytes, float** p) {
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, bytes ? bytes : 4);
+    if (e != hipSuccess) return fail(DCN_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+    ptrs.push_back(q);
+    *p = static_cast<float*>(q);
+    return DCN_OK;
+  }
+};
+
+int ensure_ws(dcn_handle* h, size_t bytes) {
+  if (h->ws_bytes >= bytes) return DCN_OK;
+  if (h->ws) HIP_TRY(hipFree(h->ws));
+  h->ws = nullptr;
+  h->ws_bytes = 0;
+  HIP_TRY(hipMalloc(&h->ws, bytes));
+  h->ws_bytes = bytes;
+  return DCN_OK;
+}
+
+int h2d(dcn_handle* h, float* dst, const float* src, size_t n) {
+  HIP_TRY(hipMemcpyAsync(dst, src, n * sizeof(float), hipMemcpyHostToDevice, h->stream));
+  return DCN_OK;
+}
+int d2h(dcn_handle* h, float* dst, const float* src, size_t n) {
+  HIP_TRY(hipMemcpyAsync(dst, src, n * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+  return DCN_OK;
+}
+}  // namespace
+
+int dcn_forward_host(dcn_handle* h, const dcn_desc* d, const float* x, const float* w_off,
+                     const float* b_off, const float* w, const float* b, float* out, float* off) {
+  Geo g;
+  DCN_TRY(make_geo(d, &g));
+  DCN_TRY(set_device(h));
+  const size_t nx = (size_t)g.B * g.C * g.HWi, nwo = (size_t)g.J * g.C * g.N, nw = (size_t)g.O * g.K;
+  const size_t nout = (size_t)g.B * g.O * g.HW, noff = (size_t)g.B * g.J * g.HW;
+  DevBufs db;
+  float *dx, *dwo, *dbo, *dw, *db_ = nullptr, *dout, *doff;
+  DCN_TRY(db.alloc(nx * 4, &dx));
+  DCN_TRY(db.alloc(nwo * 4, &dwo));
+  DCN_TRY(db.alloc((size_t)g.J * 4, &dbo));
+  DCN_TRY(db.alloc(nw * 4, &dw));
+  if (d->has_bias) DCN_TRY(db.alloc((size_t)g.O * 4, &db_));
+  DCN_TRY(db.alloc(nout * 4, &dout));
+  DCN_TRY(db.alloc(noff * 4, &doff));
+  DCN_TRY(h2d(h, dx, x, nx));
+  DCN_TRY(h2d(h, dwo, w_off, nwo));
+  DCN_TRY(h2d(h, dbo, b_off, g.J));
+  DCN_TRY(h2d(h, dw, w, nw));
+  if (d->has_bias) DCN_TRY(h2d(h, db_, b, g.O));
+  const size_t wsb = ws_layout(g, false).total;
+  DCN_TRY(ensure_ws(h, wsb));
+  DCN_TRY(dcn_forward(h, d, dx, dwo, dbo, dw, db_, dout, doff, h->ws, h->ws_bytes));
+  DCN_TRY(d2h(h, out, dout, nout));
+  if (off) DCN_TRY(d2h(h, off, doff, noff));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return DCN_OK;
+}
+
+int dcn_backward_host(dcn_handle* h, const dcn_desc* d, const float* x, const float* off,
+                      const float* w_off, const float* w, const float* grad_out, float* grad_x,
+                      float* grad_w, float* grad_b, float* grad_w_off, float* grad_b_off,
+                      float* grad_off_out) {
+  Geo g;
+  DCN_TRY(make_geo(d, &g));
+  DCN_TRY(set_device(h));
+  const size_t nx = (size_t)g.B * g.C * g.HWi, nwo = (size_t)g.J * g.C * g.N, nw = (size_t)g.O * g.K;
+  const size_t nout = (size_t)g.B * g.O * g.HW, noff = (size_t)g.B * g.J * g.HW;
+  DevBufs db;
+  float *dx, *doff, *dwo, *dw, *dgo, *dgx, *dgw, *dgb = nullptr, *dgwo, *dgbo, *dgoff;
+  DCN_TRY(db.alloc(nx * 4, &dx));
+  DCN_TRY(db.alloc(noff * 4, &doff));
+  DCN_TRY(db.alloc(nwo * 4, &dwo));
+  DCN_TRY(db.alloc(nw * 4, &dw));
+  DCN_TRY(db.alloc(nout * 4, &dgo));
+  DCN_TRY(db.alloc(nx * 4, &dgx));
+  DCN_TRY(db.alloc(nw * 4, &dgw));
+  if (d->has_bias) DCN_TRY(db.alloc((size_t)g.O * 4, &dgb));
+  DCN_TRY(db.alloc(nwo * 4, &dgwo));
+  DCN_TRY(db.alloc((size_t)g.J * 4, &dgbo));
+  DCN_TRY(db.alloc(noff * 4, &dgoff));
+  DCN_TRY(h2d(h, dx, x, nx));
+  DCN_TRY(h2d(h, doff, off, noff));
+  DCN_TRY(h2d(h, dwo, w_off, nwo));
+  DCN_TRY(h2d(h, dw, w, nw));
+  DCN_TRY(h2d(h, dgo, grad_out, nout));
+  const size_t wsb = ws_layout(g, true).total;
+  DCN_TRY(ensure_ws(h, wsb));
+  DCN_TRY(dcn_backward(h, d, dx, doff, dwo, dw, dgo, dgx, dgw, dgb, dgwo, dgbo, dgoff, h->ws,
+                       h->ws_bytes, 0));
+  DCN_TRY(d2h(h, grad_x, dgx, nx));
+  DCN_TRY(d2h(h, grad_w, dgw, nw));
+  if (d->has_bias) DCN_TRY(d2h(h, grad_b, dgb, g.O));
+  DCN_TRY(d2h(h, grad_w_off, dgwo, nwo));
+  DCN_TRY(d2h(h, grad_b_off, dgbo, g.J));
+  if (grad_off_out) DCN_TRY(d2h(h, grad_off_out, dgoff, noff));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return DCN_OK;
+}
+
+// ---- profiling ------------------------------------------------------------------
+int dcn_prof_enable(dcn_handle* h, int capacity) {
+  DCN_TRY(set_device(h));
+  if (capacity < 0) return fail(DCN_ERR_INVALID, "negative capacity");
+  for (int k = 0; k < DCN_K_COUNT; ++k) {
+    while ((int)h->ev[k].size() < 2 * capacity) {
+      hipEvent_t e;
+      HIP_TRY(hipEventCreate(&e));
+      h->ev[k].push_back(e);
+    }
+    h->prof_n[k] = 0;
+  }
+  h->prof_cap = capacity;
+  return DCN_OK;
+}
+
+int dcn_prof_read(dcn_handle* h, int kernel_id, double* total_ms, int* count) {
+  DCN_TRY(set_device(h));
+  if (kernel_id < 0 || kernel_id >= DCN_K_COUNT) return fail(DCN_ERR_INVALID, "bad kernel id");
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  double t = 0;
+  for (int i = 0; i < h->prof_n[kernel_id]; ++i) {
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, h->ev[kernel_id][2 * i], h->ev[kernel_id][2 * i + 1]));
+    t += ms;
+  }
+  if (total_ms) *total_ms = t;
+  if (count) *count = h->prof_n[kernel_id];
+  return DCN_OK;
+}
+
+int dcn_prof_reset(dcn_handle* h) {
+  if (!h) return fail(DCN_ERR_INVALID, "null handle");
+  for (int k = 0; k < DCN_K_COUNT; ++k) h->prof_n[k] = 0;
+  return DCN_OK;
+}
+
+// Test hook (not in dcn.h): force the generic global-memory im2col/col2im kernels.
+int dcn_debug_force_generic(int on) {
+  dcn::set_force_generic(on);
+  return DCN_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,210 @@
+"""ctypes binding of libdcn.so (include/dcn.h) — the product's only path to the GPU.
+
+The reference is a Jittor/NumPy code base (deform_conv.py, train.py), so the
+operator is exposed as a plain C-ABI shared library bound with ctypes; there is
+no torch extension and no CPU fallback: if the library or a HIP device is
+missing every compute call raises RuntimeError.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DCN_LIB", os.path.join(HERE, "lib", "libdcn.so"))
+
+DCN_F32, DCN_BF16 = 0, 1
+DCN_BWD_COL_IN_WS = 1
+KERNEL_IDS = {
+    "offset_fwd": 0, "im2col": 1, "gemm_fwd": 2, "bias_fwd": 3, "bwd_bias": 4,
+    "gemm_dw": 5, "gemm_dcol": 6, "col2im": 7, "offset_bwd": 8,
+}
+
+
+class Desc(ctypes.Structure):
+    """dcn_desc (include/dcn.h)."""
+    _fields_ = [(n, ctypes.c_int) for n in
+                ("B", "C", "H", "W", "O", "kh", "kw", "sh", "sw", "ph", "pw", "dil_h", "dil_w",
+                 "deform_groups", "dtype", "has_bias")]
+
+
+_vp = ctypes.c_void_p
+_ip = ctypes.POINTER(ctypes.c_int)
+_dp = ctypes.POINTER(Desc)
+_sz = ctypes.c_size_t
+
+# name -> argtypes (restype int unless listed in _RESTYPES). Mirrors include/dcn.h.
+SIGNATURES = {
+    "dcn_abi_version": [],
+    "dcn_last_error": [],
+    "dcn_device_count": [_ip],
+    "dcn_create": [ctypes.c_int, ctypes.POINTER(_vp)],
+    "dcn_destroy": [_vp],
+    "dcn_set_stream": [_vp, _vp],
+    "dcn_get_stream": [_vp, ctypes.POINTER(_vp)],
+    "dcn_synchronize": [_vp],
+    "dcn_malloc": [_vp, _sz, ctypes.POINTER(_vp)],
+    "dcn_free": [_vp, _vp],
+    "dcn_memcpy_h2d": [_vp, _vp, _vp, _sz],
+    "dcn_memcpy_d2h": [_vp, _vp, _vp, _sz],
+    "dcn_memset_zero": [_vp, _vp, _sz],
+    "dcn_out_shape": [_dp, _ip, _ip],
+    "dcn_workspace_bytes": [_dp, ctypes.c_int, ctypes.POINTER(_sz)],
+    "dcn_offset_conv_fwd": [_vp, _dp, _vp, _vp, _vp, _vp],
+    "dcn_offset_conv_bwd": [_vp, _dp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "dcn_im2col_fwd": [_vp, _dp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int],
+    "dcn_col2im_coord_bwd": [_vp, _dp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int],
+    "dcn_forward": [_vp, _dp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz],
+    "dcn_backward": [_vp, _dp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz,
+                     ctypes.c_int],
+    "dcn_forward_host": [_vp, _dp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "dcn_backward_host": [_vp, _dp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "dcn_prof_enable": [_vp, ctypes.c_int],
+    "dcn_prof_read": [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), _ip],
+    "dcn_prof_reset": [_vp],
+    "dcn_debug_force_generic": [ctypes.c_int],
+}
+_RESTYPES = {"dcn_last_error": ctypes.c_char_p}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str | None = None):
+    """Load libdcn.so and declare every prototype. Raises if it is missing."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise RuntimeError(f"libdcn.so not found at {p}: build it with "
+                               f"`python -c 'import __graft_entry__ as g; g.build()'` "
+                               f"(no CPU fallback exists)")
+        L = ctypes.CDLL(p)
+        for name, args in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
+        if L.dcn_abi_version() != 1:
+            raise RuntimeError("libdcn ABI version mismatch")
+        if path is None:
+            _lib = L
+        return L
+
+
+def last_error() -> str:
+    msg = load().dcn_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str = "libdcn"):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed (status {rc}): {last_error()}")
+
+
+def make_desc(B, C, H, W, O, kernel_size, stride, padding, dilation=(1, 1), deform_groups=1,
+              bias=True, dtype=DCN_F32) -> Desc:
+    return Desc(B, C, H, W, O, kernel_size[0], kernel_size[1], stride[0], stride[1], padding[0],
+                padding[1], dilation[0], dilation[1], deform_groups, dtype, int(bool(bias)))
+
+
+def out_shape(desc: Desc):
+    ho, wo = ctypes.c_int(), ctypes.c_int()
+    check(load().dcn_out_shape(ctypes.byref(desc), ctypes.byref(ho), ctypes.byref(wo)),
+          "dcn_out_shape")
+    return ho.value, wo.value
+
+
+def workspace_bytes(desc: Desc, with_backward: bool) -> int:
+    n = ctypes.c_size_t()
+    check(load().dcn_workspace_bytes(ctypes.byref(desc), int(with_backward), ctypes.byref(n)),
+          "dcn_workspace_bytes")
+    return n.value
+
+
+def device_count() -> int:
+    n = ctypes.c_int()
+    rc = load().dcn_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0
+
+
+class Handle:
+    """One dcn_handle (device + stream + rocBLAS handle). Not thread-safe."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        h = ctypes.c_void_p()
+        check(self.lib.dcn_create(int(device), ctypes.byref(h)), "dcn_create")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.dcn_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- streams / memory -----------------------------------------------------
+    def set_stream(self, stream_ptr: int | None):
+        check(self.lib.dcn_set_stream(self.h, ctypes.c_void_p(stream_ptr or 0)), "dcn_set_stream")
+
+    def synchronize(self):
+        check(self.lib.dcn_synchronize(self.h), "dcn_synchronize")
+
+    def malloc(self, nbytes: int) -> int:
+        p = ctypes.c_void_p()
+        check(self.lib.dcn_malloc(self.h, nbytes, ctypes.byref(p)), "dcn_malloc")
+        return p.value
+
+    def free(self, ptr: int):
+        check(self.lib.dcn_free(self.h, ctypes.c_void_p(ptr)), "dcn_free")
+
+    def h2d(self, dst: int, arr):
+        check(self.lib.dcn_memcpy_h2d(self.h, ctypes.c_void_p(dst), arr.ctypes.data_as(_vp),
+                                      arr.nbytes), "dcn_memcpy_h2d")
+
+    def d2h(self, arr, src: int):
+        check(self.lib.dcn_memcpy_d2h(self.h, arr.ctypes.data_as(_vp), ctypes.c_void_p(src),
+                                      arr.nbytes), "dcn_memcpy_d2h")
+
+    # --- profiling -------------------------------------------------------------
+    def prof_enable(self, capacity: int):
+        check(self.lib.dcn_prof_enable(self.h, int(capacity)), "dcn_prof_enable")
+
+    def prof_read(self, kernel: str):
+        t, n = ctypes.c_double(), ctypes.c_int()
+        check(self.lib.dcn_prof_read(self.h, KERNEL_IDS[kernel], ctypes.byref(t), ctypes.byref(n)),
+              "dcn_prof_read")
+        return t.value, n.value
+
+    def prof_reset(self):
+        check(self.lib.dcn_prof_reset(self.h), "dcn_prof_reset")
+
+
+def ptr(a):
+    """Host pointer of a C-contiguous float32 numpy array (None -> NULL)."""
+    if a is None:
+        return None
+    if a.dtype.name != "float32" or not a.flags.c_contiguous:
+        raise TypeError("libdcn expects C-contiguous float32 arrays")
+    return a.ctypes.data_as(_vp)
+
+
+_default = {}
+
+
+def default_handle(device: int | None = None) -> Handle:
+    """Process-wide handle per device (DCN_DEVICE env var selects the default)."""
+    dev = int(os.environ.get("DCN_DEVICE", "0")) if device is None else int(device)
+    key = (threading.get_ident(), dev)
+    h = _default.get(key)
+    if h is None:
+        h = _default[key] = Handle(dev)
+    return h

@@ -1,0 +1,265 @@
+"""Drop-in replacement for the reference's `deform_conv.DeformConv2d`.
+
+Callers keep their import line unchanged (train.py:299, test.py:12):
+
+    import sys; sys.path.insert(0, "<repo>/jittor-dcn_amd")
+    from deform_conv import DeformConv2d
+    conv = DeformConv2d(16, 32, 3, 2, 1)          # train.py:311
+
+Surface kept from /root/reference/deform_conv.py:6-81:
+  * constructor (in_channels, out_channels, kernel_size=3, stride=1, padding=1,
+    bias=True) (:7); kernel_size/stride/padding normalised to tuples (:11-13);
+  * attributes in_channels, out_channels, kernel_size, stride, padding, N (:9-14);
+  * parameters offset_conv.weight [2N, C, kh, kw], offset_conv.bias [2N] (zero
+    init, :16-21, :27-28), weight [O, C, kh, kw] ~ N(0, sqrt(2/(C*kh*kw))) (:23-24),
+    bias [O] zero or None (:25) — so state-dict keys round-trip (train.py:461,
+    test.py:19);
+  * execute(x) -> [B, O, H_out, W_out] (:56-81), reached through __call__.
+
+Compute: every call goes to libdcn.so (hand-written gfx950 HIP kernels + rocBLAS)
+through ctypes (dcn_runtime.py). There is no CPU fallback: without the library
+or a HIP device, execute() raises RuntimeError.
+
+Backends:
+  * Jittor importable  -> a jt.nn.Module whose execute() is a jt.Function, so the
+    gradients reach Jittor autodiff / optimizer.backward (train.py:414).
+  * otherwise          -> a NumPy module: execute(x) returns a NumPy array and
+    backward(grad_out) fills `.grad` on the four parameters and returns ∂x.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+import dcn_runtime as rt
+
+try:  # pragma: no cover - Jittor is not installable in the build image
+    import jittor as jt
+    from jittor import nn as jnn
+    HAVE_JITTOR = True
+except Exception:  # ImportError or a broken jittor install
+    jt = None
+    HAVE_JITTOR = False
+
+
+def _pair(v):
+    return v if isinstance(v, tuple) else (v, v)
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def dcn_forward_numpy(x, w_off, b_off, w, b, stride, padding, handle=None):
+    """out, off = DeformConv2d.execute on host arrays (one libdcn call)."""
+    h = handle or rt.default_handle()
+    x, w_off, b_off, w = _f32(x), _f32(w_off), _f32(b_off), _f32(w)
+    b = None if b is None else _f32(b)
+    B, C, H, W = x.shape
+    O, Cw, kh, kw = w.shape
+    if Cw != C:
+        raise ValueError(f"input has {C} channels, weight expects {Cw}")
+    desc = rt.make_desc(B, C, H, W, O, (kh, kw), stride, padding, bias=b is not None)
+    Ho, Wo = rt.out_shape(desc)
+    out = np.empty((B, O, Ho, Wo), np.float32)
+    off = np.empty((B, w_off.shape[0], Ho, Wo), np.float32)
+    rt.check(h.lib.dcn_forward_host(h.h, desc, rt.ptr(x), rt.ptr(w_off), rt.ptr(b_off), rt.ptr(w),
+                                    rt.ptr(b), rt.ptr(out), rt.ptr(off)), "dcn_forward_host")
+    return out, off
+
+
+def dcn_backward_numpy(x, off, w_off, w, has_bias, grad_out, stride, padding, handle=None):
+    """Grads of DeformConv2d.execute (dict keyed like the state dict, plus 'x', 'offset')."""
+    h = handle or rt.default_handle()
+    x, off, w_off, w, grad_out = map(_f32, (x, off, w_off, w, grad_out))
+    B, C, H, W = x.shape
+    O, _, kh, kw = w.shape
+    desc = rt.make_desc(B, C, H, W, O, (kh, kw), stride, padding, bias=has_bias)
+    g = {"x": np.empty_like(x), "weight": np.empty_like(w),
+         "offset_conv.weight": np.empty_like(w_off),
+         "offset_conv.bias": np.empty(w_off.shape[0], np.float32), "offset": np.empty_like(off)}
+    gb = np.empty(O, np.float32) if has_bias else None
+    rt.check(h.lib.dcn_backward_host(h.h, desc, rt.ptr(x), rt.ptr(off), rt.ptr(w_off), rt.ptr(w),
+                                     rt.ptr(grad_out), rt.ptr(g["x"]), rt.ptr(g["weight"]),
+                                     rt.ptr(gb), rt.ptr(g["offset_conv.weight"]),
+                                     rt.ptr(g["offset_conv.bias"]), rt.ptr(g["offset"])),
+             "dcn_backward_host")
+    if has_bias:
+        g["bias"] = gb
+    return g
+
+
+# ---------------------------------------------------------------------------
+# NumPy backend
+# ---------------------------------------------------------------------------
+class Parameter(np.ndarray):
+    """float32 ndarray with a `.grad` slot (what Adam in train.py:350 iterates)."""
+
+    def __new__(cls, data):
+        obj = np.ascontiguousarray(data, dtype=np.float32).view(cls)
+        obj.grad = None
+        return obj
+
+    def __array_finalize__(self, obj):
+        self.grad = getattr(obj, "grad", None)
+
+
+class Module:
+    """Minimal module protocol: parameters / state_dict / load_state_dict / __call__."""
+
+    def __init__(self):
+        self.training = True
+
+    def _children(self):
+        return [(k, v) for k, v in vars(self).items() if isinstance(v, Module)]
+
+    def named_parameters(self, prefix=""):
+        for k, v in vars(self).items():
+            if isinstance(v, Parameter):
+                yield prefix + k, v
+        for k, m in self._children():
+            yield from m.named_parameters(prefix + k + ".")
+
+    def parameters(self):
+        return [p for _, p in self.named_parameters()]
+
+    def state_dict(self):
+        return {k: np.array(v) for k, v in self.named_parameters()}
+
+    def load_state_dict(self, sd):
+        for k, v in sd.items():
+            obj, *path = [self] + k.split(".")
+            for part in path[:-1]:
+                obj = getattr(obj, part)
+            cur = getattr(obj, path[-1])
+            v = np.asarray(v, np.float32)
+            if cur is not None and tuple(cur.shape) != tuple(v.shape):
+                raise ValueError(f"shape mismatch for {k}: {cur.shape} vs {v.shape}")
+            setattr(obj, path[-1], Parameter(v))
+
+    def load(self, path):
+        """Like jt.Module.load (test.py:19) for .npz state dicts."""
+        with np.load(path, allow_pickle=False) as z:
+            self.load_state_dict({k: z[k] for k in z.files})
+
+    def save(self, path):
+        np.savez(path, **self.state_dict())
+
+    def zero_grad(self):
+        for p in self.parameters():
+            p.grad = None
+
+    def train(self):
+        self.training = True
+
+    def eval(self):
+        self.training = False
+
+    def __call__(self, *a, **k):
+        return self.execute(*a, **k)
+
+
+class Conv(Module):
+    """Parameter holder for `offset_conv` (nn.Conv in deform_conv.py:16-21). Its
+    math runs fused inside libdcn (dcn_forward); it is never executed alone."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride, padding):
+        super().__init__()
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.kernel_size, self.stride, self.padding = kernel_size, stride, padding
+        self.weight = Parameter(np.zeros((out_channels, in_channels, *kernel_size), np.float32))
+        self.bias = Parameter(np.zeros(out_channels, np.float32))
+
+
+class DeformConv2dNumpy(Module):
+    """DeformConv2d (deform_conv.py:6-81) over NumPy arrays, computed by libdcn."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=3, stride=1, padding=1, bias=True,
+                 seed=None):
+        super().__init__()
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.kernel_size = _pair(kernel_size)
+        self.stride = _pair(stride)
+        self.padding = _pair(padding)
+        self.N = self.kernel_size[0] * self.kernel_size[1]
+        self.offset_conv = Conv(in_channels, 2 * self.N, self.kernel_size, self.stride, self.padding)
+        std = math.sqrt(2.0 / (in_channels * self.kernel_size[0] * self.kernel_size[1]))
+        rng = np.random.default_rng(seed)
+        self.weight = Parameter(rng.normal(0.0, std, (out_channels, in_channels, *self.kernel_size)))
+        self.bias = Parameter(np.zeros(out_channels, np.float32)) if bias else None
+        self._ctx = None
+
+    def execute(self, x):
+        x = _f32(x)
+        out, off = dcn_forward_numpy(x, self.offset_conv.weight, self.offset_conv.bias,
+                                     self.weight, self.bias, self.stride, self.padding)
+        self._ctx = (x, off) if self.training else None
+        return out
+
+    def backward(self, grad_out):
+        """Accumulate parameter grads (.grad) and return ∂L/∂x."""
+        if self._ctx is None:
+            raise RuntimeError("backward() needs a preceding execute() in training mode")
+        x, off = self._ctx
+        g = dcn_backward_numpy(x, off, self.offset_conv.weight, self.weight, self.bias is not None,
+                               grad_out, self.stride, self.padding)
+        for name, p in self.named_parameters():
+            p.grad = g[name] if p.grad is None else p.grad + g[name]
+        return g["x"]
+
+
+# ---------------------------------------------------------------------------
+# Jittor backend (exercised only where jittor imports; not in the build image)
+# ---------------------------------------------------------------------------
+if HAVE_JITTOR:  # pragma: no cover
+
+    class _DCNFunction(jt.Function):
+        """jt.Function whose execute/grad call libdcn; inputs are the module's Vars so
+        Jittor autodiff routes gradients to offset_conv.{weight,bias}, weight, bias."""
+
+        def execute(self, x, w_off, b_off, w, b, stride, padding):
+            self.stride, self.padding = stride, padding
+            self.has_bias = b is not None
+            xn, won, wn = x.numpy(), w_off.numpy(), w.numpy()
+            out, off = dcn_forward_numpy(xn, won, b_off.numpy(), wn,
+                                         None if b is None else b.numpy(), stride, padding)
+            self.saved = (xn, off, won, wn)
+            return jt.array(out)
+
+        def grad(self, grad_out):
+            xn, off, won, wn = self.saved
+            g = dcn_backward_numpy(xn, off, won, wn, self.has_bias, grad_out.numpy(),
+                                   self.stride, self.padding)
+            gb = jt.array(g["bias"]) if self.has_bias else None
+            return (jt.array(g["x"]), jt.array(g["offset_conv.weight"]),
+                    jt.array(g["offset_conv.bias"]), jt.array(g["weight"]), gb, None, None)
+
+    class DeformConv2d(jnn.Module):
+        def __init__(self, in_channels, out_channels, kernel_size=3, stride=1, padding=1,
+                     bias=True):
+            super().__init__()
+            self.in_channels = in_channels
+            self.out_channels = out_channels
+            self.kernel_size = _pair(kernel_size)
+            self.stride = _pair(stride)
+            self.padding = _pair(padding)
+            self.N = self.kernel_size[0] * self.kernel_size[1]
+            self.offset_conv = jnn.Conv(in_channels, 2 * self.N, kernel_size=self.kernel_size,
+                                        stride=self.stride, padding=self.padding)
+            std = math.sqrt(2.0 / (in_channels * self.kernel_size[0] * self.kernel_size[1]))
+            self.weight = jt.init.gauss([out_channels, in_channels, *self.kernel_size], mean=0.0,
+                                        std=std)
+            self.bias = jt.init.constant(shape=[out_channels], value=0.0) if bias else None
+            self.offset_conv.weight = jt.zeros_like(self.offset_conv.weight)
+            self.offset_conv.bias = jt.zeros_like(self.offset_conv.bias)
+
+        def execute(self, x):
+            return _DCNFunction.apply(x, self.offset_conv.weight, self.offset_conv.bias,
+                                      self.weight, self.bias, self.stride, self.padding)
+else:
+    DeformConv2d = DeformConv2dNumpy
+
+__all__ = ["DeformConv2d", "DeformConv2dNumpy", "dcn_forward_numpy", "dcn_backward_numpy",
+           "HAVE_JITTOR"]

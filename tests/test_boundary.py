@@ -1,0 +1,90 @@
+"""CPU: the C-ABI boundary — libdcn.so loads, exports every symbol include/dcn.h
+declares, the ctypes prototypes cover the header, and the shape/validation
+entry points behave without a device. No compute calls (no GPU here)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import dcn_runtime as rt
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "dcn.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(dcn_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_library_exists_and_loads():
+    assert os.path.exists(rt.LIB_PATH), "build libdcn.so first (__graft_entry__.build())"
+    rt.load()
+
+
+def test_every_header_symbol_is_exported():
+    funcs = header_functions()
+    assert len(funcs) >= 25
+    out = subprocess.run(["nm", "-D", "--defined-only", rt.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (dcn_\w+)", out))
+    missing = [f for f in funcs if f not in exported]
+    assert not missing, f"declared in dcn.h but not exported: {missing}"
+
+
+def test_ctypes_prototypes_cover_header():
+    funcs = header_functions()
+    assert sorted(rt.SIGNATURES) == funcs
+
+
+def test_library_links_no_torch():
+    out = subprocess.run(["ldd", rt.LIB_PATH], capture_output=True, text=True).stdout
+    assert "torch" not in out and "libc10" not in out
+    assert "librocblas" in out and "libamdhip64" in out
+
+
+def test_desc_layout_matches_header():
+    # dcn_desc = 16 ints
+    assert ctypes.sizeof(rt.Desc) == 16 * 4
+
+
+def desc(**kw):
+    base = dict(B=2, C=4, H=9, W=11, O=3, kernel_size=(3, 3), stride=(1, 1), padding=(1, 1))
+    base.update(kw)
+    return rt.make_desc(**base)
+
+
+def test_out_shape_and_workspace():
+    assert rt.out_shape(desc()) == (9, 11)
+    assert rt.out_shape(desc(stride=(2, 2))) == (5, 6)
+    assert rt.out_shape(desc(H=14, W=14, stride=(2, 2), dilation=(2, 2))) == (6, 6)
+    d = desc()
+    fwd = rt.workspace_bytes(d, False)
+    bwd = rt.workspace_bytes(d, True)
+    K, HW = 9 * 4, 9 * 11
+    assert fwd >= 2 * K * HW * 4
+    assert bwd > fwd
+
+
+@pytest.mark.parametrize("bad,msg", [
+    (dict(B=0), "positive"),
+    (dict(stride=(0, 1)), "positive"),
+    (dict(H=2, W=2, padding=(0, 0)), "empty output"),
+    (dict(H=3, W=8, padding=(0, 1)), "divides"),        # H_out == 1 (deform_conv.py:38)
+    (dict(deform_groups=3), "divisible"),
+    (dict(dtype=rt.DCN_BF16), "only DCN_F32"),
+])
+def test_invalid_descriptors_are_rejected(bad, msg):
+    with pytest.raises(RuntimeError, match=msg):
+        rt.out_shape(desc(**bad))
+
+
+def test_no_device_fails_loudly():
+    if rt.device_count() > 0:
+        pytest.skip("a HIP device is visible")
+    with pytest.raises(RuntimeError, match="dcn_create"):
+        rt.Handle(0)
+    assert rt.last_error() != ""

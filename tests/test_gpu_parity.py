@@ -1,0 +1,258 @@
+"""GPU parity: libdcn (HIP kernels on gfx950 + rocBLAS) vs the oracles, through the C-ABI.
+
+Tolerance (north star): fp32 results within |Δ| <= 1e-4 + 1e-4·|ref| of the
+reference restatement; M-reductions (∂W, ∂b, ∂W_off, ∂b_off) within
+max|Δ|/max|ref| <= 1e-4. Everything here runs on the HIP device (no fallback).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import dcn_oracle as O
+import dcn_runtime as rt
+import ref_lib as R
+from conftest import assert_close, assert_close_reduction, golden_names, load_golden
+from deform_conv import DeformConv2dNumpy, dcn_backward_numpy, dcn_forward_numpy
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(out, off, g, ref_out, ref_off, ref_g, has_bias, what):
+    assert_close(out, ref_out, what=f"{what} out")
+    assert_close(off, ref_off, what=f"{what} offset")
+    assert_close(g["x"], ref_g["x"], what=f"{what} ∂x")
+    assert_close(g["offset"], ref_g["offset"], what=f"{what} ∂offset")
+    for k in ("weight", "offset_conv.weight", "offset_conv.bias") + (("bias",) if has_bias else ()):
+        assert_close_reduction(g[k], ref_g[k], what=f"{what} ∂{k}")
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_host_api_vs_golden(gpu_handle, name):
+    d = load_golden(name)
+    out, off = dcn_forward_numpy(d["x"], d["w_off"], d["b_off"], d["w"], d["b"], d["stride"],
+                                 d["padding"], handle=gpu_handle)
+    g = dcn_backward_numpy(d["x"], off, d["w_off"], d["w"], d["b"] is not None, d["grad_out"],
+                           d["stride"], d["padding"], handle=gpu_handle)
+    ref_g = {"x": d["f32_grad_x"], "offset": d["f32_grad_offset"], "weight": d["f32_grad_weight"],
+             "offset_conv.weight": d["f32_grad_offset_weight"],
+             "offset_conv.bias": d["f32_grad_offset_bias"]}
+    if d["b"] is not None:
+        ref_g["bias"] = d["f32_grad_bias"]
+    _check(out, off, g, d["f32_out"], d["f32_off"], ref_g, d["b"] is not None, name)
+
+
+def _rand_case(seed, B, C, O_, H, W, k=(3, 3), s=(1, 1), p=(1, 1), dil=(1, 1), G=1, off_scale=1.0,
+               bias_scale=0.5, bias=True):
+    rng = np.random.default_rng(seed)
+    N = k[0] * k[1]
+    x = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    # offsets ~ N(0, off_scale) px (SURVEY §8(d) synthetic inputs)
+    wo = (rng.standard_normal((2 * N * G, C, *k)) * off_scale / np.sqrt(C * N)).astype(np.float32)
+    bo = rng.uniform(-bias_scale, bias_scale, 2 * N * G).astype(np.float32)
+    w = (rng.standard_normal((O_, C, *k)) * np.sqrt(2 / (C * N))).astype(np.float32)
+    b = (rng.standard_normal(O_) * 0.1).astype(np.float32) if bias else None
+    Ho, Wo = O.out_size(H, W, *k, *s, *p, *dil)
+    gout = rng.standard_normal((B, O_, Ho, Wo)).astype(np.float32)
+    return dict(x=x, w_off=wo, b_off=bo, w=w, b=b, grad_out=gout, stride=s, padding=p, dil=dil, G=G)
+
+
+class Dev:
+    """Device buffers through the C-ABI memory helpers (no other GPU runtime)."""
+
+    def __init__(self, h):
+        self.h, self.ptrs = h, []
+
+    def up(self, a):
+        a = np.ascontiguousarray(a, np.float32)
+        p = self.h.malloc(a.nbytes)
+        self.h.h2d(p, a)
+        self.ptrs.append(p)
+        return p
+
+    def zeros(self, nbytes):
+        p = self.h.malloc(nbytes)
+        rt.check(self.h.lib.dcn_memset_zero(self.h.h, ctypes.c_void_p(p), nbytes))
+        self.ptrs.append(p)
+        return p
+
+    def down(self, p, shape):
+        a = np.empty(shape, np.float32)
+        self.h.synchronize()
+        self.h.d2h(a, p)
+        return a
+
+    def free(self):
+        for p in self.ptrs:
+            self.h.free(p)
+        self.ptrs = []
+
+
+def _device_fwd_bwd(h, c):
+    """dcn_forward + dcn_backward on device buffers, columns reused (DCN_BWD_COL_IN_WS)."""
+    x, wo, bo, w, b, gout = c["x"], c["w_off"], c["b_off"], c["w"], c["b"], c["grad_out"]
+    B, C, H, W = x.shape
+    O_, _, kh, kw = w.shape
+    desc = rt.make_desc(B, C, H, W, O_, (kh, kw), c["stride"], c["padding"], c["dil"], c["G"],
+                        bias=b is not None)
+    Ho, Wo = rt.out_shape(desc)
+    J = wo.shape[0]
+    D = Dev(h)
+    try:
+        px, pwo, pbo, pw = D.up(x), D.up(wo), D.up(bo), D.up(w)
+        pb = D.up(b) if b is not None else None
+        pout, poff = D.zeros(B * O_ * Ho * Wo * 4), D.zeros(B * J * Ho * Wo * 4)
+        wsb = rt.workspace_bytes(desc, True)
+        ws = D.zeros(wsb)
+        vp = ctypes.c_void_p
+        rt.check(h.lib.dcn_forward(h.h, desc, vp(px), vp(pwo), vp(pbo), vp(pw), vp(pb), vp(pout),
+                                   vp(poff), vp(ws), wsb), "dcn_forward")
+        pgo = D.up(gout)
+        pgx, pgw = D.zeros(x.nbytes), D.zeros(w.nbytes)
+        pgb = D.zeros(O_ * 4) if b is not None else None
+        pgwo, pgbo, pgoff = D.zeros(wo.nbytes), D.zeros(J * 4), D.zeros(B * J * Ho * Wo * 4)
+        rt.check(h.lib.dcn_backward(h.h, desc, vp(px), vp(poff), vp(pwo), vp(pw), vp(pgo), vp(pgx),
+                                    vp(pgw), vp(pgb), vp(pgwo), vp(pgbo), vp(pgoff), vp(ws), wsb,
+                                    rt.DCN_BWD_COL_IN_WS), "dcn_backward")
+        out, off = D.down(pout, (B, O_, Ho, Wo)), D.down(poff, (B, J, Ho, Wo))
+        g = {"x": D.down(pgx, x.shape), "weight": D.down(pgw, w.shape),
+             "offset_conv.weight": D.down(pgwo, wo.shape), "offset_conv.bias": D.down(pgbo, (J,)),
+             "offset": D.down(pgoff, (B, J, Ho, Wo))}
+        if b is not None:
+            g["bias"] = D.down(pgb, (O_,))
+        return out, off, g
+    finally:
+        D.free()
+
+
+def _oracle(c):
+    out, off, cache = O.forward(c["x"], c["w_off"], c["b_off"], c["w"], c["b"], c["stride"],
+                                c["padding"], c["dil"], c["G"])
+    return out, off, O.backward(cache, c["grad_out"])
+
+
+@pytest.mark.parametrize("case", [
+    dict(seed=1, B=2, C=32, O_=24, H=28, W=28),
+    dict(seed=2, B=3, C=16, O_=16, H=20, W=17, s=(2, 2)),
+    dict(seed=3, B=1, C=40, O_=8, H=33, W=35, off_scale=3.0, bias_scale=2.0),
+    dict(seed=4, B=2, C=8, O_=8, H=64, W=64, s=(2, 2)),           # EDNet conv2 geometry
+    dict(seed=5, B=2, C=12, O_=6, H=10, W=12, k=(1, 1), p=(0, 0)),
+    dict(seed=6, B=2, C=12, O_=6, H=11, W=12, k=(3, 2), s=(1, 2), p=(1, 0), bias=False),
+])
+def test_device_api_vs_oracle(gpu_handle, case):
+    c = _rand_case(**case)
+    out, off, g = _device_fwd_bwd(gpu_handle, c)
+    ro, roff, rg = _oracle(c)
+    _check(out, off, g, ro, roff, rg, c["b"] is not None, str(case))
+
+
+@pytest.mark.parametrize("dil,G", [((2, 2), 1), ((1, 1), 4), ((2, 2), 4)])
+def test_extension_dilation_groups_vs_oracle(gpu_handle, dil, G):
+    """Config-5 option set (parity unpinned: checked against our own restatement)."""
+    c = _rand_case(21, B=2, C=16, O_=12, H=14, W=14, s=(2, 2), p=(1, 1), dil=dil, G=G)
+    out, off, g = _device_fwd_bwd(gpu_handle, c)
+    ro, roff, rg = _oracle(c)
+    _check(out, off, g, ro, roff, rg, True, f"dil={dil} G={G}")
+
+
+def test_pathological_offsets_window_fallback(gpu_handle):
+    """Offsets of tens of pixels blow the LDS window: the kernels fall back to L2 gathers."""
+    c = _rand_case(31, B=2, C=8, O_=8, H=40, W=40, off_scale=40.0, bias_scale=30.0)
+    out, off, g = _device_fwd_bwd(gpu_handle, c)
+    ro, roff, rg = _oracle(c)
+    _check(out, off, g, ro, roff, rg, True, "huge offsets")
+
+
+def test_all_samples_out_of_image(gpu_handle):
+    """Every sample lands outside the image: out == bias, sampling grads vanish."""
+    c = _rand_case(41, B=2, C=4, O_=3, H=12, W=12, off_scale=0.0, bias_scale=0.0)
+    c["b_off"][:] = 500.0
+    out, off, g = _device_fwd_bwd(gpu_handle, c)
+    np.testing.assert_allclose(out, np.broadcast_to(c["b"][None, :, None, None], out.shape))
+    assert not np.any(g["offset"]) and not np.any(g["weight"])
+    ro, roff, rg = _oracle(c)
+    _check(out, off, g, ro, roff, rg, True, "all OOB")
+
+
+def test_window_kernels_match_generic_kernels(gpu_handle):
+    """The LDS-window K1/K5 and the independent global-gather kernels agree: columns and
+    ∂offset bit for bit (same fp32 op order), ∂x to rounding (atomic order)."""
+    h = gpu_handle
+    c = _rand_case(51, B=3, C=24, O_=4, H=30, W=26, s=(1, 1), off_scale=2.0)
+    x, wo, bo = c["x"], c["w_off"], c["b_off"]
+    B, C, H, W = x.shape
+    desc = rt.make_desc(B, C, H, W, 4, (3, 3), (1, 1), (1, 1))
+    Ho, Wo = rt.out_shape(desc)
+    K, HW = 9 * C, Ho * Wo
+    rng = np.random.default_rng(5)
+    gcol = rng.standard_normal((B, K, HW)).astype(np.float32)
+    vp = ctypes.c_void_p
+    res = {}
+    for generic in (0, 1):
+        D = Dev(h)
+        try:
+            px, pwo, pbo = D.up(x), D.up(wo), D.up(bo)
+            poff = D.zeros(B * 18 * HW * 4)
+            rt.check(h.lib.dcn_offset_conv_fwd(h.h, desc, vp(px), vp(pwo), vp(pbo), vp(poff)))
+            pcol = D.zeros(B * K * HW * 4)
+            rt.check(h.lib.dcn_debug_force_generic(generic))
+            rt.check(h.lib.dcn_im2col_fwd(h.h, desc, vp(px), vp(poff), vp(pcol), 0, B))
+            pg = D.up(gcol)
+            pgx, pgoff = D.zeros(x.nbytes), D.zeros(B * 18 * HW * 4)
+            rt.check(h.lib.dcn_col2im_coord_bwd(h.h, desc, vp(px), vp(poff), vp(pg), vp(pgx),
+                                                vp(pgoff), 0, B))
+            res[generic] = (D.down(pcol, (B, K, HW)), D.down(pgx, x.shape),
+                            D.down(pgoff, (B, 18, Ho, Wo)), D.down(poff, (B, 18, Ho, Wo)))
+        finally:
+            rt.check(h.lib.dcn_debug_force_generic(0))
+            D.free()
+    col_w, gx_w, goff_w, off_w = res[0]
+    col_g, gx_g, goff_g, _ = res[1]
+    np.testing.assert_array_equal(col_w, col_g)
+    np.testing.assert_array_equal(goff_w, goff_g)
+    np.testing.assert_allclose(gx_w, gx_g, rtol=1e-5, atol=1e-5)
+    # and both equal the oracle's column block
+    assert_close(col_w, O.im2col(x, off_w, 3, 3), what="im2col vs oracle")
+
+
+def test_module_numpy_backend_on_gpu():
+    d = load_golden("nonsquare_stride2")
+    m = DeformConv2dNumpy(d["x"].shape[1], d["w"].shape[0], 3, 2, 1)
+    m.load_state_dict({"weight": d["w"], "bias": d["b"], "offset_conv.weight": d["w_off"],
+                       "offset_conv.bias": d["b_off"]})
+    out = m(d["x"])
+    assert_close(out, d["f32_out"], what="module out")
+    gx = m.backward(d["grad_out"])
+    assert_close(gx, d["f32_grad_x"], what="module ∂x")
+    assert_close_reduction(m.weight.grad, d["f32_grad_weight"], what="module ∂W")
+    assert_close_reduction(m.offset_conv.weight.grad, d["f32_grad_offset_weight"],
+                           what="module ∂W_off")
+    m.eval()
+    out2 = m(d["x"])  # no_grad-style forward (train.py:430)
+    np.testing.assert_array_equal(out, out2)
+
+
+def test_config3_full_size_properties(gpu_handle):
+    """BASELINE config 3 (B=64, C=O=256, 56², k3 s1 p1) at full size: spot-check two
+    images' per-image outputs/grads against the C oracle (fp32) and ∂W by linearity
+    (batch = sum of its two halves computed separately)."""
+    h = gpu_handle
+    c = _rand_case(61, B=64, C=256, O_=256, H=56, W=56)
+    out, off, g = _device_fwd_bwd(h, c)
+    assert np.isfinite(out).all() and np.isfinite(g["x"]).all()
+    for bi in (0, 63):
+        sub = {k: (v[bi:bi + 1] if k in ("x", "grad_out") else v) for k, v in c.items()}
+        desc = R.make_desc(sub["x"].shape, c["w"].shape, (1, 1), (1, 1))
+        ro, roff = R.forward(desc, sub["x"], c["w_off"], c["b_off"], c["w"], c["b"])
+        rg = R.backward(desc, sub["x"], roff, c["w_off"], c["w"], sub["grad_out"])
+        assert_close(out[bi:bi + 1], ro, what=f"img{bi} out")
+        assert_close(off[bi:bi + 1], roff, what=f"img{bi} offset")
+        assert_close(g["x"][bi:bi + 1], rg["x"], what=f"img{bi} ∂x")
+        assert_close(g["offset"][bi:bi + 1], rg["offset"], what=f"img{bi} ∂offset")
+    halves = []
+    for lo, hi in ((0, 32), (32, 64)):
+        sub = dict(c)
+        sub["x"], sub["grad_out"] = c["x"][lo:hi], c["grad_out"][lo:hi]
+        halves.append(_device_fwd_bwd(h, sub)[2])
+    for k in ("weight", "bias", "offset_conv.weight", "offset_conv.bias"):
+        assert_close_reduction(g[k], halves[0][k] + halves[1][k], tol=2e-5, what=f"linearity ∂{k}")
