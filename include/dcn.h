@@ -99,12 +99,13 @@ int dcn_offset_conv_bwd(dcn_handle* h, const dcn_desc* d, const float* x,
                         const float* w_off, const float* grad_off,
                         float* grad_x, float* grad_w_off, float* grad_b_off);
 /* Deformable bilinear im2col (K1): replaces deform_conv.py:30-54 and :62-73
- * (grid build, normalisation, x_repeat, grid_sample, permutes).
- * col[b][n·C + c][ho·Wo + wo] for images b in [b0, b0+nb). */
+ * (grid build, normalisation, x_repeat, grid_sample, permutes). Writes the
+ * sampled matrix of deform_conv.py:73 row by row, channels-last:
+ * col[b - b0][ho·Wo + wo][n·C + c] for images b in [b0, b0+nb). */
 int dcn_im2col_fwd(dcn_handle* h, const dcn_desc* d, const float* x,
                    const float* off, float* col, int b0, int nb);
-/* Backward of K1 (K5): grad_x += Σ scatter(grad_col) (accumulated, atomics);
- * grad_off[b][..][ho][wo] = coordinate gradient (overwritten), for images
+/* Backward of K1 (K5): grad_x = Σ scatter(grad_col) (sampling route only) and
+ * grad_off[b][..][ho][wo] = coordinate gradient, both OVERWRITTEN for images
  * [b0, b0+nb). grad_col has the layout of dcn_im2col_fwd's col. */
 int dcn_col2im_coord_bwd(dcn_handle* h, const dcn_desc* d, const float* x,
                          const float* off, const float* grad_col,
@@ -153,7 +154,8 @@ typedef enum {
   DCN_K_GEMM_DCOL = 6,
   DCN_K_COL2IM = 7,
   DCN_K_OFFSET_BWD = 8,
-  DCN_K_COUNT = 9
+  DCN_K_XPOSE = 9, /* x -> channels-last copy used by K1/K5 */
+  DCN_K_COUNT = 10
 } dcn_kernel_id;
 /* Record start/stop events around every launch of each kernel class, up to
  * `capacity` launches per class (0 disables). */

@@ -87,24 +87,32 @@ int make_geo(const dcn_desc* d, Geo* g) {
 }
 
 struct WsLayout {
-  size_t col = 0, col_bytes = 0;    // [B][K][HW]
-  size_t parts = 0, parts_bytes = 0;  // [B][O*K] ∂W partials
-  size_t goff = 0, goff_bytes = 0;  // [B][J][HW] ∂offset (when caller passes none)
+  size_t xT = 0;     // [B][H*W][C] channels-last copy of x (forward, kept for backward)
+  size_t col = 0;    // [B][HW][K] channels-last columns / ∂columns
+  size_t parts = 0;  // [B][O*K] ∂W partials
+  size_t goff = 0;   // [B][J][HW] ∂offset (when the caller passes none)
+  size_t goffT = 0;  // [B][HW][J] channels-last ∂offset (offset-conv ∂W)
+  size_t gxT = 0;    // [B][H*W][C] channels-last ∂x (sampling route)
+  size_t bins = 0;   // sample bins of K5b
   size_t total = 0;
 };
 
 WsLayout ws_layout(const Geo& g, bool bwd) {
   WsLayout L;
-  L.col = 0;
-  L.col_bytes = (size_t)g.B * g.K * g.HW * sizeof(float);
-  size_t off = align_up(L.col_bytes, 256);
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = off;
+    off = align_up(off + bytes, 256);
+    return at;
+  };
+  L.xT = take((size_t)g.B * g.HWi * g.C * sizeof(float));
+  L.col = take((size_t)g.B * g.HW * g.K * sizeof(float));
   if (bwd) {
-    L.parts = off;
-    L.parts_bytes = (size_t)g.B * g.O * g.K * sizeof(float);
-    off = align_up(off + L.parts_bytes, 256);
-    L.goff = off;
-    L.goff_bytes = (size_t)g.B * g.J * g.HW * sizeof(float);
-    off = align_up(off + L.goff_bytes, 256);
+    L.parts = take((size_t)g.B * g.O * g.K * sizeof(float));
+    L.goff = take((size_t)g.B * g.J * g.HW * sizeof(float));
+    L.goffT = take((size_t)g.B * g.J * g.HW * sizeof(float));
+    L.gxT = take((size_t)g.B * g.HWi * g.C * sizeof(float));
+    L.bins = take(dcn::bins_ws_bytes(g, g.B));
   }
   L.total = off;
   return L;
@@ -117,9 +125,11 @@ struct dcn_handle {
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   rocblas_handle blas = nullptr;
-  // handle-owned workspace (host-pointer API)
+  // handle-owned workspace (host-pointer API) and scratch (standalone kernel API)
   void* ws = nullptr;
   size_t ws_bytes = 0;
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
   // profiling: events per kernel class
   int prof_cap = 0;
   std::vector<hipEvent_t> ev[DCN_K_COUNT];  // pairs: [2*i] start, [2*i+1] stop
@@ -149,19 +159,24 @@ int set_device(dcn_handle* h) {
   return DCN_OK;
 }
 
-// ---- forward core ------------------------------------------------------------
+// ---- forward / backward cores ---------------------------------------------------
 int core_forward(dcn_handle* h, const Geo& g, const float* x, const float* off, const float* w,
-                 const float* b, bool has_bias, float* out, float* col) {
+                 const float* b, bool has_bias, float* out, float* xT, float* colT) {
   {
-    ProfScope ps(h, DCN_K_IM2COL);
-    HIP_TRY(dcn::launch_im2col(g, x, off, col, 0, g.B, h->stream));
+    ProfScope ps(h, DCN_K_XPOSE);
+    HIP_TRY(dcn::launch_nchw_to_nhwc(x, xT, g.B, g.C, g.HWi, h->stream));
   }
   {
-    // out_b[O][HW] = Wf[O][K] · col_b[K][HW]; column-major: C(HW×O) = col_b(HW×K) · Wf(K×O)
+    ProfScope ps(h, DCN_K_IM2COL);
+    HIP_TRY(dcn::launch_im2col(g, x, xT, off, colT, 0, g.B, h->stream));
+  }
+  {
+    // out_b[O][HW] = Wf[O][K] · colT_b[HW][K]ᵀ; column-major: C(HW×O) = colT_bᵀ · Wf (TN GEMM,
+    // both operands K-contiguous)
     ProfScope ps(h, DCN_K_GEMM_FWD);
     const float one = 1.f, zero = 0.f;
-    BLAS_TRY(rocblas_sgemm_strided_batched(h->blas, rocblas_operation_none, rocblas_operation_none,
-                                           g.HW, g.O, g.K, &one, col, g.HW, (rocblas_stride)g.K * g.HW,
+    BLAS_TRY(rocblas_sgemm_strided_batched(h->blas, rocblas_operation_transpose, rocblas_operation_none,
+                                           g.HW, g.O, g.K, &one, colT, g.K, (rocblas_stride)g.K * g.HW,
                                            w, g.K, 0, &zero, out, g.HW, (rocblas_stride)g.O * g.HW, g.B));
   }
   if (has_bias) {
@@ -173,10 +188,14 @@ int core_forward(dcn_handle* h, const Geo& g, const float* x, const float* off, 
 
 int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off, const float* w,
                   const float* gout, float* gx, float* gw, float* gb, bool has_bias, float* goff,
-                  float* col, float* parts, bool col_valid) {
+                  float* xT, float* colT, float* parts, float* gxT, void* bins, bool col_valid) {
   if (!col_valid) {
+    {
+      ProfScope ps(h, DCN_K_XPOSE);
+      HIP_TRY(dcn::launch_nchw_to_nhwc(x, xT, g.B, g.C, g.HWi, h->stream));
+    }
     ProfScope ps(h, DCN_K_IM2COL);
-    HIP_TRY(dcn::launch_im2col(g, x, off, col, 0, g.B, h->stream));
+    HIP_TRY(dcn::launch_im2col(g, x, xT, off, colT, 0, g.B, h->stream));
   }
   if (has_bias) {
     ProfScope ps(h, DCN_K_BWD_BIAS);
@@ -184,27 +203,42 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
   }
   const float one = 1.f, zero = 0.f;
   {
-    // ∂Wf[O][K] = Σ_b ∂out_b[O][HW] · col_bᵀ; column-major per image:
-    // P_b(K×O) = col_bᵀ (K×HW) · ∂out_b (HW×O); then deterministic Σ_b.
+    // ∂Wf[O][K] = Σ_b ∂out_b[O][HW] · colT_b[HW][K]; column-major per image:
+    // P_b(K×O) = colT_b(K×HW) · ∂out_b(HW×O) (NN); then a deterministic Σ_b.
     ProfScope ps(h, DCN_K_GEMM_DW);
-    BLAS_TRY(rocblas_sgemm_strided_batched(h->blas, rocblas_operation_transpose, rocblas_operation_none,
-                                           g.K, g.O, g.HW, &one, col, g.HW, (rocblas_stride)g.K * g.HW,
+    BLAS_TRY(rocblas_sgemm_strided_batched(h->blas, rocblas_operation_none, rocblas_operation_none,
+                                           g.K, g.O, g.HW, &one, colT, g.K, (rocblas_stride)g.K * g.HW,
                                            gout, g.HW, (rocblas_stride)g.O * g.HW, &zero, parts, g.K,
                                            (rocblas_stride)g.K * g.O, g.B));
     HIP_TRY(dcn::launch_sum_partials(parts, g.B, (size_t)g.K * g.O, gw, h->stream));
   }
   {
-    // ∂col_b[K][HW] = Wfᵀ · ∂out_b; column-major: C(HW×K) = ∂out_b(HW×O) · Wfᵀ(O×K)
+    // ∂colT_b[HW][K] = ∂out_bᵀ · Wf; column-major: C(K×HW) = Wf(K×O) · ∂out_bᵀ(O×HW) (NT);
+    // overwrites the columns (no longer needed after ∂W)
     ProfScope ps(h, DCN_K_GEMM_DCOL);
     BLAS_TRY(rocblas_sgemm_strided_batched(h->blas, rocblas_operation_none, rocblas_operation_transpose,
-                                           g.HW, g.K, g.O, &one, gout, g.HW, (rocblas_stride)g.O * g.HW,
-                                           w, g.K, 0, &zero, col, g.HW, (rocblas_stride)g.K * g.HW, g.B));
+                                           g.K, g.HW, g.O, &one, w, g.K, 0, gout, g.HW,
+                                           (rocblas_stride)g.O * g.HW, &zero, colT, g.K,
+                                           (rocblas_stride)g.K * g.HW, g.B));
   }
-  HIP_TRY(hipMemsetAsync(gx, 0, (size_t)g.B * g.C * g.HWi * sizeof(float), h->stream));
   {
+    // K5 overwrites grad_x (sampling route) and grad_off
     ProfScope ps(h, DCN_K_COL2IM);
-    HIP_TRY(dcn::launch_col2im_coord(g, x, off, col, gx, goff, 0, g.B, h->stream));
+    HIP_TRY(dcn::launch_col2im_coord(g, x, xT, off, colT, gx, gxT, goff, bins, 0, g.B, h->stream));
   }
+  return DCN_OK;
+}
+
+int ensure_scratch(dcn_handle* h, size_t bytes) {
+  if (h->scratch_bytes >= bytes) return DCN_OK;
+  if (h->scratch) {
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hipFree(h->scratch));
+  }
+  h->scratch = nullptr;
+  h->scratch_bytes = 0;
+  HIP_TRY(hipMalloc(&h->scratch, bytes));
+  h->scratch_bytes = bytes;
   return DCN_OK;
 }
 
@@ -260,6 +294,7 @@ int dcn_destroy(dcn_handle* h) {
   for (auto& v : h->ev)
     for (hipEvent_t e : v) (void)hipEventDestroy(e);
   if (h->ws) (void)hipFree(h->ws);
+  if (h->scratch) (void)hipFree(h->scratch);
   if (h->blas) (void)rocblas_destroy_handle(h->blas);
   if (h->own) (void)hipStreamDestroy(h->own);
   delete h;
@@ -340,7 +375,7 @@ int dcn_offset_conv_fwd(dcn_handle* h, const dcn_desc* d, const float* x, const 
   DCN_TRY(make_geo(d, &g));
   DCN_TRY(set_device(h));
   ProfScope ps(h, DCN_K_OFFSET_FWD);
-  HIP_TRY(dcn::launch_offset_conv_fwd(g, x, w_off, b_off, off, nullptr, h->stream));
+  HIP_TRY(dcn::launch_offset_conv_fwd(g, x, w_off, b_off, off, h->stream));
   return DCN_OK;
 }
 
@@ -350,9 +385,14 @@ int dcn_offset_conv_bwd(dcn_handle* h, const dcn_desc* d, const float* x, const 
   Geo g;
   DCN_TRY(make_geo(d, &g));
   DCN_TRY(set_device(h));
+  const size_t xbytes = align_up((size_t)g.B * g.HWi * g.C * sizeof(float), 256);
+  DCN_TRY(ensure_scratch(h, xbytes + (size_t)g.B * g.HW * g.J * sizeof(float)));
+  float* xT = static_cast<float*>(h->scratch);
+  float* goffT = reinterpret_cast<float*>(static_cast<char*>(h->scratch) + xbytes);
   ProfScope ps(h, DCN_K_OFFSET_BWD);
-  HIP_TRY(dcn::launch_offset_conv_bwd(g, x, w_off, grad_off, grad_x, grad_w_off, grad_b_off,
-                                      h->stream));
+  HIP_TRY(dcn::launch_nchw_to_nhwc(x, xT, g.B, g.C, g.HWi, h->stream));
+  HIP_TRY(dcn::launch_offset_conv_bwd(g, xT, w_off, grad_off, goffT, grad_x, grad_w_off,
+                                      grad_b_off, h->stream));
   return DCN_OK;
 }
 
@@ -362,8 +402,12 @@ int dcn_im2col_fwd(dcn_handle* h, const dcn_desc* d, const float* x, const float
   DCN_TRY(make_geo(d, &g));
   DCN_TRY(set_device(h));
   if (b0 < 0 || nb < 0 || b0 + nb > g.B) return fail(DCN_ERR_INVALID, "image range out of bounds");
+  DCN_TRY(ensure_scratch(h, (size_t)g.B * g.HWi * g.C * sizeof(float)));
+  float* xT = static_cast<float*>(h->scratch);
   ProfScope ps(h, DCN_K_IM2COL);
-  HIP_TRY(dcn::launch_im2col(g, x, off, col, b0, nb, h->stream));
+  HIP_TRY(dcn::launch_nchw_to_nhwc(x + (size_t)b0 * g.C * g.HWi, xT + (size_t)b0 * g.HWi * g.C, nb,
+                                   g.C, g.HWi, h->stream));
+  HIP_TRY(dcn::launch_im2col(g, x, xT, off, col, b0, nb, h->stream));
   return DCN_OK;
 }
 
@@ -373,8 +417,17 @@ int dcn_col2im_coord_bwd(dcn_handle* h, const dcn_desc* d, const float* x, const
   DCN_TRY(make_geo(d, &g));
   DCN_TRY(set_device(h));
   if (b0 < 0 || nb < 0 || b0 + nb > g.B) return fail(DCN_ERR_INVALID, "image range out of bounds");
+  const size_t xbytes = align_up((size_t)g.B * g.HWi * g.C * sizeof(float), 256);
+  DCN_TRY(ensure_scratch(h, 2 * xbytes + dcn::bins_ws_bytes(g, nb)));
+  char* sc = static_cast<char*>(h->scratch);
+  float* xT = reinterpret_cast<float*>(sc);
+  float* gxT = reinterpret_cast<float*>(sc + xbytes);
+  void* bins = sc + 2 * xbytes;
   ProfScope ps(h, DCN_K_COL2IM);
-  HIP_TRY(dcn::launch_col2im_coord(g, x, off, grad_col, grad_x, grad_off, b0, nb, h->stream));
+  HIP_TRY(dcn::launch_nchw_to_nhwc(x + (size_t)b0 * g.C * g.HWi, xT + (size_t)b0 * g.HWi * g.C, nb,
+                                   g.C, g.HWi, h->stream));
+  HIP_TRY(dcn::launch_col2im_coord(g, x, xT, off, grad_col, grad_x, gxT, grad_off, bins, b0, nb,
+                                   h->stream));
   return DCN_OK;
 }
 
@@ -389,10 +442,11 @@ int dcn_forward(dcn_handle* h, const dcn_desc* d, const float* x, const float* w
   if (d->has_bias && !b) return fail(DCN_ERR_INVALID, "has_bias set but bias is NULL");
   {
     ProfScope ps(h, DCN_K_OFFSET_FWD);
-    HIP_TRY(dcn::launch_offset_conv_fwd(g, x, w_off, b_off, off, nullptr, h->stream));
+    HIP_TRY(dcn::launch_offset_conv_fwd(g, x, w_off, b_off, off, h->stream));
   }
-  float* col = reinterpret_cast<float*>(static_cast<char*>(ws) + L.col);
-  return core_forward(h, g, x, off, w, b, d->has_bias != 0, out, col);
+  char* base = static_cast<char*>(ws);
+  return core_forward(h, g, x, off, w, b, d->has_bias != 0, out,
+                      reinterpret_cast<float*>(base + L.xT), reinterpret_cast<float*>(base + L.col));
 }
 
 int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* off,
@@ -406,13 +460,14 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
   if (!ws || ws_bytes < L.total) return fail(DCN_ERR_WORKSPACE, "workspace too small for dcn_backward");
   if (d->has_bias && !grad_b) return fail(DCN_ERR_INVALID, "has_bias set but grad_b is NULL");
   char* base = static_cast<char*>(ws);
-  float* col = reinterpret_cast<float*>(base + L.col);
-  float* parts = reinterpret_cast<float*>(base + L.parts);
-  float* goff = grad_off_out ? grad_off_out : reinterpret_cast<float*>(base + L.goff);
+  auto F = [&](size_t o) { return reinterpret_cast<float*>(base + o); };
+  float* goff = grad_off_out ? grad_off_out : F(L.goff);
   DCN_TRY(core_backward(h, g, x, off, w, grad_out, grad_x, grad_w, grad_b, d->has_bias != 0, goff,
-                        col, parts, (flags & DCN_BWD_COL_IN_WS) != 0));
+                        F(L.xT), F(L.col), F(L.parts), F(L.gxT), base + L.bins,
+                        (flags & DCN_BWD_COL_IN_WS) != 0));
   ProfScope ps(h, DCN_K_OFFSET_BWD);
-  HIP_TRY(dcn::launch_offset_conv_bwd(g, x, w_off, goff, grad_x, grad_w_off, grad_b_off, h->stream));
+  HIP_TRY(dcn::launch_offset_conv_bwd(g, F(L.xT), w_off, goff, F(L.goffT), grad_x, grad_w_off,
+                                      grad_b_off, h->stream));
   return DCN_OK;
 }
 

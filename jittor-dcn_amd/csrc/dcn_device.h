@@ -1,0 +1,122 @@
+// dcn_device.h — device-side helpers shared by the libdcn kernels (gfx950).
+//
+// Semantics follow /root/reference/deform_conv.py:56-81 exactly:
+//   * sample for output (h, w), tap n:  row ≈ w + Δx[n], col ≈ h + Δy[n]   (Q1, :39/:47)
+//   * coordinates normalised by the OUTPUT size and unnormalised by the INPUT
+//     size with align_corners=True (Q2, :37-38 + grid_sample)
+//   * no per-tap base position (Q3, :64-66); offsets [Δx(0..N-1) | Δy(0..N-1)] (Q4, :62)
+//   * columns ordered k = n*C + c (Q5, :72-74)
+// The coordinate chain is evaluated in fp32 in the reference's own op order; every
+// kernel source is compiled with -ffp-contract=off so no FMA changes which side of
+// an integer a coordinate lands on (Q6). Interpolation uses explicit fmaf.
+#pragma once
+#include "dcn_internal.h"
+
+namespace dcn {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// deform_conv.py:64-68 (grid (w,h) + offset), :37-39 (norm by (W_out-1),(H_out-1);
+// grid = [norm_y, norm_x]) and grid_sample's align_corners=True unnormalisation
+// ((g+1)/2)*(size-1): grid[...,0] = norm_y indexes the input COLUMN, grid[...,1]
+// = norm_x the input ROW.
+__device__ __forceinline__ void ref_coord(int h, int w, float dx, float dy, const Geo& g,
+                                          float& iy, float& ix) {
+  const float cx = (float)w + dx;                // grid x + offset x
+  float nx = cx / (float)(g.Wo - 1);             // coords[...,0] / (W_out - 1)
+  nx = nx * 2.0f;
+  nx = nx - 1.0f;
+  iy = ((nx + 1.0f) / 2.0f) * (float)(g.H - 1);  // unnormalise over input H
+  const float cy = (float)h + dy;
+  float ny = cy / (float)(g.Ho - 1);
+  ny = ny * 2.0f;
+  ny = ny - 1.0f;
+  ix = ((ny + 1.0f) / 2.0f) * (float)(g.W - 1);  // unnormalise over input W
+}
+
+// A sample contributes only if at least one of its four corners can be inside the
+// image: floor(row) in [-1, H-1] and floor(col) in [-1, W-1]. Otherwise its value
+// and every derivative are exactly 0 (zeros padding). NaN -> invalid.
+struct Tap {
+  int r0, c0;
+  float fr, fc;
+  bool ok;
+};
+
+__device__ __forceinline__ Tap make_tap(float iy, float ix, const Geo& g) {
+  Tap t;
+  const float r0f = floorf(iy), c0f = floorf(ix);
+  t.ok = (r0f >= -1.0f) && (r0f <= (float)(g.H - 1)) && (c0f >= -1.0f) &&
+         (c0f <= (float)(g.W - 1));
+  t.r0 = t.ok ? (int)r0f : 0;
+  t.c0 = t.ok ? (int)c0f : 0;
+  t.fr = t.ok ? iy - r0f : 0.f;
+  t.fc = t.ok ? ix - c0f : 0.f;
+  return t;
+}
+
+// The tap of sample (b, group gi, tap n, output pixel m).
+__device__ __forceinline__ Tap sample_tap(const Geo& g, const float* __restrict__ off, int b,
+                                          int gi, int n, int m) {
+  const float* ob = off + ((size_t)b * g.J + (size_t)gi * 2 * g.N) * g.HW;
+  const int h = m / g.Wo, w = m - h * g.Wo;
+  float iy, ix;
+  ref_coord(h, w, ob[(size_t)n * g.HW + m], ob[(size_t)(g.N + n) * g.HW + m], g, iy, ix);
+  return make_tap(iy, ix, g);
+}
+
+// Canonical fp32 bilinear combination (all kernels and oracle/dcn_ref.c use this
+// exact op order, so independent implementations agree bit for bit).
+__device__ __forceinline__ float bilerp(float fr, float fc, float x00, float x01, float x10,
+                                        float x11) {
+  const float gr = 1.0f - fr, gc = 1.0f - fc;
+  float v = (gr * gc) * x00;
+  v = fmaf(gr * fc, x01, v);
+  v = fmaf(fr * gc, x10, v);
+  v = fmaf(fr * fc, x11, v);
+  return v;
+}
+
+// d(bilerp)/d(row) and d(bilerp)/d(col) (floor has zero gradient: one-sided).
+__device__ __forceinline__ float dbilerp_row(float fc, float x00, float x01, float x10,
+                                             float x11) {
+  return fmaf(fc, x11 - x01, (1.0f - fc) * (x10 - x00));
+}
+__device__ __forceinline__ float dbilerp_col(float fr, float x00, float x01, float x10,
+                                             float x11) {
+  return fmaf(fr, x11 - x10, (1.0f - fr) * (x01 - x00));
+}
+
+__device__ __forceinline__ float ldx(const float* __restrict__ xp, int r, int c, const Geo& g) {
+  return (r >= 0 && r < g.H && c >= 0 && c < g.W) ? xp[r * g.W + c] : 0.f;
+}
+
+// XCD-aware block order (cdna_hip_programming.md §5.5 T1, bijective form): the
+// dispatcher deals blocks round-robin over the 8 XCDs, so give the blocks that share
+// an XCD (equal linear id mod 8) a contiguous range of logical ids. Neighbouring
+// logical blocks then reuse each other's x / ∂col rows through that XCD's L2. Speed
+// only: correctness never depends on placement.
+struct Block3 {
+  unsigned x, y, z;
+};
+__device__ __forceinline__ Block3 xcd_block() {
+  const unsigned nx = gridDim.x, ny = gridDim.y;
+  const unsigned nwg = nx * ny * gridDim.z;
+  const unsigned bid = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+  const unsigned q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+  const unsigned lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  Block3 o;
+  o.x = lid % nx;
+  o.y = (lid / nx) % ny;
+  o.z = lid / (nx * ny);
+  return o;
+}
+
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// Row of D[row][col] held in register r by lane half hi, for 32x32 MFMA tiles.
+__device__ __forceinline__ int drow(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
+
+}  // namespace dcn

@@ -22,28 +22,34 @@ struct Geo {
   int J;       // offset channels = 2*N*G
 };
 
-// Launchers (dcn_kernels.hip). All stream-ordered, return hipError_t.
-hipError_t launch_im2col(const Geo& g, const float* x, const float* off,
-                         float* col, int b0, int nb, hipStream_t s);
-hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* off,
-                               const float* gcol, float* gx, float* goff,
-                               int b0, int nb, hipStream_t s);
-hipError_t launch_offset_conv_fwd(const Geo& g, const float* x,
-                                  const float* w_off, const float* b_off,
-                                  float* off, float* wt_scratch, hipStream_t s);
-hipError_t launch_offset_conv_bwd(const Geo& g, const float* x,
-                                  const float* w_off, const float* goff,
-                                  float* gx, float* gw_off, float* gb_off,
-                                  hipStream_t s);
-hipError_t launch_bias_add(const Geo& g, float* out, const float* bias, int b0,
-                           int nb, hipStream_t s);
-hipError_t launch_bias_grad(const Geo& g, const float* gout, float* gb,
-                            hipStream_t s);
-hipError_t launch_sum_partials(const float* parts, int nparts, size_t n,
-                               float* dst, hipStream_t s);
+// Launchers. All stream-ordered, return hipError_t.
+// dcn_sampling.hip (channels-last columns colT[b][m][n*C + c]):
+hipError_t launch_nchw_to_nhwc(const float* in, float* out, int B, int C, int P, hipStream_t s);
+hipError_t launch_nhwc_to_nchw(const float* in, float* out, int B, int C, int P, hipStream_t s);
+hipError_t launch_im2col(const Geo& g, const float* x, const float* xT, const float* off,
+                         float* colT, int b0, int nb, hipStream_t s);
+size_t bins_ws_bytes(const Geo& g, int nb);
+// Overwrites gx (NCHW) and goff for images [b0, b0+nb); gxT is scratch [B][HWi][C].
+hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, const float* off,
+                               const float* gcolT, float* gx, float* gxT, float* goff,
+                               void* bins_ws, int b0, int nb, hipStream_t s);
+// dcn_offset_conv.hip:
+hipError_t launch_offset_conv_fwd(const Geo& g, const float* x, const float* w_off,
+                                  const float* b_off, float* off, hipStream_t s);
+// xT: channels-last x; goffT: scratch [B][HW][J]. grad_x is accumulated.
+hipError_t launch_offset_conv_bwd(const Geo& g, const float* xT, const float* w_off,
+                                  const float* goff, float* goffT, float* gx, float* gw_off,
+                                  float* gb_off, hipStream_t s);
+// dcn_reduce.hip:
+void launch_channel_sum(const float* in, int B, int Cn, int HW, float* out, hipStream_t s);
+hipError_t launch_bias_add(const Geo& g, float* out, const float* bias, int b0, int nb,
+                           hipStream_t s);
+hipError_t launch_bias_grad(const Geo& g, const float* gout, float* gb, hipStream_t s);
+hipError_t launch_sum_partials(const float* parts, int nparts, size_t n, float* dst,
+                               hipStream_t s);
 
 // Selection of the im2col / col2im implementation (tests force the generic
-// global-memory kernels to cross-check the LDS-window kernels).
+// global-memory kernels to cross-check the channels-last ones).
 void set_force_generic(int on);
 int get_force_generic();
 

@@ -1,0 +1,108 @@
+// dcn_reduce.hip — bias add (deform_conv.py:79-80) and the deterministic channel
+// / partial reductions of the backward (∂b, ∂b_off, Σ_b ∂W partials).
+#include "dcn_device.h"
+
+namespace dcn {
+
+// out[ch] = Σ_{b,m} in[b][ch][m]: one 1024-thread block per channel streams its
+// B·HW values with 16-byte loads; fixed reduction order (deterministic).
+template <bool VEC>
+__global__ __launch_bounds__(1024) void channel_sum(const float* __restrict__ in, int B, int Cn,
+                                                    int HW, float* __restrict__ out) {
+  __shared__ float red[1024 / 64];
+  const int ch = blockIdx.x, tid = threadIdx.x;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float* p = in + ((size_t)b * Cn + ch) * HW;
+    if (VEC) {
+      const float4* p4 = reinterpret_cast<const float4*>(p);
+      for (int m = tid; m < HW / 4; m += 1024) {
+        const float4 v = p4[m];
+        s += (v.x + v.y) + (v.z + v.w);
+      }
+    } else {
+      for (int m = tid; m < HW; m += 1024) s += p[m];
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
+  if (tid == 0) {
+    float t = 0.f;
+    for (int w = 0; w < 1024 / 64; ++w) t += red[w];
+    out[ch] = t;
+  }
+}
+
+void launch_channel_sum(const float* in, int B, int Cn, int HW, float* out, hipStream_t s) {
+  if (HW % 4 == 0)
+    hipLaunchKernelGGL(channel_sum<true>, dim3(Cn), dim3(1024), 0, s, in, B, Cn, HW, out);
+  else
+    hipLaunchKernelGGL(channel_sum<false>, dim3(Cn), dim3(1024), 0, s, in, B, Cn, HW, out);
+}
+
+// ---------------------------------------------------------------------------
+// Bias (deform_conv.py:79-80) and reductions.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bias_add_kernel(float* __restrict__ out,
+                                                       const float* __restrict__ bias, int O,
+                                                       int HW, long n) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int o = (int)((i / HW) % O);
+    out[i] += bias[o];
+  }
+}
+
+__global__ __launch_bounds__(256) void bias_add_vec4(float4* __restrict__ out,
+                                                     const float* __restrict__ bias, int O,
+                                                     int HW4, long n4) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const float bv = bias[(int)((i / HW4) % O)];
+    float4 v = out[i];
+    v.x += bv;
+    v.y += bv;
+    v.z += bv;
+    v.w += bv;
+    out[i] = v;
+  }
+}
+
+hipError_t launch_bias_add(const Geo& g, float* out, const float* bias, int b0, int nb,
+                           hipStream_t s) {
+  float* o = out + (size_t)b0 * g.O * g.HW;
+  const long n = (long)nb * g.O * g.HW;
+  if (g.HW % 4 == 0) {
+    const long n4 = n / 4;
+    const unsigned grid = (unsigned)min((n4 + 255) / 256, 8192L);
+    hipLaunchKernelGGL(bias_add_vec4, dim3(grid), dim3(256), 0, s, reinterpret_cast<float4*>(o),
+                       bias, g.O, g.HW / 4, n4);
+  } else {
+    const unsigned grid = (unsigned)min((n + 255) / 256, 8192L);
+    hipLaunchKernelGGL(bias_add_kernel, dim3(grid), dim3(256), 0, s, o, bias, g.O, g.HW, n);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_bias_grad(const Geo& g, const float* gout, float* gb, hipStream_t s) {
+  launch_channel_sum(gout, g.B, g.O, g.HW, gb, s);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restrict__ parts,
+                                                           int nparts, size_t n,
+                                                           float* __restrict__ dst) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    float s = 0.f;
+    for (int p = 0; p < nparts; ++p) s += parts[(size_t)p * n + i];
+    dst[i] = s;
+  }
+}
+
+hipError_t launch_sum_partials(const float* parts, int nparts, size_t n, float* dst,
+                               hipStream_t s) {
+  const unsigned grid = (unsigned)min((n + 255) / 256, (size_t)4096);
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(grid), dim3(256), 0, s, parts, nparts, n, dst);
+  return hipGetLastError();
+}
+
+}  // namespace dcn

@@ -1,0 +1,682 @@
+// dcn_sampling.hip — the deformable bilinear sampling kernels of the hot path (gfx950):
+//   K1  im2col_cl     columns colT[b][m][n*C + c]            (deform_conv.py:30-54, :62-73)
+//   K5a offgrad_cl    ∂offset from ∂colT                     (autodiff of :37-38, :47-52)
+//   K5b bins + dx_gather_cl  ∂x by deterministic gather     (autodiff of :41-52)
+// plus the NCHW <-> NHWC transposes they need.
+//
+// Layout: channels-last ("CL"). x is transposed once to xT[b][r][q][c]; columns are
+// stored row-per-pixel colT[b][m][k], k = n*C + c (the reference's own column order,
+// deform_conv.py:72-73). A wave therefore handles a whole sample (one tap of one
+// output pixel) at a time with its lanes on consecutive channels: every corner read
+// and every column write is a contiguous 16-byte-per-lane run (1 KiB per wave
+// instruction at C = 256); the per-sample coordinates are computed once and
+// broadcast across the sample's lanes.
+//
+// ∂x without atomics: LDS float atomics (ds_add_f32) measured ~0.3 lanes/clk/CU on
+// MI355X and global float atomics cap at ~1.3 TB/s, both far too slow for the
+// 4·B·HW·N·C scatter. Instead each sample is binned by its top-left corner
+// (counting sort per image: int atomics on 28k samples/image), every bin list is
+// sorted, and each input pixel gathers the ∂col rows of the four bins whose 2x2
+// footprint covers it — a fixed summation order, so ∂x is bitwise reproducible.
+#include "dcn_device.h"
+
+namespace dcn {
+
+static int g_force_generic = 0;
+void set_force_generic(int on) { g_force_generic = on; }
+int get_force_generic() { return g_force_generic; }
+
+// ---------------------------------------------------------------------------
+// Channel-lane mapping: a sample's Cg channels are covered by LP lanes, each
+// owning VEC consecutive channels; SP = 64/LP samples share a wave instruction.
+// ---------------------------------------------------------------------------
+struct LaneMap {
+  int CQ;  // channel units (of VEC channels) per group
+  int LP;  // lanes per sample (power of two, <= 64)
+  int SP;  // samples per wave step
+};
+
+static LaneMap lane_map(int Cg, int vec) {
+  LaneMap L;
+  L.CQ = (Cg + vec - 1) / vec;
+  L.LP = 1;
+  while (L.LP < L.CQ && L.LP < 64) L.LP <<= 1;
+  L.SP = 64 / L.LP;
+  return L;
+}
+
+template <int VEC>
+struct Vec;
+template <>
+struct Vec<4> {
+  typedef float4 T;
+  __device__ static T zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+};
+template <>
+struct Vec<1> {
+  typedef float T;
+  __device__ static T zero() { return 0.f; }
+};
+
+template <int VEC>
+__device__ __forceinline__ typename Vec<VEC>::T ldv(const float* p, bool ok) {
+  if (!ok) return Vec<VEC>::zero();
+  return *reinterpret_cast<const typename Vec<VEC>::T*>(p);
+}
+template <int VEC>
+__device__ __forceinline__ void stv(float* p, typename Vec<VEC>::T v) {
+  *reinterpret_cast<typename Vec<VEC>::T*>(p) = v;
+}
+
+__device__ __forceinline__ float4 bilerp4(float fr, float fc, float4 a, float4 b, float4 c,
+                                          float4 d) {
+  return make_float4(bilerp(fr, fc, a.x, b.x, c.x, d.x), bilerp(fr, fc, a.y, b.y, c.y, d.y),
+                     bilerp(fr, fc, a.z, b.z, c.z, d.z), bilerp(fr, fc, a.w, b.w, c.w, d.w));
+}
+__device__ __forceinline__ float bilerp4(float fr, float fc, float a, float b, float c, float d) {
+  return bilerp(fr, fc, a, b, c, d);
+}
+
+// Per-sample state computed by lane i for sample s0 + i and broadcast with shfl.
+struct SampleBcast {
+  int r0, c0, m, n;
+  float fr, fc;
+  bool ok;
+};
+
+__device__ __forceinline__ SampleBcast bcast(const SampleBcast& v, int src) {
+  SampleBcast o;
+  o.r0 = __shfl(v.r0, src);
+  o.c0 = __shfl(v.c0, src);
+  o.m = __shfl(v.m, src);
+  o.n = __shfl(v.n, src);
+  o.fr = __shfl(v.fr, src);
+  o.fc = __shfl(v.fc, src);
+  o.ok = __shfl((int)v.ok, src) != 0;
+  return o;
+}
+
+__device__ __forceinline__ SampleBcast lane_sample(const Geo& g, const float* off, int b, int gi,
+                                                   int s, int NS) {
+  SampleBcast v;
+  v.ok = false;
+  v.r0 = v.c0 = v.m = v.n = 0;
+  v.fr = v.fc = 0.f;
+  if (s < NS) {
+    v.m = s / g.N;
+    v.n = s - v.m * g.N;
+    const Tap t = sample_tap(g, off, b, gi, v.n, v.m);
+    v.ok = t.ok;
+    v.r0 = t.r0;
+    v.c0 = t.c0;
+    v.fr = t.fr;
+    v.fc = t.fc;
+  }
+  return v;
+}
+
+template <int VEC>
+struct Corners {
+  typename Vec<VEC>::T a, b, c, d;  // (r0,c0) (r0,c0+1) (r0+1,c0) (r0+1,c0+1)
+};
+
+template <int VEC>
+__device__ __forceinline__ void load_corners(const float* __restrict__ xb, const SampleBcast& sm,
+                                             const Geo& g, int c, Corners<VEC>& q) {
+  const bool r0ok = sm.ok && sm.r0 >= 0, r1ok = sm.ok && sm.r0 + 1 < g.H;
+  const bool c0ok = sm.c0 >= 0, c1ok = sm.c0 + 1 < g.W;
+  const float* p00 = xb + ((long)sm.r0 * g.W + sm.c0) * (long)g.C + c;
+  const long rs = (long)g.W * g.C;
+  q.a = ldv<VEC>(p00, r0ok && c0ok);
+  q.b = ldv<VEC>(p00 + g.C, r0ok && c1ok);
+  q.c = ldv<VEC>(p00 + rs, r1ok && c0ok);
+  q.d = ldv<VEC>(p00 + rs + g.C, r1ok && c1ok);
+}
+
+// Samples per software-pipelined batch: all of a batch's row loads are issued before
+// the first one is consumed, so each wave keeps 4*U (K1) / 5*U (K5a) 1-KiB rows in flight.
+constexpr int kU = 4;
+
+// ---------------------------------------------------------------------------
+// K1: colT[bl][m][n*C + gi*Cg + c] = bilinear(xT[b][.][.][gi*Cg + c]).
+// One wave = 64 consecutive samples s = m*N + n of one image and group.
+// ---------------------------------------------------------------------------
+template <int VEC>
+__global__ __launch_bounds__(256) void im2col_cl(Geo g, LaneMap L, const float* __restrict__ xT,
+                                                 const float* __restrict__ off,
+                                                 float* __restrict__ colT, int b0) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const Block3 blk = xcd_block();
+  const int gi = blk.y, bl = blk.z, b = b0 + bl;
+  const int NS = g.HW * g.N;
+  const int s0 = (blk.x * 4 + wave) * 64;
+  if (s0 >= NS) return;
+  const SampleBcast mine = lane_sample(g, off, b, gi, s0 + lane, NS);
+  const int sub = lane / L.LP, u0 = lane - sub * L.LP;
+  const float* xb = xT + (size_t)b * g.HWi * g.C + (size_t)gi * g.Cg;
+  float* cb = colT + (size_t)bl * g.HW * g.K + (size_t)gi * g.Cg;
+  for (int it = 0; it < 64; it += kU * L.SP) {
+    SampleBcast sm[kU];
+    bool live[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int src = it + u * L.SP + sub;
+      sm[u] = bcast(mine, src & 63);
+      live[u] = src < 64 && s0 + src < NS;
+    }
+    for (int cu = u0; cu < L.CQ; cu += L.LP) {
+      const int c = cu * VEC;
+      Corners<VEC> q[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) load_corners<VEC>(xb, sm[u], g, c, q[u]);
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (!live[u]) continue;
+        const typename Vec<VEC>::T v = sm[u].ok ? bilerp4(sm[u].fr, sm[u].fc, q[u].a, q[u].b,
+                                                          q[u].c, q[u].d)
+                                                : Vec<VEC>::zero();
+        stv<VEC>(cb + (size_t)sm[u].m * g.K + (size_t)sm[u].n * g.C + c, v);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K5a: ∂off for every sample from its ∂colT row and the four xT corner rows.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void acc_dgrad(float fr, float fc, float gv, float a, float b, float c,
+                                          float d, float& diy, float& dix) {
+  diy = fmaf(gv, dbilerp_row(fc, a, b, c, d), diy);
+  dix = fmaf(gv, dbilerp_col(fr, a, b, c, d), dix);
+}
+__device__ __forceinline__ void acc_dgrad(float fr, float fc, float4 gv, float4 a, float4 b,
+                                          float4 c, float4 d, float& diy, float& dix) {
+  acc_dgrad(fr, fc, gv.x, a.x, b.x, c.x, d.x, diy, dix);
+  acc_dgrad(fr, fc, gv.y, a.y, b.y, c.y, d.y, diy, dix);
+  acc_dgrad(fr, fc, gv.z, a.z, b.z, c.z, d.z, diy, dix);
+  acc_dgrad(fr, fc, gv.w, a.w, b.w, c.w, d.w, diy, dix);
+}
+
+template <int VEC>
+__global__ __launch_bounds__(256) void offgrad_cl(Geo g, LaneMap L, const float* __restrict__ xT,
+                                                  const float* __restrict__ off,
+                                                  const float* __restrict__ gcolT,
+                                                  float* __restrict__ goff, int b0) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const Block3 blk = xcd_block();
+  const int gi = blk.y, bl = blk.z, b = b0 + bl;
+  const int NS = g.HW * g.N;
+  const int s0 = (blk.x * 4 + wave) * 64;
+  if (s0 >= NS) return;
+  const SampleBcast mine = lane_sample(g, off, b, gi, s0 + lane, NS);
+  const int sub = lane / L.LP, u0 = lane - sub * L.LP;
+  const float* xb = xT + (size_t)b * g.HWi * g.C + (size_t)gi * g.Cg;
+  const float* gb = gcolT + (size_t)bl * g.HW * g.K + (size_t)gi * g.Cg;
+  float* gob = goff + ((size_t)b * g.J + (size_t)gi * 2 * g.N) * g.HW;
+  const float sy = (float)(g.H - 1) / (float)(g.Wo - 1);
+  const float sx = (float)(g.W - 1) / (float)(g.Ho - 1);
+  for (int it = 0; it < 64; it += kU * L.SP) {
+    SampleBcast sm[kU];
+    bool live[kU];
+    float diy[kU], dix[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int src = it + u * L.SP + sub;
+      sm[u] = bcast(mine, src & 63);
+      live[u] = src < 64 && s0 + src < NS;
+      diy[u] = dix[u] = 0.f;
+    }
+    for (int cu = u0; cu < L.CQ; cu += L.LP) {
+      const int c = cu * VEC;
+      Corners<VEC> q[kU];
+      typename Vec<VEC>::T gv[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        gv[u] = ldv<VEC>(gb + (size_t)sm[u].m * g.K + (size_t)sm[u].n * g.C + c,
+                         live[u] && sm[u].ok);
+        load_corners<VEC>(xb, sm[u], g, c, q[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (sm[u].ok)
+          acc_dgrad(sm[u].fr, sm[u].fc, gv[u], q[u].a, q[u].b, q[u].c, q[u].d, diy[u], dix[u]);
+    }
+    // reduce over the LP lanes of each sample (fixed tree: deterministic)
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      for (int o = L.LP >> 1; o > 0; o >>= 1) {
+        diy[u] += __shfl_xor(diy[u], o);
+        dix[u] += __shfl_xor(dix[u], o);
+      }
+    if (u0 == 0) {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (!live[u]) continue;
+        gob[(size_t)sm[u].n * g.HW + sm[u].m] = diy[u] * sy;
+        gob[(size_t)(g.N + sm[u].n) * g.HW + sm[u].m] = dix[u] * sx;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K5b: sample bins. Bin of a valid sample = its top-left corner (r0, c0) in
+// [-1, H-1] x [-1, W-1] -> (r0+1)*(W+1) + (c0+1); NB = (H+1)*(W+1) bins per
+// (image, group). rec[s] = {bin, fr, fc}.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bins_count(Geo g, const float* __restrict__ off,
+                                                  int* __restrict__ cnt, float4* __restrict__ rec,
+                                                  int b0, int nb) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const int NS = g.HW * g.N;
+  const long total = (long)nb * g.G * NS;
+  if (idx >= total) return;
+  const int s = (int)(idx % NS);
+  const int bg = (int)(idx / NS);  // bl*G + gi
+  const int gi = bg % g.G, bl = bg / g.G;
+  const Tap t = sample_tap(g, off, b0 + bl, gi, s % g.N, s / g.N);
+  const int NB = (g.H + 1) * (g.W + 1);
+  int bin = -1;
+  if (t.ok) {
+    bin = (t.r0 + 1) * (g.W + 1) + (t.c0 + 1);
+    atomicAdd(cnt + (size_t)bg * NB + bin, 1);
+  }
+  rec[idx] = make_float4(__int_as_float(bin), t.fr, t.fc, 0.f);
+}
+
+// Exclusive scan of the NB counts of one (image, group); start has NB+1 entries.
+__global__ __launch_bounds__(1024) void bins_scan(int NB, const int* __restrict__ cnt,
+                                                  int* __restrict__ start,
+                                                  int* __restrict__ cursor) {
+  __shared__ int wsum[16];
+  const int bg = blockIdx.x, tid = threadIdx.x;
+  const int* c = cnt + (size_t)bg * NB;
+  int* st = start + (size_t)bg * (NB + 1);
+  int* cu = cursor + (size_t)bg * NB;
+  const int per = (NB + 1023) / 1024;
+  const int lo = min(tid * per, NB), hi = min(lo + per, NB);
+  int local = 0;
+  for (int i = lo; i < hi; ++i) local += c[i];
+  // inclusive scan of `local` across the block
+  int v = local;
+  const int lane = tid & 63, wv = tid >> 6;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(v, o);
+    if (lane >= o) v += t;
+  }
+  if (lane == 63) wsum[wv] = v;
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int i = 0; i < 16; ++i) {
+      const int t = wsum[i];
+      wsum[i] = acc;
+      acc += t;
+    }
+  }
+  __syncthreads();
+  int run = v - local + wsum[wv];
+  for (int i = lo; i < hi; ++i) {
+    st[i] = run;
+    cu[i] = 0;
+    run += c[i];
+  }
+  if (tid == 1023) st[NB] = run;
+}
+
+__global__ __launch_bounds__(256) void bins_fill(Geo g, const float4* __restrict__ rec,
+                                                 const int* __restrict__ start,
+                                                 int* __restrict__ cursor, int* __restrict__ list,
+                                                 int nb) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const int NS = g.HW * g.N;
+  if (idx >= (long)nb * g.G * NS) return;
+  const int bin = __float_as_int(rec[idx].x);
+  if (bin < 0) return;
+  const int bg = (int)(idx / NS);
+  const int NB = (g.H + 1) * (g.W + 1);
+  const int slot = atomicAdd(cursor + (size_t)bg * NB + bin, 1);
+  list[(size_t)bg * NS + start[(size_t)bg * (NB + 1) + bin] + slot] = (int)(idx % NS);
+}
+
+// Sort every bin list ascending: fixes the gather's summation order.
+__global__ __launch_bounds__(256) void bins_sort(int NB, int NS, long nbins,
+                                                 const int* __restrict__ start,
+                                                 int* __restrict__ list) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= nbins) return;
+  const int bg = (int)(idx / NB), bin = (int)(idx % NB);
+  const int* st = start + (size_t)bg * (NB + 1);
+  int* l = list + (size_t)bg * NS;
+  const int lo = st[bin], hi = st[bin + 1];
+  for (int i = lo + 1; i < hi; ++i) {
+    const int v = l[i];
+    int j = i - 1;
+    while (j >= lo && l[j] > v) {
+      l[j + 1] = l[j];
+      --j;
+    }
+    l[j + 1] = v;
+  }
+}
+
+// ∂xT[b][r][q][gi*Cg + c] = Σ over the samples of bins (r-1,q-1), (r-1,q), (r,q-1),
+// (r,q) of (their w11, w10, w01, w00 weight) · ∂colT row. One group of LP lanes per
+// input pixel. The group's lanes first fetch up to LP (bin entry -> sample -> weight,
+// row offset) records in parallel, then the row loads are issued kU at a time.
+template <int VEC>
+__global__ __launch_bounds__(256) void dx_gather_cl(Geo g, LaneMap L,
+                                                    const float4* __restrict__ rec,
+                                                    const int* __restrict__ start,
+                                                    const int* __restrict__ list,
+                                                    const float* __restrict__ gcolT,
+                                                    float* __restrict__ gxT, int b0) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const Block3 blk = xcd_block();
+  const int gi = blk.y, bl = blk.z, b = b0 + bl;
+  const int sub = lane / L.LP, u0 = lane - sub * L.LP;
+  const int p = (blk.x * 4 + wave) * L.SP + sub;  // input pixel r*W + q
+  const bool pok = p < g.HWi;
+  const int pp = pok ? p : 0;
+  const int r = pp / g.W, q = pp - r * g.W;
+  const int NB = (g.H + 1) * (g.W + 1), NS = g.HW * g.N;
+  const int bg = bl * g.G + gi;
+  const int* st = start + (size_t)bg * (NB + 1);
+  const int* lst = list + (size_t)bg * NS;
+  const float4* rc = rec + (size_t)bg * NS;
+  const float* gb = gcolT + (size_t)bl * g.HW * g.K + (size_t)gi * g.Cg;
+  // the four bins: k=0 (r-1,q-1) -> w11, 1 (r-1,q) -> w10, 2 (r,q-1) -> w01, 3 (r,q) -> w00
+  int lo[4], cntk[4];
+  int E = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int dr = (k >> 1) ^ 1, dc = (k & 1) ^ 1;
+    const int bin = (r - dr + 1) * (g.W + 1) + (q - dc + 1);
+    lo[k] = pok ? st[bin] : 0;
+    cntk[k] = pok ? st[bin + 1] - lo[k] : 0;
+    E += cntk[k];
+  }
+  // E differs between the pixel groups of a wave: loop to the wave maximum
+  int Emax = E;
+  for (int o = 32; o >= L.LP; o >>= 1) Emax = max(Emax, __shfl_xor(Emax, o));
+  const int gbase = sub * L.LP;  // first lane of this pixel's group
+  // every lane of the group takes part in entry resolution and the shuffles, also
+  // lanes whose channel unit is past CQ (they only skip the loads / FMAs)
+  for (int cu0 = 0; cu0 < L.CQ; cu0 += L.LP) {
+    const int cu = cu0 + u0;
+    const bool cok = cu < L.CQ;
+    const int c = (cok ? cu : 0) * VEC;
+    typename Vec<VEC>::T acc = Vec<VEC>::zero();
+    for (int e0 = 0; e0 < Emax; e0 += L.LP) {
+      // lane u0 of the group resolves entry e0 + u0
+      const int e = e0 + u0;
+      float wgt = 0.f;
+      int row = 0;
+      if (e < E) {
+        int k = 0, idx = e;
+        while (idx >= cntk[k]) {
+          idx -= cntk[k];
+          ++k;
+        }
+        const int s = lst[lo[k] + idx];
+        const float4 R = rc[s];
+        const float wr = (k >> 1) == 0 ? R.y : 1.0f - R.y;  // rows r-1 bins weigh fr
+        const float wc = (k & 1) == 0 ? R.z : 1.0f - R.z;   // cols q-1 bins weigh fc
+        wgt = wr * wc;
+        const int m = s / g.N;
+        row = m * g.K + (s - m * g.N) * g.C;
+      }
+      const int n_here = min(L.LP, max(E - e0, 0));
+      const int n_wave = min(L.LP, Emax - e0);
+      for (int i = 0; i < n_wave; i += kU) {
+        float wv[kU];
+        int rv[kU];
+        typename Vec<VEC>::T gv[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int src = gbase + min(i + u, L.LP - 1);
+          wv[u] = __shfl(wgt, src);
+          rv[u] = __shfl(row, src);
+          gv[u] = ldv<VEC>(gb + (size_t)rv[u] + c, cok && i + u < n_here);
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          if (i + u >= n_here) continue;
+          if constexpr (VEC == 4) {
+            acc.x = fmaf(wv[u], gv[u].x, acc.x);
+            acc.y = fmaf(wv[u], gv[u].y, acc.y);
+            acc.z = fmaf(wv[u], gv[u].z, acc.z);
+            acc.w = fmaf(wv[u], gv[u].w, acc.w);
+          } else {
+            acc = fmaf(wv[u], gv[u], acc);
+          }
+        }
+      }
+    }
+    if (pok && cok) stv<VEC>(gxT + ((size_t)b * g.HWi + p) * g.C + (size_t)gi * g.Cg + c, acc);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Transposes (64x64 tiles through LDS, odd pitch).
+// ---------------------------------------------------------------------------
+// out[b][p][c] = in[b][c][p]
+__global__ __launch_bounds__(256) void nchw_to_nhwc(const float* __restrict__ in,
+                                                    float* __restrict__ out, int C, int P) {
+  __shared__ float t[64][65];
+  const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64, b = blockIdx.z;
+  const float* ib = in + (size_t)b * C * P;
+  float* ob = out + (size_t)b * C * P;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int c = c0 + i, p = p0 + tx;
+    if (c < C && p < P) t[i][tx] = ib[(size_t)c * P + p];
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int p = p0 + i, c = c0 + tx;
+    if (c < C && p < P) ob[(size_t)p * C + c] = t[tx][i];
+  }
+}
+
+// out[b][c][p] = in[b][p][c]
+__global__ __launch_bounds__(256) void nhwc_to_nchw(const float* __restrict__ in,
+                                                    float* __restrict__ out, int C, int P) {
+  __shared__ float t[64][65];
+  const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64, b = blockIdx.z;
+  const float* ib = in + (size_t)b * C * P;
+  float* ob = out + (size_t)b * C * P;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int p = p0 + i, c = c0 + tx;
+    if (c < C && p < P) t[i][tx] = ib[(size_t)p * C + c];
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int c = c0 + i, p = p0 + tx;
+    if (c < C && p < P) ob[(size_t)c * P + p] = t[tx][i];
+  }
+}
+
+hipError_t launch_nchw_to_nhwc(const float* in, float* out, int B, int C, int P, hipStream_t s) {
+  dim3 grid((P + 63) / 64, (C + 63) / 64, B);
+  hipLaunchKernelGGL(nchw_to_nhwc, grid, dim3(256), 0, s, in, out, C, P);
+  return hipGetLastError();
+}
+
+hipError_t launch_nhwc_to_nchw(const float* in, float* out, int B, int C, int P, hipStream_t s) {
+  dim3 grid((P + 63) / 64, (C + 63) / 64, B);
+  hipLaunchKernelGGL(nhwc_to_nchw, grid, dim3(256), 0, s, in, out, C, P);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Generic kernels (NCHW x, one thread per column element / sample): an
+// implementation independent of the transposes, lane maps and bins, used for
+// cross-checks and forced by dcn_debug_force_generic.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void im2col_generic(Geo g, const float* __restrict__ x,
+                                                      const float* __restrict__ off,
+                                                      float* __restrict__ colT, int b0, int nb) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const long total = (long)nb * g.HW * g.K;
+  if (idx >= total) return;
+  const int k = (int)(idx % g.K);
+  const long row = idx / g.K;
+  const int m = (int)(row % g.HW), bl = (int)(row / g.HW), b = b0 + bl;
+  const int n = k / g.C, c = k - n * g.C, gi = c / g.Cg;
+  const Tap tp = sample_tap(g, off, b, gi, n, m);
+  float v = 0.f;
+  if (tp.ok) {
+    const float* xp = x + ((size_t)b * g.C + c) * g.HWi;
+    v = bilerp(tp.fr, tp.fc, ldx(xp, tp.r0, tp.c0, g), ldx(xp, tp.r0, tp.c0 + 1, g),
+               ldx(xp, tp.r0 + 1, tp.c0, g), ldx(xp, tp.r0 + 1, tp.c0 + 1, g));
+  }
+  colT[idx] = v;
+}
+
+__device__ __forceinline__ void scatter_global(float* __restrict__ gxp, int r, int c, float v,
+                                               const Geo& g) {
+  if (v != 0.f && r >= 0 && r < g.H && c >= 0 && c < g.W) atomicAdd(gxp + r * g.W + c, v);
+}
+
+// gx (NCHW) must be zeroed by the caller; goff overwritten.
+__global__ __launch_bounds__(256) void col2im_generic(Geo g, const float* __restrict__ x,
+                                                      const float* __restrict__ off,
+                                                      const float* __restrict__ gcolT,
+                                                      float* __restrict__ gx,
+                                                      float* __restrict__ goff, int b0, int nb) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const long total = (long)nb * g.G * g.N * g.HW;
+  if (idx >= total) return;
+  const int m = (int)(idx % g.HW);
+  long t = idx / g.HW;
+  const int n = (int)(t % g.N);
+  t /= g.N;
+  const int gi = (int)(t % g.G);
+  const int bl = (int)(t / g.G), b = b0 + bl;
+  const Tap tp = sample_tap(g, off, b, gi, n, m);
+  float diy = 0.f, dix = 0.f;
+  if (tp.ok) {
+    const float gr = 1.0f - tp.fr, gc = 1.0f - tp.fc;
+    const float* grow = gcolT + ((size_t)bl * g.HW + m) * g.K + (size_t)n * g.C;
+    for (int cl = 0; cl < g.Cg; ++cl) {
+      const int c = gi * g.Cg + cl;
+      const float gv = grow[c];
+      const float* xp = x + ((size_t)b * g.C + c) * g.HWi;
+      const float x00 = ldx(xp, tp.r0, tp.c0, g), x01 = ldx(xp, tp.r0, tp.c0 + 1, g);
+      const float x10 = ldx(xp, tp.r0 + 1, tp.c0, g), x11 = ldx(xp, tp.r0 + 1, tp.c0 + 1, g);
+      diy = fmaf(gv, dbilerp_row(tp.fc, x00, x01, x10, x11), diy);
+      dix = fmaf(gv, dbilerp_col(tp.fr, x00, x01, x10, x11), dix);
+      float* gxp = gx + ((size_t)b * g.C + c) * g.HWi;
+      scatter_global(gxp, tp.r0, tp.c0, gv * (gr * gc), g);
+      scatter_global(gxp, tp.r0, tp.c0 + 1, gv * (gr * tp.fc), g);
+      scatter_global(gxp, tp.r0 + 1, tp.c0, gv * (tp.fr * gc), g);
+      scatter_global(gxp, tp.r0 + 1, tp.c0 + 1, gv * (tp.fr * tp.fc), g);
+    }
+  }
+  const float sy = (float)(g.H - 1) / (float)(g.Wo - 1);
+  const float sx = (float)(g.W - 1) / (float)(g.Ho - 1);
+  float* gob = goff + ((size_t)b * g.J + (size_t)gi * 2 * g.N) * g.HW;
+  gob[(size_t)n * g.HW + m] = diy * sy;
+  gob[(size_t)(g.N + n) * g.HW + m] = dix * sx;
+}
+
+// ---------------------------------------------------------------------------
+// Launchers
+// ---------------------------------------------------------------------------
+static bool can_vec4(const Geo& g) { return g.C % 4 == 0 && g.Cg % 4 == 0; }
+
+size_t bins_ws_bytes(const Geo& g, int nb) {
+  const size_t NB = (size_t)(g.H + 1) * (g.W + 1), NS = (size_t)g.HW * g.N;
+  const size_t groups = (size_t)nb * g.G;
+  size_t b = 0;
+  b += groups * NB * 4;        // cnt
+  b += groups * (NB + 1) * 4;  // start
+  b += groups * NB * 4;        // cursor
+  b = (b + 15) / 16 * 16;
+  b += groups * NS * 16;       // rec
+  b += groups * NS * 4;        // list
+  return (b + 255) / 256 * 256;
+}
+
+hipError_t launch_im2col(const Geo& g, const float* x, const float* xT, const float* off,
+                         float* colT, int b0, int nb, hipStream_t s) {
+  if (nb <= 0) return hipSuccess;
+  if (g_force_generic) {
+    const long total = (long)nb * g.HW * g.K;
+    hipLaunchKernelGGL(im2col_generic, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, g,
+                       x, off, colT, b0, nb);
+    return hipGetLastError();
+  }
+  const int NS = g.HW * g.N;
+  dim3 grid((NS + 255) / 256, g.G, nb);
+  if (can_vec4(g))
+    hipLaunchKernelGGL(im2col_cl<4>, grid, dim3(256), 0, s, g, lane_map(g.Cg, 4), xT, off, colT,
+                       b0);
+  else
+    hipLaunchKernelGGL(im2col_cl<1>, grid, dim3(256), 0, s, g, lane_map(g.Cg, 1), xT, off, colT,
+                       b0);
+  return hipGetLastError();
+}
+
+hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, const float* off,
+                               const float* gcolT, float* gx, float* gxT, float* goff,
+                               void* bins_ws, int b0, int nb, hipStream_t s) {
+  if (nb <= 0) return hipSuccess;
+  hipError_t e;
+  if (g_force_generic) {
+    e = hipMemsetAsync(gx + (size_t)b0 * g.C * g.HWi, 0, (size_t)nb * g.C * g.HWi * sizeof(float),
+                       s);
+    if (e != hipSuccess) return e;
+    const long total = (long)nb * g.G * g.N * g.HW;
+    hipLaunchKernelGGL(col2im_generic, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, g,
+                       x, off, gcolT, gx, goff, b0, nb);
+    return hipGetLastError();
+  }
+  const bool v4 = can_vec4(g);
+  const LaneMap L = lane_map(g.Cg, v4 ? 4 : 1);
+  const int NS = g.HW * g.N;
+  {  // K5a: ∂offset
+    dim3 grid((NS + 255) / 256, g.G, nb);
+    if (v4)
+      hipLaunchKernelGGL(offgrad_cl<4>, grid, dim3(256), 0, s, g, L, xT, off, gcolT, goff, b0);
+    else
+      hipLaunchKernelGGL(offgrad_cl<1>, grid, dim3(256), 0, s, g, L, xT, off, gcolT, goff, b0);
+  }
+  // K5b: bins
+  const int NB = (g.H + 1) * (g.W + 1);
+  const size_t groups = (size_t)nb * g.G;
+  char* w = static_cast<char*>(bins_ws);
+  int* cnt = reinterpret_cast<int*>(w);
+  int* start = cnt + groups * NB;
+  int* cursor = start + groups * (NB + 1);
+  size_t o = (size_t)((char*)(cursor + groups * NB) - w);
+  o = (o + 15) / 16 * 16;
+  float4* rec = reinterpret_cast<float4*>(w + o);
+  int* list = reinterpret_cast<int*>(rec + groups * NS);
+  e = hipMemsetAsync(cnt, 0, groups * NB * sizeof(int), s);
+  if (e != hipSuccess) return e;
+  const long total = (long)groups * NS;
+  const unsigned gs = (unsigned)((total + 255) / 256);
+  hipLaunchKernelGGL(bins_count, dim3(gs), dim3(256), 0, s, g, off, cnt, rec, b0, nb);
+  hipLaunchKernelGGL(bins_scan, dim3((unsigned)groups), dim3(1024), 0, s, NB, cnt, start, cursor);
+  hipLaunchKernelGGL(bins_fill, dim3(gs), dim3(256), 0, s, g, rec, start, cursor, list, nb);
+  const long nbins = (long)groups * NB;
+  hipLaunchKernelGGL(bins_sort, dim3((unsigned)((nbins + 255) / 256)), dim3(256), 0, s, NB, NS,
+                     nbins, start, list);
+  {  // gather ∂xT, then back to NCHW (overwrites gx for these images)
+    const int pix_per_block = 4 * L.SP;
+    dim3 grid((g.HWi + pix_per_block - 1) / pix_per_block, g.G, nb);
+    if (v4)
+      hipLaunchKernelGGL(dx_gather_cl<4>, grid, dim3(256), 0, s, g, L, rec, start, list, gcolT,
+                         gxT, b0);
+    else
+      hipLaunchKernelGGL(dx_gather_cl<1>, grid, dim3(256), 0, s, g, L, rec, start, list, gcolT,
+                         gxT, b0);
+  }
+  return launch_nhwc_to_nchw(gxT + (size_t)b0 * g.HWi * g.C, gx + (size_t)b0 * g.C * g.HWi, nb,
+                             g.C, g.HWi, s);
+}
+
+}  // namespace dcn

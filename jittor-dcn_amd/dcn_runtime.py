@@ -18,7 +18,7 @@ DCN_F32, DCN_BF16 = 0, 1
 DCN_BWD_COL_IN_WS = 1
 KERNEL_IDS = {
     "offset_fwd": 0, "im2col": 1, "gemm_fwd": 2, "bias_fwd": 3, "bwd_bias": 4,
-    "gemm_dw": 5, "gemm_dcol": 6, "col2im": 7, "offset_bwd": 8,
+    "gemm_dw": 5, "gemm_dcol": 6, "col2im": 7, "offset_bwd": 8, "xpose": 9,
 }
 
 

@@ -145,12 +145,23 @@ def weight_matrix(w):
     return np.asarray(w, np.float64).reshape(O, kh * kw, C)
 
 
-def forward(x, w_off, b_off, w, b, stride, padding, dilation=(1, 1), G=1):
-    """DeformConv2d.execute (deform_conv.py:56-81). Returns (out f64, off f32, cache)."""
+def forward(x, w_off, b_off, w, b, stride, padding, dilation=(1, 1), G=1, offsets=None):
+    """DeformConv2d.execute (deform_conv.py:56-81). Returns (out f64, off f32, cache).
+
+    `offsets` (optional, fp32 [B, 2NG, Ho, Wo]) conditions everything after the offset
+    conv on given offsets. ∂offset and ∂x are discontinuous where a sampling coordinate
+    crosses an integer (floor), so two implementations whose offset convs round
+    differently by one ulp legitimately disagree at such knife edges; the kernel
+    parity tests therefore feed the device's own offsets to the oracle and check the
+    offsets themselves separately."""
     O, C, kh, kw = w.shape
     N = kh * kw
-    off = offset_conv(x, w_off, b_off, stride, padding, dilation)
-    off32 = off.astype(F32)  # the reference's offsets are fp32 tensors
+    if offsets is None:
+        off = offset_conv(x, w_off, b_off, stride, padding, dilation)
+        off32 = off.astype(F32)  # the reference's offsets are fp32 tensors
+    else:
+        off32 = np.ascontiguousarray(offsets, F32)
+        off = off32
     B, _, Ho, Wo = off.shape
     S, coords = deform_sample(x, off32, Ho, Wo, N, G)
     Wf = weight_matrix(w)

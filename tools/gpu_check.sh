@@ -1,0 +1,21 @@
+#!/bin/bash
+# One GPU round-trip: parity tests, smoke, bench, rocprofv3 kernel stats.
+# Every GPU step has its own time limit; the chain stops at the first failure.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TAG=${1:-r01}
+STEPS=${STEPS:-10}
+echo "== pytest -m gpu" && \
+timeout -k 10 420 python -m pytest tests -m gpu -q -rf > gpurun_out/pytest_gpu_$TAG.log 2>&1; rc=$?
+tail -25 gpurun_out/pytest_gpu_$TAG.log
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || { echo "pytest aborted rc=$rc"; exit $rc; }
+echo "== smoke" && \
+timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" && \
+echo "== bench" && \
+timeout -k 10 420 python bench.py --steps $STEPS --warmup 3 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err && \
+cat gpurun_out/bench_$TAG.json && \
+echo "== rocprofv3" && \
+timeout -k 10 420 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1 && \
+echo "done"
