@@ -7,8 +7,6 @@
 // Backward = Jittor autodiff of the same graph (train.py:414): ∂b, ∂W (per-image
 //            GEMM partials + deterministic sum), ∂col = Wᵀ·∂out, K5 col2im +
 //            coordinate gradient, offset-conv backward.
-#include <rocblas/rocblas.h>
-
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -34,11 +32,11 @@ int fail(int code, const std::string& msg) {
       return fail(DCN_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));           \
   } while (0)
 
-#define BLAS_TRY(expr)                                                                       \
+#define GEMM_TRY(h, spec, A, B, C)                                                           \
   do {                                                                                       \
-    rocblas_status s_ = (expr);                                                              \
-    if (s_ != rocblas_status_success)                                                        \
-      return fail(DCN_ERR_BLAS, std::string(#expr) + ": " + rocblas_status_to_string(s_));   \
+    std::string e_;                                                                          \
+    if (dcn::gemm_run((h)->gemm, (spec), (A), (B), (C), (h)->stream, &e_) != 0)              \
+      return fail(DCN_ERR_BLAS, e_);                                                         \
   } while (0)
 
 #define DCN_TRY(expr)           \
@@ -124,7 +122,7 @@ struct dcn_handle {
   int device = 0;
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
-  rocblas_handle blas = nullptr;
+  dcn::GemmEngine* gemm = nullptr;
   // handle-owned workspace (host-pointer API) and scratch (standalone kernel API)
   void* ws = nullptr;
   size_t ws_bytes = 0;
@@ -174,10 +172,14 @@ int core_forward(dcn_handle* h, const Geo& g, const float* x, const float* off, 
     // out_b[O][HW] = Wf[O][K] · colT_b[HW][K]ᵀ; column-major: C(HW×O) = colT_bᵀ · Wf (TN GEMM,
     // both operands K-contiguous)
     ProfScope ps(h, DCN_K_GEMM_FWD);
-    const float one = 1.f, zero = 0.f;
-    BLAS_TRY(rocblas_sgemm_strided_batched(h->blas, rocblas_operation_transpose, rocblas_operation_none,
-                                           g.HW, g.O, g.K, &one, colT, g.K, (rocblas_stride)g.K * g.HW,
-                                           w, g.K, 0, &zero, out, g.HW, (rocblas_stride)g.O * g.HW, g.B));
+    dcn::GemmSpec sp;
+    sp.ta = true;
+    sp.m = g.HW; sp.n = g.O; sp.k = g.K;
+    sp.lda = g.K; sp.sa = (long)g.K * g.HW;
+    sp.ldb = g.K; sp.sb = 0;
+    sp.ldc = g.HW; sp.sc = (long)g.O * g.HW;
+    sp.batch = g.B;
+    GEMM_TRY(h, sp, colT, w, out);
   }
   if (has_bias) {
     ProfScope ps(h, DCN_K_BIAS_FWD);
@@ -201,25 +203,31 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
     ProfScope ps(h, DCN_K_BWD_BIAS);
     HIP_TRY(dcn::launch_bias_grad(g, gout, gb, h->stream));
   }
-  const float one = 1.f, zero = 0.f;
   {
     // ∂Wf[O][K] = Σ_b ∂out_b[O][HW] · colT_b[HW][K]; column-major per image:
     // P_b(K×O) = colT_b(K×HW) · ∂out_b(HW×O) (NN); then a deterministic Σ_b.
     ProfScope ps(h, DCN_K_GEMM_DW);
-    BLAS_TRY(rocblas_sgemm_strided_batched(h->blas, rocblas_operation_none, rocblas_operation_none,
-                                           g.K, g.O, g.HW, &one, colT, g.K, (rocblas_stride)g.K * g.HW,
-                                           gout, g.HW, (rocblas_stride)g.O * g.HW, &zero, parts, g.K,
-                                           (rocblas_stride)g.K * g.O, g.B));
+    dcn::GemmSpec sp;
+    sp.m = g.K; sp.n = g.O; sp.k = g.HW;
+    sp.lda = g.K; sp.sa = (long)g.K * g.HW;
+    sp.ldb = g.HW; sp.sb = (long)g.O * g.HW;
+    sp.ldc = g.K; sp.sc = (long)g.K * g.O;
+    sp.batch = g.B;
+    GEMM_TRY(h, sp, colT, gout, parts);
     HIP_TRY(dcn::launch_sum_partials(parts, g.B, (size_t)g.K * g.O, gw, h->stream));
   }
   {
     // ∂colT_b[HW][K] = ∂out_bᵀ · Wf; column-major: C(K×HW) = Wf(K×O) · ∂out_bᵀ(O×HW) (NT);
     // overwrites the columns (no longer needed after ∂W)
     ProfScope ps(h, DCN_K_GEMM_DCOL);
-    BLAS_TRY(rocblas_sgemm_strided_batched(h->blas, rocblas_operation_none, rocblas_operation_transpose,
-                                           g.K, g.HW, g.O, &one, w, g.K, 0, gout, g.HW,
-                                           (rocblas_stride)g.O * g.HW, &zero, colT, g.K,
-                                           (rocblas_stride)g.K * g.HW, g.B));
+    dcn::GemmSpec sp;
+    sp.tb = true;
+    sp.m = g.K; sp.n = g.HW; sp.k = g.O;
+    sp.lda = g.K; sp.sa = 0;
+    sp.ldb = g.HW; sp.sb = (long)g.O * g.HW;
+    sp.ldc = g.K; sp.sc = (long)g.K * g.HW;
+    sp.batch = g.B;
+    GEMM_TRY(h, sp, w, gout, colT);
   }
   {
     // K5 overwrites grad_x (sampling route) and grad_off
@@ -277,11 +285,11 @@ int dcn_create(int device, dcn_handle** out) {
     return fail(DCN_ERR_HIP, std::string("dcn_create: ") + hipGetErrorString(e));
   }
   h->stream = h->own;
-  if (rocblas_create_handle(&h->blas) != rocblas_status_success ||
-      rocblas_set_stream(h->blas, h->stream) != rocblas_status_success) {
+  std::string gerr;
+  if (dcn::gemm_engine_create(&h->gemm, &gerr) != 0) {
     (void)hipStreamDestroy(h->own);
     delete h;
-    return fail(DCN_ERR_BLAS, "rocblas_create_handle failed");
+    return fail(DCN_ERR_BLAS, gerr);
   }
   *out = h;
   return DCN_OK;
@@ -295,7 +303,7 @@ int dcn_destroy(dcn_handle* h) {
     for (hipEvent_t e : v) (void)hipEventDestroy(e);
   if (h->ws) (void)hipFree(h->ws);
   if (h->scratch) (void)hipFree(h->scratch);
-  if (h->blas) (void)rocblas_destroy_handle(h->blas);
+  dcn::gemm_engine_destroy(h->gemm);
   if (h->own) (void)hipStreamDestroy(h->own);
   delete h;
   return DCN_OK;
@@ -304,7 +312,6 @@ int dcn_destroy(dcn_handle* h) {
 int dcn_set_stream(dcn_handle* h, void* s) {
   DCN_TRY(set_device(h));
   h->stream = s ? reinterpret_cast<hipStream_t>(s) : h->own;
-  BLAS_TRY(rocblas_set_stream(h->blas, h->stream));
   return DCN_OK;
 }
 

@@ -4,6 +4,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "../../include/dcn.h"
 
 namespace dcn {
@@ -47,6 +49,20 @@ hipError_t launch_bias_add(const Geo& g, float* out, const float* bias, int b0, 
 hipError_t launch_bias_grad(const Geo& g, const float* gout, float* gb, hipStream_t s);
 hipError_t launch_sum_partials(const float* parts, int nparts, size_t n, float* dst,
                                hipStream_t s);
+
+// dcn_gemm.cpp: C = op(A)·op(B) (column-major, alpha 1, beta 0), strided batched.
+struct GemmSpec {
+  bool ta = false, tb = false;
+  int m = 0, n = 0, k = 0, lda = 0, ldb = 0, ldc = 0;
+  long sa = 0, sb = 0, sc = 0;
+  int batch = 1;
+};
+struct GemmEngine;
+int gemm_engine_create(GemmEngine** out, std::string* err);
+void gemm_engine_destroy(GemmEngine* e);
+int gemm_run(GemmEngine* e, const GemmSpec& s, const float* A, const float* B, float* C,
+             hipStream_t st, std::string* err);
+int gemm_backend_of(GemmEngine* e, const GemmSpec& s);  // -1 untuned, 0 rocBLAS, 1 hipBLASLt
 
 // Selection of the im2col / col2im implementation (tests force the generic
 // global-memory kernels to cross-check the channels-last ones).
