@@ -86,6 +86,8 @@ int make_geo(const dcn_desc* d, Geo* g) {
 
 struct WsLayout {
   size_t xT = 0;     // [B][H*W][C] channels-last copy of x (forward, kept for backward)
+  size_t wt = 0;     // transposed w_off copy for the offset-conv kernels
+  size_t part = 0;   // offset-conv channel-slice partials (forward)
   size_t col = 0;    // [B][HW][K] channels-last columns / ∂columns
   size_t parts = 0;  // [B][O*K] ∂W partials
   size_t goff = 0;   // [B][J][HW] ∂offset (when the caller passes none)
@@ -104,11 +106,13 @@ WsLayout ws_layout(const Geo& g, bool bwd) {
     return at;
   };
   L.xT = take((size_t)g.B * g.HWi * g.C * sizeof(float));
+  L.wt = take(dcn::offset_conv_wt_floats(g) * sizeof(float));
+  L.part = take(dcn::offset_conv_fpart_floats(g) * sizeof(float));
   L.col = take((size_t)g.B * g.HW * g.K * sizeof(float));
   if (bwd) {
     L.parts = take((size_t)g.B * g.O * g.K * sizeof(float));
     L.goff = take((size_t)g.B * g.J * g.HW * sizeof(float));
-    L.goffT = take((size_t)g.B * g.J * g.HW * sizeof(float));
+    L.goffT = take(dcn::offset_conv_goffT_floats(g) * sizeof(float));
     L.gxT = take((size_t)g.B * g.HWi * g.C * sizeof(float));
     L.bins = take(dcn::bins_ws_bytes(g, g.B));
   }
@@ -381,8 +385,12 @@ int dcn_offset_conv_fwd(dcn_handle* h, const dcn_desc* d, const float* x, const 
   Geo g;
   DCN_TRY(make_geo(d, &g));
   DCN_TRY(set_device(h));
+  const size_t wbytes = align_up(dcn::offset_conv_wt_floats(g) * sizeof(float), 256);
+  DCN_TRY(ensure_scratch(h, wbytes + dcn::offset_conv_fpart_floats(g) * sizeof(float)));
+  char* sc = static_cast<char*>(h->scratch);
   ProfScope ps(h, DCN_K_OFFSET_FWD);
-  HIP_TRY(dcn::launch_offset_conv_fwd(g, x, w_off, b_off, off, h->stream));
+  HIP_TRY(dcn::launch_offset_conv_fwd(g, x, w_off, b_off, off, reinterpret_cast<float*>(sc),
+                                      reinterpret_cast<float*>(sc + wbytes), h->stream));
   return DCN_OK;
 }
 
@@ -393,12 +401,15 @@ int dcn_offset_conv_bwd(dcn_handle* h, const dcn_desc* d, const float* x, const 
   DCN_TRY(make_geo(d, &g));
   DCN_TRY(set_device(h));
   const size_t xbytes = align_up((size_t)g.B * g.HWi * g.C * sizeof(float), 256);
-  DCN_TRY(ensure_scratch(h, xbytes + (size_t)g.B * g.HW * g.J * sizeof(float)));
-  float* xT = static_cast<float*>(h->scratch);
-  float* goffT = reinterpret_cast<float*>(static_cast<char*>(h->scratch) + xbytes);
+  const size_t gbytes = align_up(dcn::offset_conv_goffT_floats(g) * sizeof(float), 256);
+  DCN_TRY(ensure_scratch(h, xbytes + gbytes + dcn::offset_conv_wt_floats(g) * sizeof(float)));
+  char* sc = static_cast<char*>(h->scratch);
+  float* xT = reinterpret_cast<float*>(sc);
+  float* goffT = reinterpret_cast<float*>(sc + xbytes);
+  float* wt2 = reinterpret_cast<float*>(sc + xbytes + gbytes);
   ProfScope ps(h, DCN_K_OFFSET_BWD);
   HIP_TRY(dcn::launch_nchw_to_nhwc(x, xT, g.B, g.C, g.HWi, h->stream));
-  HIP_TRY(dcn::launch_offset_conv_bwd(g, xT, w_off, grad_off, goffT, grad_x, grad_w_off,
+  HIP_TRY(dcn::launch_offset_conv_bwd(g, x, xT, w_off, grad_off, goffT, wt2, grad_x, grad_w_off,
                                       grad_b_off, h->stream));
   return DCN_OK;
 }
@@ -449,7 +460,10 @@ int dcn_forward(dcn_handle* h, const dcn_desc* d, const float* x, const float* w
   if (d->has_bias && !b) return fail(DCN_ERR_INVALID, "has_bias set but bias is NULL");
   {
     ProfScope ps(h, DCN_K_OFFSET_FWD);
-    HIP_TRY(dcn::launch_offset_conv_fwd(g, x, w_off, b_off, off, h->stream));
+    HIP_TRY(dcn::launch_offset_conv_fwd(g, x, w_off, b_off, off,
+                                        reinterpret_cast<float*>(static_cast<char*>(ws) + L.wt),
+                                        reinterpret_cast<float*>(static_cast<char*>(ws) + L.part),
+                                        h->stream));
   }
   char* base = static_cast<char*>(ws);
   return core_forward(h, g, x, off, w, b, d->has_bias != 0, out,
@@ -473,8 +487,8 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
                         F(L.xT), F(L.col), F(L.parts), F(L.gxT), base + L.bins,
                         (flags & DCN_BWD_COL_IN_WS) != 0));
   ProfScope ps(h, DCN_K_OFFSET_BWD);
-  HIP_TRY(dcn::launch_offset_conv_bwd(g, F(L.xT), w_off, goff, F(L.goffT), grad_x, grad_w_off,
-                                      grad_b_off, h->stream));
+  HIP_TRY(dcn::launch_offset_conv_bwd(g, x, F(L.xT), w_off, goff, F(L.goffT), F(L.wt), grad_x,
+                                      grad_w_off, grad_b_off, h->stream));
   return DCN_OK;
 }
 

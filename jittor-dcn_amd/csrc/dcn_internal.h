@@ -36,12 +36,18 @@ hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, co
                                const float* gcolT, float* gx, float* gxT, float* goff,
                                void* bins_ws, int b0, int nb, hipStream_t s);
 // dcn_offset_conv.hip:
+// wt / wt2: scratch of offset_conv_wt_floats(g) floats (transposed w_off copies).
+size_t offset_conv_wt_floats(const Geo& g);
+size_t offset_conv_goffT_floats(const Geo& g);  // ∂offT rows + ∂w_off block partials
+size_t offset_conv_fpart_floats(const Geo& g);  // forward channel-slice partials
+// part: scratch of offset_conv_fpart_floats(g) floats (channel-slice partial sums).
 hipError_t launch_offset_conv_fwd(const Geo& g, const float* x, const float* w_off,
-                                  const float* b_off, float* off, hipStream_t s);
-// xT: channels-last x; goffT: scratch [B][HW][J]. grad_x is accumulated.
-hipError_t launch_offset_conv_bwd(const Geo& g, const float* xT, const float* w_off,
-                                  const float* goff, float* goffT, float* gx, float* gw_off,
-                                  float* gb_off, hipStream_t s);
+                                  const float* b_off, float* off, float* wt, float* part,
+                                  hipStream_t s);
+// xT: channels-last x; goffT: scratch of offset_conv_goffT_floats(g). grad_x is accumulated.
+hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
+                                  const float* w_off, const float* goff, float* goffT, float* wt2,
+                                  float* gx, float* gw_off, float* gb_off, hipStream_t s);
 // dcn_reduce.hip:
 void launch_channel_sum(const float* in, int B, int Cn, int HW, float* out, hipStream_t s);
 hipError_t launch_bias_add(const Geo& g, float* out, const float* bias, int b0, int nb,

@@ -1,315 +1,461 @@
-// dcn_offset_conv.hip — the offset conv (deform_conv.py:16-21, :58) and its backward
-// as implicit GEMMs on the exact-fp32 MFMA v_mfma_f32_32x32x2_f32 (gfx950).
+// dcn_offset_conv.hip — the offset conv (deform_conv.py:16-21, :58) and its backward.
 //
-// Operand maps (gfx950, 32x32x2 f32): lane l supplies A[i=l&31][k=l>>5] and
-// B[k=l>>5][j=l&31]; D[row][col] lives in lane col=l&31, register r: row = drow(r, l>>5).
-// Only the lane&31 index of an operand can be made contiguous in memory, so each
-// kernel puts a memory-contiguous dimension there and stages the other operand in LDS:
-//   K3  fwd   D[j][pixel]   A = w_off  (LDS, [c][tap][j], odd pitch)   B = x NCHW (lanes = pixels)
-//   K7a ∂W    D[j][c]       A = ∂offT  (channels-last rows, lanes = j)  B = xT (lanes = channels)
-//   K7b ∂x    D[c][pixel]   A = w_off  (LDS, [j][tap][c], odd pitch)   B = ∂off NCHW (lanes = pixels)
-// Taps are padded to an even count (slot s of lane half hi = tap 2s+hi) so a k pair never
-// straddles channels; padded taps carry zero weights.
+// The offset conv has only J = 2*N*G = 18 output channels, so as an MFMA GEMM 14 of
+// every 32 tile rows are padding and every MFMA needs its own per-lane gather (the
+// 32x32x2 f32 MFMA versions of these kernels were load-issue bound at 3-4x their MFMA
+// floor). These kernels are VALU implicit GEMMs built around wave-uniform operands: the
+// J offset-channel values that every lane of a wave needs at the same time (weights in
+// the forward / input-gradient passes, ∂offsets in the weight-gradient pass) are read
+// with scalar loads from small transposed copies, so each coalesced vector load feeds
+// J (or 4*J) FMAs:
+//   K3  fwd   lanes = output pixels (NCHW x)    acc[J]      weights  wT[c][tap][J]   scalar
+//   K7a ∂W    lanes = channels (xT, float4)     acc[J][4]   ∂offT[p][J]              scalar
+//   K7b ∂x    lanes = input pixels (NCHW ∂x)    acc[32 ch]  weights  wT2[j][tap][C]  scalar
+#include <algorithm>
+
 #include "dcn_device.h"
 
 namespace dcn {
 
-// LDS chunking of w_off: 32 channels (K3) / 32 offset channels (K7b) per stage for
-// kernels up to 3x3 (S <= 5, 42 KiB), 8 for larger kernels.
-template <int S>
-struct Chunk {
-  static constexpr int v = S <= 5 ? 32 : 8;
-};
+constexpr int kJB = 18;  // offset channels per pass (one pass for the reference's 3x3)
+constexpr int kCB = 32;  // channels per K7b pass
 
-// off[b][j][p] = b_off[j] + Σ_{c,tap} w_off[j][c][tap] · x[b][c][tap-shifted p]
-// Block = 4 waves x 2 tiles x 32 pixels; grid.y = tiles of 32 offset channels j.
-template <int S>
-__global__ __launch_bounds__(256) void offset_conv_fwd_mfma(Geo g, const float* __restrict__ x,
-                                                           const float* __restrict__ w_off,
-                                                           const float* __restrict__ b_off,
-                                                           float* __restrict__ off) {
-  constexpr int kCCh = Chunk<S>::v;
-  __shared__ float wt[kCCh * 2 * S * 33];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hi = lane >> 5;
-  const int KK = g.kh * g.kw, KKp = 2 * S;
-  const long Mtot = (long)g.B * g.HW;
-  const int j0 = blockIdx.y * 32;
-  long pt[2];
-  bool pok[2];
-  int b[2], m[2], offs[2][S];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    pt[t] = ((long)blockIdx.x * 8 + wave * 2 + t) * 32 + (lane & 31);
-    pok[t] = pt[t] < Mtot;
-    b[t] = pok[t] ? (int)(pt[t] / g.HW) : 0;
-    m[t] = pok[t] ? (int)(pt[t] - (long)b[t] * g.HW) : 0;
-    const int ho = m[t] / g.Wo, wo = m[t] - (m[t] / g.Wo) * g.Wo;
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      const int tap = 2 * s + hi;
-      offs[t][s] = -1;
-      if (pok[t] && tap < KK) {
-        const int i = tap / g.kw, kx = tap - i * g.kw;
-        const int y = ho * g.sh - g.ph + i * g.dh, xx = wo * g.sw - g.pw + kx * g.dw;
-        if (y >= 0 && y < g.H && xx >= 0 && xx < g.W) offs[t][s] = y * g.W + xx;
-      }
-    }
-  }
-  const float* xb0 = x + (size_t)b[0] * g.C * g.HWi;
-  const float* xb1 = x + (size_t)b[1] * g.C * g.HWi;
-  f32x16 acc0 = {0}, acc1 = {0};
-  for (int c0 = 0; c0 < g.C; c0 += kCCh) {
-    __syncthreads();
-    // stage w_off[j0..j0+31][c0..c0+31][tap] -> wt[(c*KKp + tap)*33 + j]; reads run along (c, tap)
-    const int nstage = 32 * kCCh * KKp;
-    for (int e = tid; e < nstage; e += 256) {
-      const int jl = e / (kCCh * KKp), rem = e - jl * (kCCh * KKp);
-      const int cl = rem / KKp, tap = rem - cl * KKp;
-      const int j = j0 + jl, c = c0 + cl;
-      float v = 0.f;
-      if (j < g.J && c < g.C && tap < KK) v = w_off[((size_t)j * g.C + c) * KK + tap];
-      wt[(cl * KKp + tap) * 33 + jl] = v;
-    }
-    __syncthreads();
-    const int cn = min(kCCh, g.C - c0);
-    // software pipeline: the x values of channel cl+1 are in flight while cl's MFMAs run
-    float v0[S], v1[S];
-    auto fetch = [&](int cl, float* d0, float* d1) {
-      const float* x0 = xb0 + (size_t)(c0 + cl) * g.HWi;
-      const float* x1 = xb1 + (size_t)(c0 + cl) * g.HWi;
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        d0[s] = offs[0][s] >= 0 ? x0[offs[0][s]] : 0.f;
-        d1[s] = offs[1][s] >= 0 ? x1[offs[1][s]] : 0.f;
-      }
-    };
-    fetch(0, v0, v1);
-    for (int cl = 0; cl < cn; ++cl) {
-      float n0[S], n1[S];
-      if (cl + 1 < cn) fetch(cl + 1, n0, n1);
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const float a = wt[(cl * KKp + 2 * s + hi) * 33 + (lane & 31)];
-        acc0 = mfma32(a, v0[s], acc0);
-        acc1 = mfma32(a, v1[s], acc1);
-      }
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        v0[s] = n0[s];
-        v1[s] = n1[s];
-      }
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int j = j0 + drow(r, hi);
-    if (j < g.J) {
-      if (pok[0]) off[((size_t)b[0] * g.J + j) * g.HW + m[0]] = acc0[r] + b_off[j];
-      if (pok[1]) off[((size_t)b[1] * g.J + j) * g.HW + m[1]] = acc1[r] + b_off[j];
-    }
-  }
+// Padded sizes: the uniform operand runs are zero-padded so every scalar load is
+// unconditional (the compiler then merges them into s_load_dwordx8/x16).
+__host__ __device__ static inline int pad_j(int J) { return (J + kJB - 1) / kJB * kJB; }
+__host__ __device__ static inline int pad_c(int C) { return (C + kCB - 1) / kCB * kCB; }
+
+// wT[(c*KK + tap)*Jp + j] = w_off[j][c][tap] (0 for j >= J)
+__global__ __launch_bounds__(256) void woff_to_ctj(const float* __restrict__ w,
+                                                   float* __restrict__ wt, int J, int Jp, int C,
+                                                   int KK) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= Jp * C * KK) return;
+  const int r = i / Jp, j = i - r * Jp;  // r = c*KK + tap
+  const int c = r / KK, tap = r - c * KK;
+  wt[i] = j < J ? w[((size_t)j * C + c) * KK + tap] : 0.f;
+}
+// wT2[(j*KK + tap)*Cp + c] = w_off[j][c][tap] (0 for c >= C)
+__global__ __launch_bounds__(256) void woff_to_jtc(const float* __restrict__ w,
+                                                   float* __restrict__ wt, int J, int C, int Cp,
+                                                   int KK) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= J * KK * Cp) return;
+  const int r = i / Cp, c = i - r * Cp;  // r = j*KK + tap
+  const int j = r / KK, tap = r - j * KK;
+  wt[i] = c < C ? w[((size_t)j * C + c) * KK + tap] : 0.f;
+}
+// goffT[(b*HW + p)*Jp + j] = goff[b][j][p] (0 for j >= J)
+__global__ __launch_bounds__(256) void goff_to_pj(const float* __restrict__ goff,
+                                                  float* __restrict__ goffT, int J, int Jp,
+                                                  int HW, long total) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;  // over (b, j, p), p fastest: coalesced reads
+  if (i >= total) return;
+  const int p = (int)(i % HW);
+  const long bj = i / HW;
+  const int j = (int)(bj % Jp), b = (int)(bj / Jp);
+  goffT[((size_t)b * HW + p) * Jp + j] = j < J ? goff[((size_t)b * J + j) * HW + p] : 0.f;
 }
 
-// ∂w_off[j][c][tap] += Σ_p ∂off[b][j][p] · x[b][c][tap-shifted p]
-// One wave = one (tap, 32-channel tile, 32-offset-channel tile, pixel range): D[j][c]
-// with A from the channels-last ∂offT[b][p][j] rows and B from the channels-last
-// xT[b][y][x][c] rows (both contiguous across lanes).
-__global__ __launch_bounds__(256) void offset_wgrad_mfma(Geo g, const float* __restrict__ xT,
+// ---------------------------------------------------------------------------
+// K3: off[b][j][p] = b_off[j] + Σ_{c,tap} w_off[j][c][tap] · x[b][c][tap-shifted p]
+// One thread per output pixel, kJB accumulators; grid.y = passes over j.
+// ---------------------------------------------------------------------------
+// grid.z = kSplit channel slices; slice z writes part[z][b][j][m] (summed by
+// offset_conv_combine in a fixed order: the offsets are bitwise reproducible).
+constexpr int kSplit = 4;
+
+template <int KK>
+__global__ __launch_bounds__(256) void offset_conv_fwd_valu(Geo g, const float* __restrict__ x,
+                                                           const float* __restrict__ wt,
+                                                           float* __restrict__ part) {
+  const long Mtot = (long)g.B * g.HW;
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  const bool pok = p < Mtot;
+  const int b = pok ? (int)(p / g.HW) : 0;
+  const int m = pok ? (int)(p - (long)b * g.HW) : 0;
+  const int ho = m / g.Wo, wo = m - (m / g.Wo) * g.Wo;
+  int offs[KK];
+#pragma unroll
+  for (int t = 0; t < KK; ++t) {
+    const int i = t / g.kw, kx = t - i * g.kw;
+    const int y = ho * g.sh - g.ph + i * g.dh, xx = wo * g.sw - g.pw + kx * g.dw;
+    offs[t] = (pok && y >= 0 && y < g.H && xx >= 0 && xx < g.W) ? y * g.W + xx : -1;
+  }
+  const int j0 = blockIdx.y * kJB;
+  const int jn = min(kJB, g.J - j0);
+  const int Jp = pad_j(g.J);
+  float acc[kJB];
+#pragma unroll
+  for (int jj = 0; jj < kJB; ++jj) acc[jj] = 0.f;
+  const float* xb = x + (size_t)b * g.C * g.HWi;
+  const int cper = (g.C + kSplit - 1) / kSplit;
+  const int cbeg = blockIdx.z * cper, cend = min(g.C, cbeg + cper);
+#pragma unroll 2
+  for (int c = cbeg; c < cend; ++c) {
+    const float* xc = xb + (size_t)c * g.HWi;
+    float v[KK];
+#pragma unroll
+    for (int t = 0; t < KK; ++t) v[t] = offs[t] >= 0 ? xc[offs[t]] : 0.f;
+#pragma unroll
+    for (int t = 0; t < KK; ++t) {
+      const float* w = wt + ((size_t)c * KK + t) * Jp + j0;  // wave-uniform, zero-padded
+#pragma unroll
+      for (int jj = 0; jj < kJB; ++jj) acc[jj] = fmaf(v[t], w[jj], acc[jj]);
+    }
+  }
+  if (!pok) return;
+  float* pz = part + (size_t)blockIdx.z * g.B * g.J * g.HW;
+#pragma unroll
+  for (int jj = 0; jj < kJB; ++jj)
+    if (jj < jn) pz[((size_t)b * g.J + j0 + jj) * g.HW + m] = acc[jj];
+}
+
+__global__ __launch_bounds__(256) void offset_conv_combine(const float* __restrict__ part,
+                                                          const float* __restrict__ b_off,
+                                                          float* __restrict__ off, int J, int HW,
+                                                          long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float v = b_off[(i / HW) % J];
+#pragma unroll
+  for (int z = 0; z < kSplit; ++z) v += part[(size_t)z * n + i];
+  off[i] = v;
+}
+
+constexpr int kWgradPpw = 256;  // pixels per wave in offset_wgrad_valu
+
+struct WgradGrid {
+  unsigned nbx, ny, nz;
+  int cper;  // channels per wave (64 lanes x VEC)
+};
+static WgradGrid wgrad_grid(const Geo& g) {
+  const long waves = ((long)g.B * g.HW + kWgradPpw - 1) / kWgradPpw;
+  WgradGrid w;
+  w.cper = g.C % 4 == 0 ? 256 : 64;
+  w.nbx = (unsigned)((waves + 3) / 4);
+  w.ny = (unsigned)(g.kh * g.kw * ((g.J + kJB - 1) / kJB));
+  w.nz = (unsigned)((g.C + w.cper - 1) / w.cper);
+  return w;
+}
+static size_t goffT_rows_floats(const Geo& g) {
+  return ((size_t)g.B * g.HW * pad_j(g.J) + 63) / 64 * 64;
+}
+
+// ---------------------------------------------------------------------------
+// K7a: ∂w_off[j][c][tap] += Σ_p ∂off[b][j][p] · x[b][c][tap-shifted p]
+// One wave = (tap, j pass, 64*VEC-channel chunk, pixel range); lane = VEC channels
+// (xT rows, 1 KiB per wave load at VEC=4); ∂offT[p][j0..] is wave-uniform (scalar).
+// ---------------------------------------------------------------------------
+template <int VEC>
+__global__ __launch_bounds__(256) void offset_wgrad_valu(Geo g, const float* __restrict__ xT,
                                                          const float* __restrict__ goffT,
-                                                         float* __restrict__ gw, int ppw) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hi = lane >> 5, l31 = lane & 31;
+                                                         float* __restrict__ part, int ppw) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably wave-uniform
+  const int KK = g.kh * g.kw;
+  const int Jp = pad_j(g.J);
+  const int tap = blockIdx.y % KK, j0 = (blockIdx.y / KK) * kJB;
+  const int c = (blockIdx.z * 64 + lane) * VEC;
+  const bool cok = c < g.C;
   const long Mtot = (long)g.B * g.HW;
   const long pstart = ((long)blockIdx.x * 4 + wave) * ppw;
-  if (pstart >= Mtot) return;
-  const long pend = min(pstart + (long)ppw, Mtot);
-  const int KK = g.kh * g.kw;
-  const int tap = blockIdx.z % KK, j0 = (blockIdx.z / KK) * 32;
+  const long pend = max(pstart, min(pstart + (long)ppw, Mtot));  // empty for tail waves
   const int ti = tap / g.kw, tx = tap - ti * g.kw;
   const int dyo = ti * g.dh - g.ph, dxo = tx * g.dw - g.pw;
-  const int c = blockIdx.y * 32 + l31;
-  const bool cok = c < g.C;
-  const bool jok = j0 + l31 < g.J;
-  long p = pstart + hi;
-  int b = (int)(p / g.HW);
-  int mm = (int)(p - (long)b * g.HW);
-  int ho = mm / g.Wo, wo = mm - ho * g.Wo;
-  f32x16 acc = {0};
-  // 8 pixel pairs per batch: all 16 loads issued before the 8 MFMAs consume them
-  constexpr int U = 8;
-  for (long q0 = pstart; q0 < pend; q0 += 2 * U) {
-    float a[U], bv[U];
+  int b = (int)(pstart / g.HW);
+  int mm = (int)(pstart - (long)b * g.HW);
+  int ho = mm / g.Wo, wo = mm - (mm / g.Wo) * g.Wo;
+  float acc[kJB][VEC];
+#pragma unroll
+  for (int jj = 0; jj < kJB; ++jj)
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) acc[jj][e] = 0.f;
+  // 4-pixel batches: the batch's xT rows (1 KiB each) and ∂offT rows (scalar) are all
+  // in flight before its 4*kJB*VEC FMAs consume them
+  constexpr int U = 4;
+  for (long p0 = pstart; p0 < pend; p0 += U) {
+    float v[U][VEC];
+    const float* gp[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      a[u] = 0.f;
-      bv[u] = 0.f;
-      if (q0 + 2 * u + hi < pend) {
-        const size_t pix = (size_t)b * g.HW + (size_t)ho * g.Wo + wo;
-        if (jok) a[u] = goffT[pix * g.J + j0 + l31];
-        const int y = ho * g.sh + dyo, xx = wo * g.sw + dxo;
-        if (cok && y >= 0 && y < g.H && xx >= 0 && xx < g.W)
-          bv[u] = xT[(((size_t)b * g.H + y) * g.W + xx) * g.C + c];
+      const long p = p0 + u;
+      const int y = ho * g.sh + dyo, xx = wo * g.sw + dxo;
+      const bool ok = p < pend && y >= 0 && y < g.H && xx >= 0 && xx < g.W;  // wave-uniform
+      gp[u] = goffT + (size_t)(p < pend ? p : pstart) * Jp + j0;  // wave-uniform, zero-padded
+      const float* src = xT + (((size_t)b * g.H + (ok ? y : 0)) * g.W + (ok ? xx : 0)) * g.C + c;
+      if constexpr (VEC == 4) {
+        float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ok && cok) t = *reinterpret_cast<const float4*>(src);
+        v[u][0] = t.x;
+        v[u][1] = t.y;
+        v[u][2] = t.z;
+        v[u][3] = t.w;
+      } else {
+        v[u][0] = (ok && cok) ? *src : 0.f;
       }
-      wo += 2;
-      if (wo >= g.Wo) {
-        wo -= g.Wo;
-        if (++ho >= g.Ho) {
+      if (++wo == g.Wo) {
+        wo = 0;
+        if (++ho == g.Ho) {
           ho = 0;
           ++b;
         }
       }
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) acc = mfma32(a[u], bv[u], acc);
-  }
-  if (!cok) return;
+    for (int u = 0; u < U; ++u)
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int j = j0 + drow(r, hi);
-    if (j < g.J) atomicAdd(gw + ((size_t)j * g.C + c) * KK + tap, acc[r]);
+      for (int jj = 0; jj < kJB; ++jj) {
+        const float gv = gp[u][jj];
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) acc[jj][e] = fmaf(gv, v[u][e], acc[jj][e]);
+      }
   }
+  // The block's 4 waves cover consecutive pixel ranges of the same (tap, j pass, chunk):
+  // fold waves 1..3 into wave 0 through LDS (fixed order), then write one partial per
+  // block; wgrad_reduce sums the partials in block order. No float atomics, so ∂w_off is
+  // bitwise reproducible (device-scope atomics from 8 XCDs also serialised badly here).
+  constexpr int R = 6;  // accumulator rows per LDS round
+  __shared__ float red[3][R][VEC][64];
+#pragma unroll
+  for (int r0 = 0; r0 < kJB; r0 += R) {
+    if (wave > 0)
+#pragma unroll
+      for (int jr = 0; jr < R; ++jr)
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) red[wave - 1][jr][e][lane] = acc[r0 + jr][e];
+    __syncthreads();
+    if (wave == 0)
+#pragma unroll
+      for (int w = 0; w < 3; ++w)
+#pragma unroll
+        for (int jr = 0; jr < R; ++jr)
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) acc[r0 + jr][e] += red[w][jr][e][lane];
+    __syncthreads();
+  }
+  if (wave != 0) return;
+  constexpr int E = kJB * VEC * 64;
+  float* pb = part + ((size_t)(blockIdx.y * gridDim.z + blockIdx.z) * gridDim.x + blockIdx.x) * E;
+#pragma unroll
+  for (int jj = 0; jj < kJB; ++jj)
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) pb[(jj * VEC + e) * 64 + lane] = acc[jj][e];
 }
 
-// ∂x[b][c][y][x] += Σ_{j,tap} w_off[j][c][tap] · ∂off[b][j][(y+pad-tap·dil)/s]
-// D[c (32)][input pixel (32)]; A = w_off slice staged in LDS [j][tap][c]; B = ∂off.
-// Each wave: 2 tiles of 32 input pixels; each tile's outputs are owned (RMW, no atomics).
-template <int S>
-__global__ __launch_bounds__(256) void offset_dgrad_mfma(Geo g, const float* __restrict__ w_off,
+// ∂w_off = Σ over pixel blocks of offset_wgrad_valu's partials, in block order. One
+// 1024-thread block per 64 partial elements: wave w sums blocks ≡ w (mod 16), then the
+// 16 wave sums are folded in wave order (deterministic).
+template <int VEC>
+__global__ __launch_bounds__(1024) void wgrad_reduce(Geo g, const float* __restrict__ part,
+                                                     float* __restrict__ gw, int nbx, int nz) {
+  constexpr int E = kJB * VEC * 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int idx = blockIdx.x * 64 + lane;  // element within E
+  const int yz = blockIdx.y;
+  const float* pp = part + (size_t)yz * nbx * E + idx;
+  float s = 0.f;
+#pragma unroll 4
+  for (int bx = w; bx < nbx; bx += 16) s += pp[(size_t)bx * E];
+  __shared__ float red[16][64];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w != 0) return;
+  s = red[0][lane];
+#pragma unroll
+  for (int k = 1; k < 16; ++k) s += red[k][lane];
+  const int KK = g.kh * g.kw;
+  const int y = yz / nz, z = yz - y * nz;
+  const int tap = y % KK, j0 = (y / KK) * kJB;
+  const int jj = idx / (VEC * 64), e = (idx / 64) % VEC;
+  const int c = (z * 64 + lane) * VEC + e;
+  if (j0 + jj < g.J && c < g.C) gw[((size_t)(j0 + jj) * g.C + c) * KK + tap] = s;
+}
+
+// ---------------------------------------------------------------------------
+// K7b: ∂x[b][c][y][x] += Σ_{j,tap} w_off[j][c][tap] · ∂off[b][j][(y+pad-tap·dil)/s]
+// One thread per input pixel and kCB channels (grid.y); weights wave-uniform.
+// ---------------------------------------------------------------------------
+template <int KK>
+__global__ __launch_bounds__(256) void offset_dgrad_valu(Geo g, const float* __restrict__ wt2,
                                                          const float* __restrict__ goff,
                                                          float* __restrict__ gx) {
-  constexpr int JC = Chunk<S>::v;
-  __shared__ float wl[JC * 2 * S * 33];  // [j][tap][c] (odd pitch)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hi = lane >> 5;
-  const int KK = g.kh * g.kw, KKp = 2 * S;
-  const int ct0 = blockIdx.y * 32;
   const long Mi = (long)g.B * g.HWi;
-  long pt[2];
-  bool pok[2];
-  int bb[2], yx[2], goffs[2][S];
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  const bool pok = p < Mi;
+  const int b = pok ? (int)(p / g.HWi) : 0;
+  const int yx = pok ? (int)(p - (long)b * g.HWi) : 0;
+  const int y = yx / g.W, xx = yx - (yx / g.W) * g.W;
+  int goffs[KK];
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    pt[t] = ((long)blockIdx.x * 8 + wave * 2 + t) * 32 + (lane & 31);
-    pok[t] = pt[t] < Mi;
-    bb[t] = pok[t] ? (int)(pt[t] / g.HWi) : 0;
-    yx[t] = pok[t] ? (int)(pt[t] - (long)bb[t] * g.HWi) : 0;
-    const int y = yx[t] / g.W, xx = yx[t] - (yx[t] / g.W) * g.W;
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      const int tap = 2 * s + hi;
-      goffs[t][s] = -1;
-      if (pok[t] && tap < KK) {
-        const int i = tap / g.kw, kx = tap - i * g.kw;
-        const int tt = y + g.ph - i * g.dh, u = xx + g.pw - kx * g.dw;
-        if (tt >= 0 && u >= 0 && tt % g.sh == 0 && u % g.sw == 0) {
-          const int ho = tt / g.sh, wo = u / g.sw;
-          if (ho < g.Ho && wo < g.Wo) goffs[t][s] = ho * g.Wo + wo;
-        }
-      }
+  for (int t = 0; t < KK; ++t) {
+    const int i = t / g.kw, kx = t - i * g.kw;
+    const int tt = y + g.ph - i * g.dh, u = xx + g.pw - kx * g.dw;
+    goffs[t] = -1;
+    if (pok && tt >= 0 && u >= 0 && tt % g.sh == 0 && u % g.sw == 0) {
+      const int ho = tt / g.sh, wo = u / g.sw;
+      if (ho < g.Ho && wo < g.Wo) goffs[t] = ho * g.Wo + wo;
     }
   }
-  const float* gb0 = goff + (size_t)bb[0] * g.J * g.HW;
-  const float* gb1 = goff + (size_t)bb[1] * g.J * g.HW;
-  f32x16 acc0 = {0}, acc1 = {0};
-  for (int jc = 0; jc < g.J; jc += JC) {
-    __syncthreads();
-    for (int e = tid; e < JC * KKp * 32; e += 256) {
-      const int jl = e / (KKp * 32), rem = e - jl * (KKp * 32);
-      const int cl = rem / KKp, tap = rem - cl * KKp;  // reads run along (c, tap) of one j
-      const int c = ct0 + cl, jj = jc + jl;
-      float v = 0.f;
-      if (jj < g.J && c < g.C && tap < KK) v = w_off[((size_t)jj * g.C + c) * KK + tap];
-      wl[(jl * KKp + tap) * 33 + cl] = v;
-    }
-    __syncthreads();
-    const int jn = min(JC, g.J - jc);
-    float v0[S], v1[S];
-    auto fetch = [&](int jl, float* d0, float* d1) {
-      const float* g0 = gb0 + (size_t)(jc + jl) * g.HW;
-      const float* g1 = gb1 + (size_t)(jc + jl) * g.HW;
+  const int c0 = blockIdx.y * kCB;
+  const int cn = min(kCB, g.C - c0);
+  const int Cp = pad_c(g.C);
+  float acc[kCB];
 #pragma unroll
-      for (int s = 0; s < S; ++s) {
-        d0[s] = goffs[0][s] >= 0 ? g0[goffs[0][s]] : 0.f;
-        d1[s] = goffs[1][s] >= 0 ? g1[goffs[1][s]] : 0.f;
-      }
-    };
-    fetch(0, v0, v1);
-    for (int jl = 0; jl < jn; ++jl) {
-      float n0[S], n1[S];
-      if (jl + 1 < jn) fetch(jl + 1, n0, n1);
+  for (int cc = 0; cc < kCB; ++cc) acc[cc] = 0.f;
+  const float* gb = goff + (size_t)b * g.J * g.HW;
+  for (int j = 0; j < g.J; ++j) {
+    const float* gj = gb + (size_t)j * g.HW;
+    float v[KK];
 #pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const float a = wl[(jl * KKp + 2 * s + hi) * 33 + (lane & 31)];
-        acc0 = mfma32(a, v0[s], acc0);
-        acc1 = mfma32(a, v1[s], acc1);
-      }
+    for (int t = 0; t < KK; ++t) v[t] = goffs[t] >= 0 ? gj[goffs[t]] : 0.f;
 #pragma unroll
-      for (int s = 0; s < S; ++s) {
-        v0[s] = n0[s];
-        v1[s] = n1[s];
-      }
+    for (int t = 0; t < KK; ++t) {
+      const float* w = wt2 + ((size_t)j * KK + t) * Cp + c0;  // wave-uniform, zero-padded
+#pragma unroll
+      for (int cc = 0; cc < kCB; ++cc) acc[cc] = fmaf(v[t], w[cc], acc[cc]);
     }
   }
+  if (!pok) return;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int c = ct0 + drow(r, hi);
-    if (c < g.C) {
-      if (pok[0]) gx[((size_t)bb[0] * g.C + c) * g.HWi + yx[0]] += acc0[r];
-      if (pok[1]) gx[((size_t)bb[1] * g.C + c) * g.HWi + yx[1]] += acc1[r];
-    }
-  }
+  for (int cc = 0; cc < kCB; ++cc)
+    if (cc < cn) gx[((size_t)b * g.C + c0 + cc) * g.HWi + yx] += acc[cc];
 }
 
-#define DCN_S_DISPATCH(SV, ...) \
-  switch (SV) {                  \
-    case 1: { constexpr int S = 1; __VA_ARGS__; } break; \
-    case 2: { constexpr int S = 2; __VA_ARGS__; } break; \
-    case 3: { constexpr int S = 3; __VA_ARGS__; } break; \
-    case 4: { constexpr int S = 4; __VA_ARGS__; } break; \
-    case 5: { constexpr int S = 5; __VA_ARGS__; } break; \
-    case 8: { constexpr int S = 8; __VA_ARGS__; } break; \
-    case 13: { constexpr int S = 13; __VA_ARGS__; } break; \
-    default: return hipErrorInvalidValue; \
+// ---------------------------------------------------------------------------
+// Generic fallbacks (kernel sizes without an instantiation): plain per-thread loops.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void offset_conv_fwd_generic(Geo g, const float* __restrict__ x,
+                                                              const float* __restrict__ w_off,
+                                                              const float* __restrict__ b_off,
+                                                              float* __restrict__ off) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)g.B * g.J * g.HW) return;
+  const int m = (int)(idx % g.HW);
+  const int j = (int)((idx / g.HW) % g.J), b = (int)(idx / ((long)g.HW * g.J));
+  const int ho = m / g.Wo, wo = m - ho * g.Wo;
+  float acc = 0.f;
+  for (int c = 0; c < g.C; ++c)
+    for (int i = 0; i < g.kh; ++i)
+      for (int k = 0; k < g.kw; ++k) {
+        const int y = ho * g.sh - g.ph + i * g.dh, xx = wo * g.sw - g.pw + k * g.dw;
+        if (y < 0 || y >= g.H || xx < 0 || xx >= g.W) continue;
+        acc = fmaf(w_off[(((size_t)j * g.C + c) * g.kh + i) * g.kw + k],
+                   x[((size_t)b * g.C + c) * g.HWi + y * g.W + xx], acc);
+      }
+  off[idx] = acc + b_off[j];
+}
+
+// one thread per (b, j, m): scatter into ∂x and ∂w_off with atomics
+__global__ __launch_bounds__(256) void offset_bwd_generic(Geo g, const float* __restrict__ x,
+                                                         const float* __restrict__ w_off,
+                                                         const float* __restrict__ goff,
+                                                         float* __restrict__ gx,
+                                                         float* __restrict__ gw) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)g.B * g.J * g.HW) return;
+  const int m = (int)(idx % g.HW);
+  const int j = (int)((idx / g.HW) % g.J), b = (int)(idx / ((long)g.HW * g.J));
+  const int ho = m / g.Wo, wo = m - ho * g.Wo;
+  const float gv = goff[idx];
+  for (int c = 0; c < g.C; ++c)
+    for (int i = 0; i < g.kh; ++i)
+      for (int k = 0; k < g.kw; ++k) {
+        const int y = ho * g.sh - g.ph + i * g.dh, xx = wo * g.sw - g.pw + k * g.dw;
+        if (y < 0 || y >= g.H || xx < 0 || xx >= g.W) continue;
+        const size_t wi = (((size_t)j * g.C + c) * g.kh + i) * g.kw + k;
+        const size_t xi = ((size_t)b * g.C + c) * g.HWi + y * g.W + xx;
+        atomicAdd(gw + wi, gv * x[xi]);
+        atomicAdd(gx + xi, gv * w_off[wi]);
+      }
+}
+
+#define DCN_KK_DISPATCH(KKV, ...) \
+  switch (KKV) {                   \
+    case 1: { constexpr int KKc = 1; __VA_ARGS__; } break; \
+    case 4: { constexpr int KKc = 4; __VA_ARGS__; } break; \
+    case 6: { constexpr int KKc = 6; __VA_ARGS__; } break; \
+    case 9: { constexpr int KKc = 9; __VA_ARGS__; } break; \
+    default: generic = true; break; \
   }
 
-static int slots_for(const Geo& g) {
-  int S = (g.kh * g.kw + 1) / 2;
-  if (S > 5 && S <= 8) S = 8;
-  else if (S > 8 && S <= 13) S = 13;
-  return S;
+size_t offset_conv_wt_floats(const Geo& g) {
+  const size_t KK = (size_t)g.kh * g.kw;
+  return std::max((size_t)pad_j(g.J) * g.C * KK, (size_t)g.J * KK * pad_c(g.C));
+}
+size_t offset_conv_fpart_floats(const Geo& g) { return (size_t)kSplit * g.B * g.J * g.HW; }
+
+// goffT rows, then offset_wgrad_valu's per-block partials.
+size_t offset_conv_goffT_floats(const Geo& g) {
+  const WgradGrid w = wgrad_grid(g);
+  return goffT_rows_floats(g) + (size_t)w.nbx * w.ny * w.nz * kJB * w.cper;
 }
 
 hipError_t launch_offset_conv_fwd(const Geo& g, const float* x, const float* w_off,
-                                  const float* b_off, float* off, hipStream_t s) {
+                                  const float* b_off, float* off, float* wt, float* part,
+                                  hipStream_t s) {
+  const int KK = g.kh * g.kw;
+  bool generic = false;
   const long Mtot = (long)g.B * g.HW;
-  const long tiles = (Mtot + 31) / 32;
-  dim3 grid((unsigned)((tiles + 7) / 8), (g.J + 31) / 32);
-  DCN_S_DISPATCH(slots_for(g), hipLaunchKernelGGL(offset_conv_fwd_mfma<S>, grid, dim3(256), 0,
-                                                  s, g, x, w_off, b_off, off));
+  const int n = pad_j(g.J) * g.C * KK;
+  hipLaunchKernelGGL(woff_to_ctj, dim3((n + 255) / 256), dim3(256), 0, s, w_off, wt, g.J,
+                     pad_j(g.J), g.C, KK);
+  dim3 grid((unsigned)((Mtot + 255) / 256), (g.J + kJB - 1) / kJB, kSplit);
+  DCN_KK_DISPATCH(KK, hipLaunchKernelGGL(offset_conv_fwd_valu<KKc>, grid, dim3(256), 0, s, g, x,
+                                         wt, part));
+  if (!generic) {
+    const long n = (long)g.B * g.J * g.HW;
+    hipLaunchKernelGGL(offset_conv_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       part, b_off, off, g.J, g.HW, n);
+  } else {
+    const long total = (long)g.B * g.J * g.HW;
+    hipLaunchKernelGGL(offset_conv_fwd_generic, dim3((unsigned)((total + 255) / 256)), dim3(256),
+                       0, s, g, x, w_off, b_off, off);
+  }
   return hipGetLastError();
 }
 
-// goffT: scratch [B][HW][J]; xT: channels-last x [B][H][W][C]. grad_x is accumulated.
-hipError_t launch_offset_conv_bwd(const Geo& g, const float* xT, const float* w_off,
-                                  const float* goff, float* goffT, float* gx, float* gw_off,
-                                  float* gb_off, hipStream_t s) {
+// xT: channels-last x; goffT, wt2: scratch ([B][HW][J], [J][KK][C]). grad_x is accumulated.
+hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
+                                  const float* w_off, const float* goff, float* goffT, float* wt2,
+                                  float* gx, float* gw_off, float* gb_off, hipStream_t s) {
   const int KK = g.kh * g.kw;
-  hipError_t e = hipMemsetAsync(gw_off, 0, (size_t)g.J * g.C * KK * sizeof(float), s);
-  if (e != hipSuccess) return e;
   launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
-  e = launch_nchw_to_nhwc(goff, goffT, g.B, g.J, g.HW, s);
-  if (e != hipSuccess) return e;
-  {
-    const long Mtot = (long)g.B * g.HW;
-    const int ppw = 2048;
-    const long waves = (Mtot + ppw - 1) / ppw;
-    dim3 grid((unsigned)((waves + 3) / 4), (g.C + 31) / 32, KK * ((g.J + 31) / 32));
-    hipLaunchKernelGGL(offset_wgrad_mfma, grid, dim3(256), 0, s, g, xT, goffT, gw_off, ppw);
+  bool generic = false;
+  DCN_KK_DISPATCH(KK, (void)KKc);
+  if (generic) {
+    hipError_t e = hipMemsetAsync(gw_off, 0, (size_t)g.J * g.C * KK * sizeof(float), s);
+    if (e != hipSuccess) return e;
+    const long total = (long)g.B * g.J * g.HW;
+    hipLaunchKernelGGL(offset_bwd_generic, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                       g, x, w_off, goff, gx, gw_off);
+    return hipGetLastError();
   }
   {
+    const long total = (long)g.B * pad_j(g.J) * g.HW;
+    hipLaunchKernelGGL(goff_to_pj, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, goff,
+                       goffT, g.J, pad_j(g.J), g.HW, total);
+  }
+  {
+    const WgradGrid w = wgrad_grid(g);
+    float* part = goffT + goffT_rows_floats(g);
+    dim3 grid(w.nbx, w.ny, w.nz), rgrid(kJB * w.cper / 64, w.ny * w.nz);
+    if (w.cper == 256) {
+      hipLaunchKernelGGL(offset_wgrad_valu<4>, grid, dim3(256), 0, s, g, xT, goffT, part, kWgradPpw);
+      hipLaunchKernelGGL(wgrad_reduce<4>, rgrid, dim3(1024), 0, s, g, part, gw_off, w.nbx, w.nz);
+    } else {
+      hipLaunchKernelGGL(offset_wgrad_valu<1>, grid, dim3(256), 0, s, g, xT, goffT, part, kWgradPpw);
+      hipLaunchKernelGGL(wgrad_reduce<1>, rgrid, dim3(1024), 0, s, g, part, gw_off, w.nbx, w.nz);
+    }
+  }
+  {
+    const int n = g.J * KK * pad_c(g.C);
+    hipLaunchKernelGGL(woff_to_jtc, dim3((n + 255) / 256), dim3(256), 0, s, w_off, wt2, g.J, g.C,
+                       pad_c(g.C), KK);
     const long Mi = (long)g.B * g.HWi;
-    const long tiles = (Mi + 31) / 32;
-    dim3 grid((unsigned)((tiles + 7) / 8), (g.C + 31) / 32);
-    DCN_S_DISPATCH(slots_for(g), hipLaunchKernelGGL(offset_dgrad_mfma<S>, grid, dim3(256), 0, s,
-                                                    g, w_off, goff, gx));
+    dim3 grid((unsigned)((Mi + 255) / 256), (g.C + kCB - 1) / kCB);
+    DCN_KK_DISPATCH(KK, hipLaunchKernelGGL(offset_dgrad_valu<KKc>, grid, dim3(256), 0, s, g, wt2,
+                                           goff, gx));
   }
   return hipGetLastError();
 }
