@@ -77,12 +77,25 @@ def cpu_baseline(cfg, budget_s=10.0, threads=None):
                       f"oracle/dcn_ref.c fp32 OpenMP, {el:.1f} s on {threads} of {ncpu} host threads"}
 
 
+K1_KERNEL = "dcn::im2col_lds"  # K1 on the channels-last path (deform_groups 1, C % 4 == 0)
+
+
 def load_traffic(path):
+    """HBM bytes per K1 launch from the newest committed PMC summary
+    (tools/pmc_pass.sh + tools/pmc_summary.py -> profiles/rNN_pmc_hbm.json)."""
+    import glob
+    paths = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_hbm.json")))
+    if not paths:
+        return None, None
     try:
-        with open(path) as f:
-            return json.load(f)
+        with open(paths[-1]) as f:
+            doc = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, None
+    for name, v in doc.get("kernels", {}).items():
+        if name.startswith(K1_KERNEL):
+            return int(v["hbm_bytes"]), f"{os.path.relpath(paths[-1], ROOT)}:{name}"
+    return None, None
 
 
 def main():
@@ -93,7 +106,8 @@ def main():
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_im2col.json"))
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC summary (default: newest profiles/r*_pmc_hbm.json)")
     args = ap.parse_args()
 
     import torch  # plumbing: HBM buffers, stream handle, torch.distributed (RCCL)
@@ -160,10 +174,6 @@ def main():
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    h.prof_enable(args.steps)  # HIP events around every libdcn launch, on `stream`
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -176,6 +186,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
+    # per-kernel durations: a second, separate pass of the same steps with HIP events
+    # around every libdcn launch on `stream` (kept out of the timed region above)
+    h.prof_enable(args.steps)
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
     kernel_ms = {}
     for name in rt.KERNEL_IDS:
         tot, cnt = h.prof_read(name)
@@ -188,7 +204,7 @@ def main():
     value = samples / el / 1e9
     if rank == 0:
         achieved = k1_b / (k1_ms * 1e-3) / 1e9 if k1_ms else None
-        traffic = load_traffic(args.traffic_json)
+        traffic, traffic_src = load_traffic(args.traffic_json)
         res = {
             "metric": METRIC,
             "value": round(value, 5),
@@ -208,13 +224,14 @@ def main():
                        "kernel": k, "stride": s, "padding": p,
                        "parallelism": f"dp{world} (batch-sharded, replicated params)"},
             "roofline": {
-                "kernel": "im2col_window<9> (K1, deformable bilinear im2col)",
+                "kernel": f"{K1_KERNEL} (K1, LDS-staged deformable bilinear im2col)",
                 "bound": "hbm",
                 "achieved": round(achieved, 1) if achieved else None,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                "traffic": traffic.get("bytes_per_launch") if traffic else None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "algorithmic_bytes": k1_b,
                 "avg_launch_ms": k1_ms,
             },

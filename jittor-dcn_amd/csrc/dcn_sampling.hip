@@ -18,11 +18,31 @@
 // (counting sort per image: int atomics on 28k samples/image), every bin list is
 // sorted, and each input pixel gathers the ∂col rows of the four bins whose 2x2
 // footprint covers it — a fixed summation order, so ∂x is bitwise reproducible.
+#include <climits>
+#include <cstdlib>
+
 #include "dcn_device.h"
 
 namespace dcn {
 
 static int g_force_generic = 0;
+
+// Development A/B knobs: DCN_EXP="a,b,..." -> exp_flag(i) (0 when unset). Speed only.
+static int exp_flag(int i) {
+  static int v[8] = {0};
+  static bool init = false;
+  if (!init) {
+    init = true;
+    if (const char* e = std::getenv("DCN_EXP")) {
+      for (int k = 0; k < 8 && *e; ++k) {
+        v[k] = std::atoi(e);
+        while (*e && *e != ',') ++e;
+        if (*e == ',') ++e;
+      }
+    }
+  }
+  return v[i];
+}
 void set_force_generic(int on) { g_force_generic = on; }
 int get_force_generic() { return g_force_generic; }
 
@@ -176,6 +196,123 @@ __global__ __launch_bounds__(256) void im2col_cl(Geo g, LaneMap L, const float* 
                                                           q[u].c, q[u].d)
                                                 : Vec<VEC>::zero();
         stv<VEC>(cb + (size_t)sm[u].m * g.K + (size_t)sm[u].n * g.C + c, v);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K1 (LDS-staged): one block = one kTH x kTW tile of output pixels of one image.
+// The block's samples (pixel-major, N taps each) are resolved once into LDS records;
+// then, per 64-channel slice, the xT window the tile's samples land in — the tile's
+// zero-offset footprint plus a MAR-pixel margin, zero outside the image — is staged in
+// LDS with coalesced 256-B row reads, and every sample's four corners come from LDS.
+// A sample whose corners leave the window (|offset| beyond the margin) reads them from
+// global memory instead; both paths compute the same canonical bilerp, so the columns
+// are bit-identical to im2col_cl's. Used for deform_groups == 1, N <= kMaxTaps,
+// C % 4 == 0 (the reference's own configuration space).
+// ---------------------------------------------------------------------------
+constexpr int kMaxTaps = 9;
+constexpr int kSkip = INT_MIN, kZero = INT_MIN + 1;  // record r0 markers
+
+template <int TH, int TW, int MAR>
+struct Win {
+  static constexpr int R = TW + 2 * MAR;  // window rows (input r follows output w, Q1)
+  static constexpr int Q = TH + 2 * MAR;  // window cols (input q follows output h)
+  static constexpr int PIX = R * Q;
+};
+
+template <int TH, int TW, int MAR, int CS, bool NT>
+__global__ __launch_bounds__(256) void im2col_lds(Geo g, const float* __restrict__ xT,
+                                                  const float* __restrict__ off,
+                                                  float* __restrict__ colT, int b0, int tw_n) {
+  typedef Win<TH, TW, MAR> Wn;
+  constexpr int kTP = TH * TW;
+  constexpr int LPS = CS / 4, GS = 256 / LPS;  // lanes per sample, samples per block step
+  __shared__ float4 win[Wn::PIX * LPS];
+  __shared__ int4 rec[kTP * kMaxTaps];
+  const int tid = threadIdx.x;
+  const Block3 blk = xcd_block();
+  const int bl = blk.z, b = b0 + bl;
+  const int th_i = blk.x / tw_n, tw_i = blk.x - th_i * tw_n;
+  const int h0 = th_i * TH, w0 = tw_i * TW;
+  // window origin: the tile's zero-offset footprint (grid_sample scale (H-1)/(Wo-1))
+  const int rlo = (int)floorf((float)w0 * (float)(g.H - 1) / (float)(g.Wo - 1)) - MAR;
+  const int qlo = (int)floorf((float)h0 * (float)(g.W - 1) / (float)(g.Ho - 1)) - MAR;
+  const int NSB = kTP * g.N;
+  for (int sidx = tid; sidx < NSB; sidx += 256) {
+    const int p = sidx / g.N, n = sidx - p * g.N;
+    const int h = h0 + p / TW, w = w0 + p % TW;
+    int4 r = make_int4(kSkip, 0, 0, 0);
+    if (h < g.Ho && w < g.Wo) {
+      const Tap t = sample_tap(g, off, b, 0, n, h * g.Wo + w);
+      r = t.ok ? make_int4(t.r0, t.c0, __float_as_int(t.fr), __float_as_int(t.fc))
+               : make_int4(kZero, 0, 0, 0);
+    }
+    rec[sidx] = r;
+  }
+  const float* xb = xT + (size_t)b * g.HWi * g.C;
+  float* cb = colT + (size_t)bl * g.HW * g.K;
+  const int grp = tid / LPS, cl = tid % LPS;  // GS sample groups of LPS lanes
+  for (int cs = 0; cs < g.C; cs += CS) {
+    const int c = cs + cl * 4;
+    const bool cok = c < g.C;
+    __syncthreads();  // records ready / previous slice consumed
+    {
+      constexpr int TOT = Wn::PIX * LPS, IT = (TOT + 255) / 256;
+      float4 v[IT];
+#pragma unroll
+      for (int k = 0; k < IT; ++k) {
+        const int idx = tid + k * 256;
+        const int pix = idx / LPS, l = idx % LPS;
+        const int rr = pix / Wn::Q, qq = pix - rr * Wn::Q;
+        const int r = rlo + rr, q = qlo + qq, cc = cs + l * 4;
+        const bool ok = idx < TOT && r >= 0 && r < g.H && q >= 0 && q < g.W && cc < g.C;
+        v[k] = ok ? *reinterpret_cast<const float4*>(xb + ((size_t)r * g.W + q) * g.C + cc)
+                  : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int k = 0; k < IT; ++k)
+        if (tid + k * 256 < TOT) win[tid + k * 256] = v[k];
+    }
+    __syncthreads();
+    for (int s = grp; s < NSB; s += GS) {
+      const int4 r = rec[s];
+      if (r.x == kSkip) continue;
+      const int p = s / g.N, n = s - p * g.N;
+      const int m = (h0 + p / TW) * g.Wo + w0 + p % TW;
+      float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r.x != kZero) {
+        const float fr = __int_as_float(r.z), fc = __int_as_float(r.w);
+        const int rr = r.x - rlo, qq = r.y - qlo;
+        float4 a, bq, cq, d;
+        if (rr >= 0 && rr + 1 < Wn::R && qq >= 0 && qq + 1 < Wn::Q) {
+          const float4* w4 = win + (rr * Wn::Q + qq) * LPS + cl;
+          a = w4[0];
+          bq = w4[LPS];
+          cq = w4[Wn::Q * LPS];
+          d = w4[(Wn::Q + 1) * LPS];
+        } else {  // outside the staged window: global corner reads
+          const bool r0ok = r.x >= 0, r1ok = r.x + 1 < g.H, c0ok = r.y >= 0, c1ok = r.y + 1 < g.W;
+          const float* p00 = xb + ((long)r.x * g.W + r.y) * (long)g.C + c;
+          const long rs = (long)g.W * g.C;
+          a = ldv<4>(p00, cok && r0ok && c0ok);
+          bq = ldv<4>(p00 + g.C, cok && r0ok && c1ok);
+          cq = ldv<4>(p00 + rs, cok && r1ok && c0ok);
+          d = ldv<4>(p00 + rs + g.C, cok && r1ok && c1ok);
+        }
+        o = bilerp4(fr, fc, a, bq, cq, d);
+      }
+      if (cok) {
+        float4* dst = reinterpret_cast<float4*>(cb + (size_t)m * g.K + (size_t)n * g.C + c);
+        if constexpr (NT) {
+          __builtin_nontemporal_store(o.x, &dst->x);
+          __builtin_nontemporal_store(o.y, &dst->y);
+          __builtin_nontemporal_store(o.z, &dst->z);
+          __builtin_nontemporal_store(o.w, &dst->w);
+        } else {
+          *dst = o;
+        }
       }
     }
   }
@@ -607,6 +744,25 @@ hipError_t launch_im2col(const Geo& g, const float* x, const float* xT, const fl
     const long total = (long)nb * g.HW * g.K;
     hipLaunchKernelGGL(im2col_generic, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, g,
                        x, off, colT, b0, nb);
+    return hipGetLastError();
+  }
+  if (g.G == 1 && g.N <= kMaxTaps && g.C % 4 == 0) {
+    auto go = [&](auto kern, int TH, int TW) {
+      const int th_n = (g.Ho + TH - 1) / TH, tw_n = (g.Wo + TW - 1) / TW;
+      hipLaunchKernelGGL(kern, dim3(th_n * tw_n, 1, nb), dim3(256), 0, s, g, xT, off, colT, b0,
+                         tw_n);
+    };
+    // Measured at config 3 (r01 A/B): whole 1-KiB column rows per wave instruction
+    // (4x4 tile, all 256 channels, 1-px margin, non-temporal column stores) 0.418 ms;
+    // 8x8 tile x 64-ch slices 0.441; margin 2/3 windows slower (LDS occupancy).
+    if (g.C <= 32)
+      go(im2col_lds<8, 8, 2, 32, true>, 8, 8);
+    else if (g.C <= 64)
+      go(im2col_lds<8, 8, 2, 64, true>, 8, 8);
+    else if (g.C <= 128)
+      go(im2col_lds<4, 4, 1, 128, true>, 4, 4);
+    else
+      go(im2col_lds<4, 4, 1, 256, true>, 4, 4);
     return hipGetLastError();
   }
   const int NS = g.HW * g.N;

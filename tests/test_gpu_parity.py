@@ -181,15 +181,22 @@ def test_all_samples_out_of_image(gpu_handle):
     _check(out, off, g, ro, roff, rg, True, "all OOB")
 
 
-def test_channels_last_kernels_match_generic_kernels(gpu_handle):
-    """The channels-last K1/K5 (transpose, lane maps, sample bins + gather) and the
-    independent generic kernels (NCHW gathers, global atomics) agree: columns bit for bit
-    (same fp32 op order), ∂offset and ∂x to rounding (different summation orders)."""
+@pytest.mark.parametrize("C,H,W,s,off_scale", [
+    (24, 30, 26, (1, 1), 2.0),
+    (100, 21, 19, (1, 1), 2.5),   # partial 64-channel LDS slice, ragged 8x8 tiles
+    (68, 23, 25, (2, 2), 1.5),    # stride 2: window scale (H-1)/(Wo-1) ~ 2
+    (8, 17, 17, (1, 1), 6.0),     # most samples leave the staged window (global path)
+])
+def test_channels_last_kernels_match_generic_kernels(gpu_handle, C, H, W, s, off_scale):
+    """The channels-last K1/K5 (LDS-staged window + global fallback, lane maps, sample
+    bins + gather) and the independent generic kernels (NCHW gathers, global atomics)
+    agree: columns bit for bit (same fp32 op order), ∂offset and ∂x to rounding
+    (different summation orders)."""
     h = gpu_handle
-    c = _rand_case(51, B=3, C=24, O_=4, H=30, W=26, s=(1, 1), off_scale=2.0)
+    c = _rand_case(51, B=3, C=C, O_=4, H=H, W=W, s=s, off_scale=off_scale)
     x, wo, bo = c["x"], c["w_off"], c["b_off"]
     B, C, H, W = x.shape
-    desc = rt.make_desc(B, C, H, W, 4, (3, 3), (1, 1), (1, 1))
+    desc = rt.make_desc(B, C, H, W, 4, (3, 3), s, (1, 1))
     Ho, Wo = rt.out_shape(desc)
     K, HW = 9 * C, Ho * Wo
     rng = np.random.default_rng(5)
