@@ -105,6 +105,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--comm", choices=("torch", "libdcn"), default="torch",
+                    help="gradient all-reduce transport for N>1: torch.distributed (RCCL) or "
+                         "libdcn's own RCCL communicator (dcn_allreduce_grads)")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (default: newest profiles/r*_pmc_hbm.json)")
@@ -113,6 +116,7 @@ def main():
     import torch  # plumbing: HBM buffers, stream handle, torch.distributed (RCCL)
     import torch.distributed as dist
 
+    import dcn_dp
     import dcn_runtime as rt
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -146,10 +150,11 @@ def main():
     out = torch.empty(B, O_, Ho, Wo, device=dev)
     off = torch.empty(B, J, Ho, Wo, device=dev)
     gx = torch.empty_like(x)
-    # all parameter grads packed in ONE buffer -> one all-reduce per step
-    n_w, n_b, n_wo, n_bo = w.numel(), b.numel(), w_off.numel(), b_off.numel()
-    gflat = torch.empty(n_w + n_b + n_wo + n_bo, device=dev)
-    gw, gb, gwo, gbo = torch.split(gflat, [n_w, n_b, n_wo, n_bo])
+    # all parameter grads packed in ONE buffer -> one all-reduce per step (dcn_dp)
+    gbuf = dcn_dp.GradBuffer(dcn_dp.param_shapes(C, O_, k, k),
+                             lambda n: torch.empty(n, device=dev))
+    gflat = gbuf.flat
+    gw, gb, gwo, gbo = (gbuf[n] for n in dcn_dp.PARAM_ORDER)
     goff = torch.empty_like(off)
     wsb = rt.workspace_bytes(desc, True)
     ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
@@ -159,6 +164,17 @@ def main():
     h.set_stream(stream.cuda_stream)
     L = h.lib
     P = lambda t: t.data_ptr()
+    comm = None
+    if world > 1 and args.comm == "libdcn":
+        uid = [dcn_dp.RcclComm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = dcn_dp.RcclComm(h, world, rank, uid[0])
+
+    def allreduce():
+        if comm is not None:
+            comm.allreduce(gflat.data_ptr(), gflat.numel())  # on the handle's stream
+        else:
+            dcn_dp.allreduce_torch(gflat)  # RCCL over xGMI: 2.53 MB of fp32 grads
 
     def step():
         rt.check(L.dcn_forward(h.h, desc, P(x), P(w_off), P(b_off), P(w), P(b), P(out), P(off),
@@ -167,7 +183,7 @@ def main():
                                 P(gb), P(gwo), P(gbo), P(goff), P(ws), wsb, rt.DCN_BWD_COL_IN_WS),
                  "dcn_backward")
         if world > 1:
-            dist.all_reduce(gflat)  # RCCL over xGMI: 2.53 MB of fp32 grads
+            allreduce()
 
     for _ in range(args.warmup):
         step()
@@ -222,7 +238,8 @@ def main():
                                    f"p{p} fp32 DeformConv2d fwd+bwd (+RCCL grad all-reduce if N>1)",
                        "global_batch": B * world, "B_per_gpu": B, "C": C, "O": O_, "H": H, "W": W,
                        "kernel": k, "stride": s, "padding": p,
-                       "parallelism": f"dp{world} (batch-sharded, replicated params)"},
+                       "parallelism": f"dp{world} (batch-sharded, replicated params)",
+                       "grad_allreduce": (args.comm if world > 1 else None)},
             "roofline": {
                 "kernel": f"{K1_KERNEL} (K1, LDS-staged deformable bilinear im2col)",
                 "bound": "hbm",
@@ -241,6 +258,8 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_budget)
         print(json.dumps(res), flush=True)
+    if comm is not None:
+        comm.close()
     h.close()
     if world > 1:
         dist.destroy_process_group()

@@ -41,7 +41,8 @@ typedef enum {
   DCN_ERR_UNSUPPORTED = -2, /* shape or dtype outside what the build supports */
   DCN_ERR_HIP = -3,         /* HIP runtime error (no device, OOM, launch) */
   DCN_ERR_BLAS = -4,        /* rocBLAS error */
-  DCN_ERR_WORKSPACE = -5    /* caller workspace too small */
+  DCN_ERR_WORKSPACE = -5,   /* caller workspace too small */
+  DCN_ERR_COMM = -6         /* RCCL missing or a collective failed */
 } dcn_status;
 
 typedef enum { DCN_F32 = 0, DCN_BF16 = 1 } dcn_dtype;
@@ -163,6 +164,20 @@ int dcn_prof_enable(dcn_handle* h, int capacity);
 /* Sum of elapsed ms and number of recorded launches (synchronises first). */
 int dcn_prof_read(dcn_handle* h, int kernel_id, double* total_ms, int* count);
 int dcn_prof_reset(dcn_handle* h);
+
+/* ---- data-parallel gradient exchange (RCCL over xGMI) ------------------------- *
+ * Batch-sharded DP: every rank runs dcn_forward/dcn_backward on its own
+ * images, then sums the packed parameter gradients once per step. The reference is
+ * single-device (train.py:414), so these have no reference counterpart. One rank calls
+ * dcn_comm_get_unique_id and ships the 128 bytes to the others (any channel); every
+ * rank then calls dcn_comm_init with its own handle. RCCL is loaded on first use. */
+#define DCN_COMM_ID_BYTES 128
+typedef struct dcn_comm dcn_comm;
+int dcn_comm_get_unique_id(void* id /* DCN_COMM_ID_BYTES */);
+int dcn_comm_init(dcn_handle* h, int nranks, int rank, const void* id, dcn_comm** out);
+int dcn_comm_destroy(dcn_comm* c);
+/* In-place sum over ranks of `count` fp32 device values, on the handle's stream. */
+int dcn_allreduce_grads(dcn_handle* h, dcn_comm* c, float* grads, size_t count);
 
 /* ---- testing ------------------------------------------------------------------ */
 /* 1 = route K1/K5 through the generic global-gather kernels (independent

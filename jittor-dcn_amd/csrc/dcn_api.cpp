@@ -637,7 +637,17 @@ int dcn_prof_reset(dcn_handle* h) {
   return DCN_OK;
 }
 
-// Test hook (not in dcn.h): force the generic global-memory im2col/col2im kernels.
+// Internal hooks for dcn_comm.cpp (not in dcn.h).
+__attribute__((visibility("hidden"))) int dcn_internal_fail(int code, const char* msg) {
+  return fail(code, msg);
+}
+__attribute__((visibility("hidden"))) int dcn_internal_bind(dcn_handle* h, void** stream) {
+  DCN_TRY(set_device(h));
+  *stream = h->stream;
+  return DCN_OK;
+}
+
+// Test hook: force the generic global-memory im2col/col2im kernels.
 int dcn_debug_force_generic(int on) {
   dcn::set_force_generic(on);
   return DCN_OK;

@@ -28,7 +28,7 @@ namespace dcn {
 static int g_force_generic = 0;
 
 // Development A/B knobs: DCN_EXP="a,b,..." -> exp_flag(i) (0 when unset). Speed only.
-static int exp_flag(int i) {
+[[maybe_unused]] static int exp_flag(int i) {
   static int v[8] = {0};
   static bool init = false;
   if (!init) {

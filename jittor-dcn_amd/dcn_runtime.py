@@ -63,6 +63,10 @@ SIGNATURES = {
     "dcn_prof_enable": [_vp, ctypes.c_int],
     "dcn_prof_read": [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), _ip],
     "dcn_prof_reset": [_vp],
+    "dcn_comm_get_unique_id": [_vp],
+    "dcn_comm_init": [_vp, ctypes.c_int, ctypes.c_int, _vp, ctypes.POINTER(_vp)],
+    "dcn_comm_destroy": [_vp],
+    "dcn_allreduce_grads": [_vp, _vp, _vp, _sz],
     "dcn_debug_force_generic": [ctypes.c_int],
 }
 _RESTYPES = {"dcn_last_error": ctypes.c_char_p}

@@ -272,3 +272,21 @@ def test_config3_full_size_properties(gpu_handle):
         halves.append(_device_fwd_bwd(h, sub)[2])
     for k in ("weight", "bias", "offset_conv.weight", "offset_conv.bias"):
         assert_close_reduction(g[k], halves[0][k] + halves[1][k], tol=2e-5, what=f"linearity ∂{k}")
+
+
+def test_rccl_comm_single_rank_allreduce(gpu_handle):
+    """libdcn's RCCL communicator (dcn_comm_* / dcn_allreduce_grads) on a 1-rank world:
+    the in-place sum is the identity, on the handle's stream."""
+    import dcn_dp
+    h = gpu_handle
+    uid = dcn_dp.RcclComm.unique_id()
+    comm = dcn_dp.RcclComm(h, 1, 0, uid)
+    D = Dev(h)
+    try:
+        g = np.random.default_rng(3).standard_normal(631_570).astype(np.float32)
+        p = D.up(g)
+        comm.allreduce(p, g.size)
+        np.testing.assert_array_equal(D.down(p, g.shape), g)
+    finally:
+        comm.close()
+        D.free()
