@@ -290,3 +290,15 @@ def test_rccl_comm_single_rank_allreduce(gpu_handle):
     finally:
         comm.close()
         D.free()
+
+
+def test_forward_backward_bitwise_reproducible(gpu_handle):
+    """No float atomics on the channels-last path (integer bin counts, fixed-order
+    partial sums and shuffle trees): two runs give identical bits."""
+    c = _rand_case(71, B=4, C=64, O_=32, H=28, W=28, off_scale=1.5)
+    r1 = _device_fwd_bwd(gpu_handle, c)
+    r2 = _device_fwd_bwd(gpu_handle, c)
+    np.testing.assert_array_equal(r1[0], r2[0])
+    np.testing.assert_array_equal(r1[1], r2[1])
+    for k in r1[2]:
+        np.testing.assert_array_equal(r1[2][k], r2[2][k], err_msg=k)
