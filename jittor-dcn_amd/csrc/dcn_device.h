@@ -112,6 +112,25 @@ __device__ __forceinline__ Block3 xcd_block() {
   return o;
 }
 
+// Sum of v over the 64 lanes of a wave, on the VALU (DPP), result wave-uniform: pairs and
+// quads (quad_perm), half rows and rows (row_half_mirror, row_mirror), then rows
+// 0+1 / 2+3 (row_bcast:15) and halves (row_bcast:31) into lane 63. Fixed order:
+// deterministic. (gfx9-family DPP; no LDS round trips unlike __shfl_xor.)
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(
+      __builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWMASK, 0xf, false));
+}
+__device__ __forceinline__ float wave_sum(float v) {
+  v += dpp_f<0xB1>(v);        // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);        // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);       // row_half_mirror
+  v += dpp_f<0x140>(v);       // row_mirror
+  v += dpp_f<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+  v += dpp_f<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }

@@ -497,6 +497,190 @@ __global__ __launch_bounds__(256) void bins_sort(int NB, int NS, long nbins,
   }
 }
 
+// ---------------------------------------------------------------------------
+// K5 fused (∂x + ∂offset from ONE pass over the binned ∂col rows).
+// One block = a kTR x kTQ tile of INPUT pixels of one image and kTR+1 waves. Bin
+// (br, bc) holds the samples whose top-left corner is (br-1, bc-1) (K5b); wave w walks
+// bin row br = R0+w (bin columns Q0..Q0+kTQ, samples in sorted order), reading each
+// ∂colT row once, and accumulates into the two pixel rows that bin row touches: r0
+// (tile row w-1, weight 1-fr) and r0+1 (tile row w, weight fr). The bin loop is
+// unrolled, so accumulator indices are static (registers). Tile row t is then wave t's
+// lower row + wave t+1's upper row, combined through LDS in that fixed order.
+// ∂offset of a sample is computed once, by the wave/block that owns its bin (bin corner
+// inside the tile; row/column -1 owned by the first tile), from the tile's
+// (kTR+1) x (kTQ+1) xT window staged in LDS (corners at row/column -1 are outside the
+// image: zero). ∂offset uses offgrad_cl's op order (per-lane channel sums, fixed xor
+// tree). Used for deform_groups == 1, C % 4 == 0, C <= 256.
+// ---------------------------------------------------------------------------
+constexpr int kTR = 4, kTQ = 4;  // tile rows x cols; kTR+1 waves per block
+constexpr int kC2iThreads = (kTR + 1) * 64;
+
+__device__ __forceinline__ float4 fma4(float w, float4 g, float4 a) {
+  return make_float4(fmaf(w, g.x, a.x), fmaf(w, g.y, a.y), fmaf(w, g.z, a.z), fmaf(w, g.w, a.w));
+}
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+template <int U>
+__global__ __launch_bounds__(kC2iThreads) void col2im_tile(Geo g, const float* __restrict__ xT,
+                                                           const int4* __restrict__ brec,
+                                                           const int* __restrict__ start,
+                                                           const float* __restrict__ gcolT,
+                                                           float* __restrict__ gxT,
+                                                           float* __restrict__ goff, int b0,
+                                                           int tq_n) {
+  constexpr int WR = kTR + 1, WQ = kTQ + 1;
+  constexpr int WIN = WR * WQ * 64, UPR = kTR * kTQ * 64;  // float4 slots
+  __shared__ float4 lds[WIN > UPR ? WIN : UPR];  // xT window, then the upper rows
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const Block3 blk = xcd_block();
+  const int bl = blk.z, b = b0 + bl;
+  const int tr_i = blk.x / tq_n, tq_i = blk.x - tr_i * tq_n;
+  const int R0 = tr_i * kTR, Q0 = tq_i * kTQ;
+  const int c = lane * 4;
+  const bool cok = c < g.C;
+  const float* xb = xT + (size_t)b * g.HWi * g.C;
+  // stage xT rows R0..R0+kTR, cols Q0..Q0+kTQ (zero outside the image)
+  for (int idx = tid; idx < WIN; idx += kC2iThreads) {
+    const int pix = idx >> 6, l = idx & 63;
+    const int r = R0 + pix / WQ, q = Q0 + pix % WQ, cc = l * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < g.H && q < g.W && cc < g.C)
+      v = *reinterpret_cast<const float4*>(xb + ((size_t)r * g.W + q) * g.C + cc);
+    lds[idx] = v;
+  }
+  __syncthreads();
+  const int NB = (g.H + 1) * (g.W + 1);
+  const int* st = start + (size_t)bl * (NB + 1);
+  const int4* rb = brec + (size_t)bl * g.HW * g.N;
+  const float* gb = gcolT + (size_t)bl * g.HW * g.K;
+  float* gob = goff + (size_t)b * g.J * g.HW;
+  const float sy = (float)(g.H - 1) / (float)(g.Wo - 1);
+  const float sx = (float)(g.W - 1) / (float)(g.Ho - 1);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 up[kTQ], dn[kTQ];  // pixel rows r0 (tile row w-1) and r0+1 (tile row w)
+#pragma unroll
+  for (int j = 0; j < kTQ; ++j) up[j] = dn[j] = z4;
+  const int br = R0 + w;  // bin row = r0 + 1
+  if (br <= g.H) {
+    const bool drow = w >= 1 || br == 0;  // owns the ∂offset of this bin row
+    // the row's bins (br, Q0..Q0+kTQ) are consecutive, so their records are one
+    // contiguous range: fetch it 64 records per vector load (lane l <- record l) and
+    // take each with v_readlane — no scalar-load round trip per sample
+    const int bin0 = br * (g.W + 1) + Q0;
+    const int nbin = min(kTQ, g.W - Q0) + 1;
+    int bst[kTQ + 2];
+#pragma unroll
+    for (int k = 0; k <= kTQ + 1; ++k) bst[k] = st[bin0 + min(k, nbin)];
+    const int rowlo = bst[0], rowhi = bst[nbin];
+    const int cc = cok ? c : 0;  // clamped channel: loads never need a guard
+    // Software pipeline over the row's records (contiguous across its bins): batch k+1's
+    // records (v_readlane from a 64-record page) and ∂colT rows are issued before batch
+    // k is consumed. Batches never straddle a bin, so each bin's compute keeps static
+    // accumulator indices while the prefetch flows across bin boundaries.
+    int p0 = rowlo;
+    int4 pg = p0 + lane < rowhi ? rb[p0 + lane] : make_int4(0, 0, 0, 0);
+    int4 nR[U];
+    float4 nx[U];
+    auto issue = [&](int ni) {
+      if (ni >= rowhi) return;
+      if (ni + U > p0 + 64) {  // next page (rows of more than 64 samples)
+        p0 = ni;
+        pg = p0 + lane < rowhi ? rb[p0 + lane] : make_int4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int l = min(ni + u, rowhi - 1) - p0;
+        nR[u] = make_int4(__builtin_amdgcn_readlane(pg.x, l), __builtin_amdgcn_readlane(pg.y, l),
+                          __builtin_amdgcn_readlane(pg.z, l), __builtin_amdgcn_readlane(pg.w, l));
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) nx[u] = *reinterpret_cast<const float4*>(gb + nR[u].x + cc);
+    };
+    issue(rowlo);
+#pragma unroll
+    for (int bj = 0; bj <= kTQ; ++bj) {
+      if (bj >= nbin) break;
+      const int bc = Q0 + bj;
+      const bool doff = drow && (bj >= 1 || bc == 0);
+      const int lo = bst[bj], hi = bst[bj + 1];
+      for (int i = lo; i < hi; i += U) {
+        int4 R[U];
+        float4 gv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          R[u] = nR[u];
+          gv[u] = cok ? nx[u] : z4;
+        }
+        issue(i + U < hi ? i + U : hi);  // next batch of this bin, else the next bin's first
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (i + u >= hi) break;
+          const float fr = __int_as_float(R[u].y), fc = __int_as_float(R[u].z);
+          const float gr = 1.0f - fr, gc = 1.0f - fc;
+          if (bj < kTQ) {
+            up[bj] = fma4(gr * fc, gv[u], up[bj]);
+            dn[bj] = fma4(fr * fc, gv[u], dn[bj]);
+          }
+          if (bj >= 1) {
+            up[bj - 1] = fma4(gr * gc, gv[u], up[bj - 1]);
+            dn[bj - 1] = fma4(fr * gc, gv[u], dn[bj - 1]);
+          }
+          if (doff) {
+            // corners (r0, c0) .. (r0+1, c0+1) at window (w-1, bj-1) .. (w, bj)
+            const float4* w4 = lds + ((w - 1) * WQ + (bj - 1)) * 64 + lane;
+            const bool rA = w >= 1, cA = bj >= 1;
+            const float4 a = (rA && cA) ? w4[0] : z4;
+            const float4 bq = rA ? w4[64] : z4;
+            const float4 cq = cA ? w4[WQ * 64] : z4;
+            const float4 d = w4[(WQ + 1) * 64];
+            float diy = 0.f, dix = 0.f;
+            acc_dgrad(fr, fc, gv[u], a, bq, cq, d, diy, dix);
+            diy = wave_sum(diy);
+            dix = wave_sum(dix);
+            if (lane == 0) {
+              gob[R[u].w] = diy * sy;
+              gob[(size_t)g.N * g.HW + R[u].w] = dix * sx;
+            }
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();  // window no longer read: reuse the LDS for the upper rows
+  if (w >= 1)
+#pragma unroll
+    for (int j = 0; j < kTQ; ++j) lds[((w - 1) * kTQ + j) * 64 + lane] = up[j];
+  __syncthreads();
+  const int r = R0 + w;
+  if (w < kTR && r < g.H && cok) {
+#pragma unroll
+    for (int j = 0; j < kTQ; ++j)
+      if (Q0 + j < g.W)
+        *reinterpret_cast<float4*>(gxT + (((size_t)b * g.H + r) * g.W + Q0 + j) * g.C + c) =
+            add4(dn[j], lds[(w * kTQ + j) * 64 + lane]);
+  }
+}
+
+// Binned samples as contiguous records for col2im_tile, in bin order:
+// {∂colT row offset m*K + n*C, fr, fc, ∂offset index n*HW + m}.
+__global__ __launch_bounds__(256) void bins_pack(Geo g, int nbg, const float4* __restrict__ rec,
+                                                 const int* __restrict__ start,
+                                                 const int* __restrict__ list,
+                                                 int4* __restrict__ brec) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const int NS = g.HW * g.N, NB = (g.H + 1) * (g.W + 1);
+  if (idx >= (long)nbg * NS) return;
+  const int bg = (int)(idx / NS), pos = (int)(idx - (long)bg * NS);
+  if (pos >= start[(size_t)bg * (NB + 1) + NB]) return;  // past the binned samples
+  const int sidx = list[idx];
+  const float4 R = rec[(size_t)bg * NS + sidx];
+  const int m = sidx / g.N, n = sidx - m * g.N;
+  brec[idx] = make_int4(m * g.K + n * g.C, __float_as_int(R.y), __float_as_int(R.z), n * g.HW + m);
+}
+
 // ∂xT[b][r][q][gi*Cg + c] = Σ over the samples of bins (r-1,q-1), (r-1,q), (r,q-1),
 // (r,q) of (their w11, w10, w01, w00 weight) · ∂colT row. One group of LP lanes per
 // input pixel. The group's lanes first fetch up to LP (bin entry -> sample -> weight,
@@ -734,6 +918,8 @@ size_t bins_ws_bytes(const Geo& g, int nb) {
   b = (b + 15) / 16 * 16;
   b += groups * NS * 16;       // rec
   b += groups * NS * 4;        // list
+  b = (b + 15) / 16 * 16;
+  b += groups * NS * 16;       // packed records (col2im_tile)
   return (b + 255) / 256 * 256;
 }
 
@@ -793,7 +979,8 @@ hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, co
   const bool v4 = can_vec4(g);
   const LaneMap L = lane_map(g.Cg, v4 ? 4 : 1);
   const int NS = g.HW * g.N;
-  {  // K5a: ∂offset
+  const bool fused = g.G == 1 && g.C % 4 == 0 && g.C <= 256 && exp_flag(2) == 0;
+  if (!fused) {  // K5a: ∂offset
     dim3 grid((NS + 255) / 256, g.G, nb);
     if (v4)
       hipLaunchKernelGGL(offgrad_cl<4>, grid, dim3(256), 0, s, g, L, xT, off, gcolT, goff, b0);
@@ -821,7 +1008,26 @@ hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, co
   const long nbins = (long)groups * NB;
   hipLaunchKernelGGL(bins_sort, dim3((unsigned)((nbins + 255) / 256)), dim3(256), 0, s, NB, NS,
                      nbins, start, list);
-  {  // gather ∂xT, then back to NCHW (overwrites gx for these images)
+  if (fused) {  // one pass over ∂colT: ∂xT tiles + ∂offset of the owned bins
+    // samples in no bin (every corner outside the image) have ∂offset 0
+    e = hipMemsetAsync(goff + (size_t)b0 * g.J * g.HW, 0, (size_t)nb * g.J * g.HW * sizeof(float),
+                       s);
+    if (e != hipSuccess) return e;
+    const size_t lend = (size_t)((char*)(list + groups * NS) - w);
+    int4* brec = reinterpret_cast<int4*>(w + (lend + 15) / 16 * 16);  // bins_ws_bytes layout
+    hipLaunchKernelGGL(bins_pack, dim3(gs), dim3(256), 0, s, g, (int)groups, rec, start, list,
+                       brec);
+    const int tr_n = (g.H + kTR - 1) / kTR, tq_n = (g.W + kTQ - 1) / kTQ;
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(tr_n * tq_n, 1, nb), dim3(kC2iThreads), 0, s, g, xT, brec,
+                         start, gcolT, gxT, goff, b0, tq_n);
+    };
+    // r01 A/B at config 3 (2-deep prefetch pipeline): U=2 0.92 ms col2im, U=4 0.93, U=8 1.50
+    switch (exp_flag(3)) {
+      case 1: go(col2im_tile<4>); break;
+      default: go(col2im_tile<2>);
+    }
+  } else {  // gather ∂xT, then back to NCHW (overwrites gx for these images)
     const int pix_per_block = 4 * L.SP;
     dim3 grid((g.HWi + pix_per_block - 1) / pix_per_block, g.G, nb);
     if (v4)
