@@ -8,6 +8,7 @@
 //            GEMM partials + deterministic sum), ∂col = Wᵀ·∂out, K5 col2im +
 //            coordinate gradient, offset-conv backward.
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -139,6 +140,24 @@ struct dcn_handle {
   std::vector<hipEvent_t> ev[DCN_K_COUNT];  // pairs: [2*i] start, [2*i+1] stop
   int prof_n[DCN_K_COUNT] = {0};
 };
+
+namespace dcn {
+int exp_flag(int i) {
+  static int v[8] = {0};
+  static bool init = false;
+  if (!init) {
+    init = true;
+    if (const char* e = std::getenv("DCN_EXP")) {
+      for (int k = 0; k < 8 && *e; ++k) {
+        v[k] = std::atoi(e);
+        while (*e && *e != ',') ++e;
+        if (*e == ',') ++e;
+      }
+    }
+  }
+  return (i >= 0 && i < 8) ? v[i] : 0;
+}
+}  // namespace dcn
 
 namespace {
 

@@ -73,6 +73,9 @@ int gemm_backend_of(GemmEngine* e, const GemmSpec& s);  // -1 untuned, 0 rocBLAS
 // Selection of the im2col / col2im implementation (tests force the generic
 // global-memory kernels to cross-check the channels-last ones).
 void set_force_generic(int on);
+// Development A/B knobs for speed experiments: DCN_EXP="a,b,..." -> exp_flag(i), 0 when
+// unset. Never changes results, only which of several equivalent kernels runs.
+int exp_flag(int i);
 int get_force_generic();
 
 }  // namespace dcn

@@ -63,7 +63,7 @@ __global__ __launch_bounds__(256) void goff_to_pj(const float* __restrict__ goff
 // ---------------------------------------------------------------------------
 // grid.z = kSplit channel slices; slice z writes part[z][b][j][m] (summed by
 // offset_conv_combine in a fixed order: the offsets are bitwise reproducible).
-constexpr int kSplit = 4;
+constexpr int kSplit = 8;
 
 template <int KK>
 __global__ __launch_bounds__(256) void offset_conv_fwd_valu(Geo g, const float* __restrict__ x,
@@ -111,6 +111,76 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_valu(Geo g, const float* 
     if (jj < jn) pz[((size_t)b * g.J + j0 + jj) * g.HW + m] = acc[jj];
 }
 
+// K3 fast path (column stride 1, column dilation 1): one thread = kPX consecutive output
+// pixels of a row, so each scalar-loaded weight feeds kPX FMAs and a channel's
+// KH x (kPX+KW-1) input patch is loaded once for kPX*KH*KW pixel-taps.
+template <int KH, int KW, int kPX>
+__global__ __launch_bounds__(256) void offset_conv_fwd_row(Geo g, const float* __restrict__ x,
+                                                          const float* __restrict__ wt,
+                                                          float* __restrict__ part, int gpr) {
+  constexpr int SPAN = kPX + KW - 1;
+  const long t = (long)blockIdx.x * 256 + threadIdx.x;  // (b, ho, group)
+  const long T = (long)g.B * g.Ho * gpr;
+  const bool tok = t < T;
+  const long tt = tok ? t : 0;
+  const int grp = (int)(tt % gpr);
+  const long bh = tt / gpr;
+  const int ho = (int)(bh % g.Ho), b = (int)(bh / g.Ho);
+  const int wo0 = grp * kPX;
+  const int x0 = wo0 - g.pw;  // input column of tap kx=0 for pixel wo0 (sw = dw = 1)
+  int rowoff[KH];
+  bool rowok[KH];
+#pragma unroll
+  for (int i = 0; i < KH; ++i) {
+    const int y = ho * g.sh - g.ph + i * g.dh;
+    rowok[i] = tok && y >= 0 && y < g.H;
+    rowoff[i] = rowok[i] ? y * g.W : 0;
+  }
+  bool colok[SPAN];
+#pragma unroll
+  for (int k = 0; k < SPAN; ++k) colok[k] = x0 + k >= 0 && x0 + k < g.W;
+  const int j0 = blockIdx.y * kJB;
+  const int jn = min(kJB, g.J - j0);
+  const int Jp = pad_j(g.J);
+  float acc[kPX][kJB];
+#pragma unroll
+  for (int q = 0; q < kPX; ++q)
+#pragma unroll
+    for (int jj = 0; jj < kJB; ++jj) acc[q][jj] = 0.f;
+  const float* xb = x + (size_t)b * g.C * g.HWi;
+  const int cper = (g.C + kSplit - 1) / kSplit;
+  const int cbeg = blockIdx.z * cper, cend = min(g.C, cbeg + cper);
+  for (int c = cbeg; c < cend; ++c) {
+    const float* xc = xb + (size_t)c * g.HWi + x0;
+    float v[KH][SPAN];
+#pragma unroll
+    for (int i = 0; i < KH; ++i)
+#pragma unroll
+      for (int k = 0; k < SPAN; ++k) v[i][k] = (rowok[i] && colok[k]) ? xc[rowoff[i] + k] : 0.f;
+#pragma unroll
+    for (int i = 0; i < KH; ++i)
+#pragma unroll
+      for (int kx = 0; kx < KW; ++kx) {
+        const float* w = wt + ((size_t)c * (KH * KW) + i * KW + kx) * Jp + j0;  // wave-uniform
+#pragma unroll
+        for (int jj = 0; jj < kJB; ++jj) {
+          const float wv = w[jj];
+#pragma unroll
+          for (int q = 0; q < kPX; ++q) acc[q][jj] = fmaf(v[i][q + kx], wv, acc[q][jj]);
+        }
+      }
+  }
+  if (!tok) return;
+  float* pz = part + (size_t)blockIdx.z * g.B * g.J * g.HW + ((size_t)b * g.J + j0) * g.HW +
+              (size_t)ho * g.Wo + wo0;
+#pragma unroll
+  for (int jj = 0; jj < kJB; ++jj)
+    if (jj < jn)
+#pragma unroll
+      for (int q = 0; q < kPX; ++q)
+        if (wo0 + q < g.Wo) pz[(size_t)jj * g.HW + q] = acc[q][jj];
+}
+
 __global__ __launch_bounds__(256) void offset_conv_combine(const float* __restrict__ part,
                                                           const float* __restrict__ b_off,
                                                           float* __restrict__ off, int J, int HW,
@@ -150,16 +220,21 @@ static size_t goffT_rows_floats(const Geo& g) {
 template <int VEC>
 __global__ __launch_bounds__(256) void offset_wgrad_valu(Geo g, const float* __restrict__ xT,
                                                          const float* __restrict__ goffT,
-                                                         float* __restrict__ part, int ppw) {
+                                                         float* __restrict__ part, int ppw,
+                                                         int nbx, int ny, int nz) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably wave-uniform
+  // 1-D grid, (tap, j pass) fastest: the KK tap blocks of one pixel range are neighbours
+  // in the XCD-aware order, so xT rows fetched for one tap are L2 hits for the others
+  const unsigned lid = xcd_block().x;
+  const int by = (int)(lid % ny), bx = (int)((lid / ny) % nbx), bz = (int)(lid / ny / nbx);
   const int KK = g.kh * g.kw;
   const int Jp = pad_j(g.J);
-  const int tap = blockIdx.y % KK, j0 = (blockIdx.y / KK) * kJB;
-  const int c = (blockIdx.z * 64 + lane) * VEC;
+  const int tap = by % KK, j0 = (by / KK) * kJB;
+  const int c = (bz * 64 + lane) * VEC;
   const bool cok = c < g.C;
   const long Mtot = (long)g.B * g.HW;
-  const long pstart = ((long)blockIdx.x * 4 + wave) * ppw;
+  const long pstart = ((long)bx * 4 + wave) * ppw;
   const long pend = max(pstart, min(pstart + (long)ppw, Mtot));  // empty for tail waves
   const int ti = tap / g.kw, tx = tap - ti * g.kw;
   const int dyo = ti * g.dh - g.ph, dxo = tx * g.dw - g.pw;
@@ -236,7 +311,7 @@ __global__ __launch_bounds__(256) void offset_wgrad_valu(Geo g, const float* __r
   }
   if (wave != 0) return;
   constexpr int E = kJB * VEC * 64;
-  float* pb = part + ((size_t)(blockIdx.y * gridDim.z + blockIdx.z) * gridDim.x + blockIdx.x) * E;
+  float* pb = part + ((size_t)(by * nz + bz) * nbx + bx) * E;
 #pragma unroll
   for (int jj = 0; jj < kJB; ++jj)
 #pragma unroll
@@ -400,9 +475,21 @@ hipError_t launch_offset_conv_fwd(const Geo& g, const float* x, const float* w_o
   const int n = pad_j(g.J) * g.C * KK;
   hipLaunchKernelGGL(woff_to_ctj, dim3((n + 255) / 256), dim3(256), 0, s, w_off, wt, g.J,
                      pad_j(g.J), g.C, KK);
-  dim3 grid((unsigned)((Mtot + 255) / 256), (g.J + kJB - 1) / kJB, kSplit);
-  DCN_KK_DISPATCH(KK, hipLaunchKernelGGL(offset_conv_fwd_valu<KKc>, grid, dim3(256), 0, s, g, x,
-                                         wt, part));
+  if (g.sw == 1 && g.dw == 1 && g.kh == 3 && g.kw == 3 && !exp_flag(4)) {
+    auto go = [&](auto kern, int npx) {
+      const int gpr = (g.Wo + npx - 1) / npx;
+      const long T = (long)g.B * g.Ho * gpr;
+      dim3 grid((unsigned)((T + 255) / 256), (g.J + kJB - 1) / kJB, kSplit);
+      hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, g, x, wt, part, gpr);
+    };
+    // r01 A/B at config 3 (8 channel slices): 2 px/thread 0.248 ms, 4 px 0.297, 8 px 0.46
+    // (occupancy beats weight reuse); the 1-px generic kernel 0.52
+    go(offset_conv_fwd_row<3, 3, 2>, 2);
+  } else {
+    dim3 grid((unsigned)((Mtot + 255) / 256), (g.J + kJB - 1) / kJB, kSplit);
+    DCN_KK_DISPATCH(KK, hipLaunchKernelGGL(offset_conv_fwd_valu<KKc>, grid, dim3(256), 0, s, g,
+                                           x, wt, part));
+  }
   if (!generic) {
     const long n = (long)g.B * g.J * g.HW;
     hipLaunchKernelGGL(offset_conv_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
@@ -439,12 +526,15 @@ hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
   {
     const WgradGrid w = wgrad_grid(g);
     float* part = goffT + goffT_rows_floats(g);
-    dim3 grid(w.nbx, w.ny, w.nz), rgrid(kJB * w.cper / 64, w.ny * w.nz);
+    dim3 grid(w.nbx * w.ny * w.nz), rgrid(kJB * w.cper / 64, w.ny * w.nz);
+    const int nbx = (int)w.nbx, ny = (int)w.ny, nz = (int)w.nz;
     if (w.cper == 256) {
-      hipLaunchKernelGGL(offset_wgrad_valu<4>, grid, dim3(256), 0, s, g, xT, goffT, part, kWgradPpw);
+      hipLaunchKernelGGL(offset_wgrad_valu<4>, grid, dim3(256), 0, s, g, xT, goffT, part, kWgradPpw,
+                         nbx, ny, nz);
       hipLaunchKernelGGL(wgrad_reduce<4>, rgrid, dim3(1024), 0, s, g, part, gw_off, w.nbx, w.nz);
     } else {
-      hipLaunchKernelGGL(offset_wgrad_valu<1>, grid, dim3(256), 0, s, g, xT, goffT, part, kWgradPpw);
+      hipLaunchKernelGGL(offset_wgrad_valu<1>, grid, dim3(256), 0, s, g, xT, goffT, part, kWgradPpw,
+                         nbx, ny, nz);
       hipLaunchKernelGGL(wgrad_reduce<1>, rgrid, dim3(1024), 0, s, g, part, gw_off, w.nbx, w.nz);
     }
   }
@@ -453,9 +543,11 @@ hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
     hipLaunchKernelGGL(woff_to_jtc, dim3((n + 255) / 256), dim3(256), 0, s, w_off, wt2, g.J, g.C,
                        pad_c(g.C), KK);
     const long Mi = (long)g.B * g.HWi;
-    dim3 grid((unsigned)((Mi + 255) / 256), (g.C + kCB - 1) / kCB);
-    DCN_KK_DISPATCH(KK, hipLaunchKernelGGL(offset_dgrad_valu<KKc>, grid, dim3(256), 0, s, g, wt2,
-                                           goff, gx));
+    {
+      dim3 grid((unsigned)((Mi + 255) / 256), (g.C + kCB - 1) / kCB);
+      DCN_KK_DISPATCH(KK, hipLaunchKernelGGL(offset_dgrad_valu<KKc>, grid, dim3(256), 0, s, g,
+                                             wt2, goff, gx));
+    }
   }
   return hipGetLastError();
 }

@@ -27,22 +27,7 @@ namespace dcn {
 
 static int g_force_generic = 0;
 
-// Development A/B knobs: DCN_EXP="a,b,..." -> exp_flag(i) (0 when unset). Speed only.
-[[maybe_unused]] static int exp_flag(int i) {
-  static int v[8] = {0};
-  static bool init = false;
-  if (!init) {
-    init = true;
-    if (const char* e = std::getenv("DCN_EXP")) {
-      for (int k = 0; k < 8 && *e; ++k) {
-        v[k] = std::atoi(e);
-        while (*e && *e != ',') ++e;
-        if (*e == ',') ++e;
-      }
-    }
-  }
-  return v[i];
-}
+
 void set_force_generic(int on) { g_force_generic = on; }
 int get_force_generic() { return g_force_generic; }
 
