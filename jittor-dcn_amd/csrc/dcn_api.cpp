@@ -129,6 +129,10 @@ struct dcn_handle {
   int device = 0;
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
+  // side stream for work that depends only on inputs (x transpose beside the offset conv,
+  // sample bins beside the GEMMs); forked from / joined back into `stream` with events
+  hipStream_t aux = nullptr;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   dcn::GemmEngine* gemm = nullptr;
   // handle-owned workspace (host-pointer API) and scratch (standalone kernel API)
   void* ws = nullptr;
@@ -165,12 +169,15 @@ struct ProfScope {
   dcn_handle* h;
   int id;
   bool on;
-  ProfScope(dcn_handle* hh, int k) : h(hh), id(k), on(hh->prof_cap > 0 && hh->prof_n[k] < hh->prof_cap) {
-    if (on) (void)hipEventRecord(h->ev[id][2 * h->prof_n[id]], h->stream);
+  hipStream_t st;
+  ProfScope(dcn_handle* hh, int k, hipStream_t s = nullptr)
+      : h(hh), id(k), on(hh->prof_cap > 0 && hh->prof_n[k] < hh->prof_cap),
+        st(s ? s : hh->stream) {
+    if (on) (void)hipEventRecord(h->ev[id][2 * h->prof_n[id]], st);
   }
   ~ProfScope() {
     if (on) {
-      (void)hipEventRecord(h->ev[id][2 * h->prof_n[id] + 1], h->stream);
+      (void)hipEventRecord(h->ev[id][2 * h->prof_n[id] + 1], st);
       ++h->prof_n[id];
     }
   }
@@ -183,9 +190,23 @@ int set_device(dcn_handle* h) {
 }
 
 // ---- forward / backward cores ---------------------------------------------------
+// aux waits for everything issued on the main stream so far
+int fork_aux(dcn_handle* h) {
+  HIP_TRY(hipEventRecord(h->fork_ev, h->stream));
+  HIP_TRY(hipStreamWaitEvent(h->aux, h->fork_ev, 0));
+  return DCN_OK;
+}
+// the main stream waits for everything issued on aux so far
+int join_aux(dcn_handle* h) {
+  HIP_TRY(hipEventRecord(h->join_ev, h->aux));
+  HIP_TRY(hipStreamWaitEvent(h->stream, h->join_ev, 0));
+  return DCN_OK;
+}
+
 int core_forward(dcn_handle* h, const Geo& g, const float* x, const float* off, const float* w,
-                 const float* b, bool has_bias, float* out, float* xT, float* colT) {
-  {
+                 const float* b, bool has_bias, float* out, float* xT, float* colT,
+                 bool xT_ready) {
+  if (!xT_ready) {
     ProfScope ps(h, DCN_K_XPOSE);
     HIP_TRY(dcn::launch_nchw_to_nhwc(x, xT, g.B, g.C, g.HWi, h->stream));
   }
@@ -217,6 +238,10 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
                   const float* gout, float* gx, float* gw, float* gb, bool has_bias, float* goff,
                   float* xT, float* colT, float* parts, float* gxT, float* goutT, void* bins,
                   bool col_valid) {
+  // the sample bins depend only on the offsets: build them on the side stream while the
+  // main stream runs the ∂W / ∂col GEMMs
+  DCN_TRY(fork_aux(h));
+  HIP_TRY(dcn::launch_bins(g, off, bins, goff, 0, g.B, h->aux));
   if (!col_valid) {
     {
       ProfScope ps(h, DCN_K_XPOSE);
@@ -267,8 +292,10 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
   }
   {
     // K5 overwrites grad_x (sampling route) and grad_off
+    DCN_TRY(join_aux(h));
     ProfScope ps(h, DCN_K_COL2IM);
-    HIP_TRY(dcn::launch_col2im_coord(g, x, xT, off, colT, gx, gxT, goff, bins, 0, g.B, h->stream));
+    HIP_TRY(dcn::launch_col2im_coord(g, x, xT, off, colT, gx, gxT, goff, bins, 0, g.B, true,
+                                     h->stream));
   }
   return DCN_OK;
 }
@@ -321,6 +348,13 @@ int dcn_create(int device, dcn_handle** out) {
     return fail(DCN_ERR_HIP, std::string("dcn_create: ") + hipGetErrorString(e));
   }
   h->stream = h->own;
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    dcn_destroy(h);
+    return fail(DCN_ERR_HIP, std::string("dcn_create: ") + hipGetErrorString(e));
+  }
   std::string gerr;
   if (dcn::gemm_engine_create(&h->gemm, &gerr) != 0) {
     (void)hipStreamDestroy(h->own);
@@ -339,7 +373,11 @@ int dcn_destroy(dcn_handle* h) {
     for (hipEvent_t e : v) (void)hipEventDestroy(e);
   if (h->ws) (void)hipFree(h->ws);
   if (h->scratch) (void)hipFree(h->scratch);
+  if (h->aux) (void)hipStreamSynchronize(h->aux);
   dcn::gemm_engine_destroy(h->gemm);
+  if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
+  if (h->join_ev) (void)hipEventDestroy(h->join_ev);
+  if (h->aux) (void)hipStreamDestroy(h->aux);
   if (h->own) (void)hipStreamDestroy(h->own);
   delete h;
   return DCN_OK;
@@ -476,7 +514,7 @@ int dcn_col2im_coord_bwd(dcn_handle* h, const dcn_desc* d, const float* x, const
   ProfScope ps(h, DCN_K_COL2IM);
   HIP_TRY(dcn::launch_nchw_to_nhwc(x + (size_t)b0 * g.C * g.HWi, xT + (size_t)b0 * g.HWi * g.C, nb,
                                    g.C, g.HWi, h->stream));
-  HIP_TRY(dcn::launch_col2im_coord(g, x, xT, off, grad_col, grad_x, gxT, grad_off, bins, b0, nb,
+  HIP_TRY(dcn::launch_col2im_coord(g, x, xT, off, grad_col, grad_x, gxT, grad_off, bins, b0, nb, false,
                                    h->stream));
   return DCN_OK;
 }
@@ -490,16 +528,23 @@ int dcn_forward(dcn_handle* h, const dcn_desc* d, const float* x, const float* w
   const WsLayout L = ws_layout(g, false);
   if (!ws || ws_bytes < L.total) return fail(DCN_ERR_WORKSPACE, "workspace too small for dcn_forward");
   if (d->has_bias && !b) return fail(DCN_ERR_INVALID, "has_bias set but bias is NULL");
+  char* base = static_cast<char*>(ws);
+  float* xT = reinterpret_cast<float*>(base + L.xT);
+  // x -> channels-last on the side stream, beside the offset conv (both only read x)
+  DCN_TRY(fork_aux(h));
+  {
+    ProfScope ps(h, DCN_K_XPOSE, h->aux);
+    HIP_TRY(dcn::launch_nchw_to_nhwc(x, xT, g.B, g.C, g.HWi, h->aux));
+  }
   {
     ProfScope ps(h, DCN_K_OFFSET_FWD);
     HIP_TRY(dcn::launch_offset_conv_fwd(g, x, w_off, b_off, off,
-                                        reinterpret_cast<float*>(static_cast<char*>(ws) + L.wt),
-                                        reinterpret_cast<float*>(static_cast<char*>(ws) + L.part),
-                                        h->stream));
+                                        reinterpret_cast<float*>(base + L.wt),
+                                        reinterpret_cast<float*>(base + L.part), h->stream));
   }
-  char* base = static_cast<char*>(ws);
-  return core_forward(h, g, x, off, w, b, d->has_bias != 0, out,
-                      reinterpret_cast<float*>(base + L.xT), reinterpret_cast<float*>(base + L.col));
+  DCN_TRY(join_aux(h));
+  return core_forward(h, g, x, off, w, b, d->has_bias != 0, out, xT,
+                      reinterpret_cast<float*>(base + L.col), true);
 }
 
 int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* off,

@@ -31,10 +31,16 @@ hipError_t launch_nhwc_to_nchw(const float* in, float* out, int B, int C, int P,
 hipError_t launch_im2col(const Geo& g, const float* x, const float* xT, const float* off,
                          float* colT, int b0, int nb, hipStream_t s);
 size_t bins_ws_bytes(const Geo& g, int nb);
+// K5b: sample bins of images [b0, b0+nb) from the offsets alone (so they can be built on
+// a side stream while the GEMMs run); also zeroes those images' goff when the fused K5
+// will only write the binned samples.
+hipError_t launch_bins(const Geo& g, const float* off, void* bins_ws, float* goff, int b0, int nb,
+                       hipStream_t s);
 // Overwrites gx (NCHW) and goff for images [b0, b0+nb); gxT is scratch [B][HWi][C].
+// bins_ready: launch_bins already ran on bins_ws for these images.
 hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, const float* off,
                                const float* gcolT, float* gx, float* gxT, float* goff,
-                               void* bins_ws, int b0, int nb, hipStream_t s);
+                               void* bins_ws, int b0, int nb, bool bins_ready, hipStream_t s);
 // dcn_offset_conv.hip:
 // wt / wt2: scratch of offset_conv_wt_floats(g) floats (transposed w_off copies).
 size_t offset_conv_wt_floats(const Geo& g);

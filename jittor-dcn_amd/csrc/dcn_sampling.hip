@@ -947,9 +947,64 @@ hipError_t launch_im2col(const Geo& g, const float* x, const float* xT, const fl
   return hipGetLastError();
 }
 
+static bool k5_fused(const Geo& g) {
+  return g.G == 1 && g.C % 4 == 0 && g.C <= 256 && exp_flag(2) == 0;
+}
+
+// Pointers into the bins workspace (bins_ws_bytes layout).
+struct BinsWs {
+  int *cnt, *start, *cursor, *list;
+  float4* rec;
+  int4* brec;
+};
+static BinsWs bins_ptrs(const Geo& g, void* bins_ws, int nb) {
+  const int NB = (g.H + 1) * (g.W + 1), NS = g.HW * g.N;
+  const size_t groups = (size_t)nb * g.G;
+  char* w = static_cast<char*>(bins_ws);
+  BinsWs P;
+  P.cnt = reinterpret_cast<int*>(w);
+  P.start = P.cnt + groups * NB;
+  P.cursor = P.start + groups * (NB + 1);
+  size_t o = (size_t)((char*)(P.cursor + groups * NB) - w);
+  o = (o + 15) / 16 * 16;
+  P.rec = reinterpret_cast<float4*>(w + o);
+  P.list = reinterpret_cast<int*>(P.rec + groups * NS);
+  const size_t lend = (size_t)((char*)(P.list + groups * NS) - w);
+  P.brec = reinterpret_cast<int4*>(w + (lend + 15) / 16 * 16);
+  return P;
+}
+
+hipError_t launch_bins(const Geo& g, const float* off, void* bins_ws, float* goff, int b0, int nb,
+                       hipStream_t s) {
+  if (nb <= 0 || g_force_generic) return hipSuccess;
+  const int NB = (g.H + 1) * (g.W + 1), NS = g.HW * g.N;
+  const size_t groups = (size_t)nb * g.G;
+  const BinsWs P = bins_ptrs(g, bins_ws, nb);
+  hipError_t e = hipMemsetAsync(P.cnt, 0, groups * NB * sizeof(int), s);
+  if (e != hipSuccess) return e;
+  const long total = (long)groups * NS;
+  const unsigned gs = (unsigned)((total + 255) / 256);
+  hipLaunchKernelGGL(bins_count, dim3(gs), dim3(256), 0, s, g, off, P.cnt, P.rec, b0, nb);
+  hipLaunchKernelGGL(bins_scan, dim3((unsigned)groups), dim3(1024), 0, s, NB, P.cnt, P.start,
+                     P.cursor);
+  hipLaunchKernelGGL(bins_fill, dim3(gs), dim3(256), 0, s, g, P.rec, P.start, P.cursor, P.list, nb);
+  const long nbins = (long)groups * NB;
+  hipLaunchKernelGGL(bins_sort, dim3((unsigned)((nbins + 255) / 256)), dim3(256), 0, s, NB, NS,
+                     nbins, P.start, P.list);
+  if (k5_fused(g)) {
+    hipLaunchKernelGGL(bins_pack, dim3(gs), dim3(256), 0, s, g, (int)groups, P.rec, P.start,
+                       P.list, P.brec);
+    // samples in no bin (every corner outside the image) have ∂offset 0
+    e = hipMemsetAsync(goff + (size_t)b0 * g.J * g.HW, 0, (size_t)nb * g.J * g.HW * sizeof(float),
+                       s);
+    if (e != hipSuccess) return e;
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, const float* off,
                                const float* gcolT, float* gx, float* gxT, float* goff,
-                               void* bins_ws, int b0, int nb, hipStream_t s) {
+                               void* bins_ws, int b0, int nb, bool bins_ready, hipStream_t s) {
   if (nb <= 0) return hipSuccess;
   hipError_t e;
   if (g_force_generic) {
@@ -964,7 +1019,7 @@ hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, co
   const bool v4 = can_vec4(g);
   const LaneMap L = lane_map(g.Cg, v4 ? 4 : 1);
   const int NS = g.HW * g.N;
-  const bool fused = g.G == 1 && g.C % 4 == 0 && g.C <= 256 && exp_flag(2) == 0;
+  const bool fused = k5_fused(g);
   if (!fused) {  // K5a: ∂offset
     dim3 grid((NS + 255) / 256, g.G, nb);
     if (v4)
@@ -972,40 +1027,16 @@ hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, co
     else
       hipLaunchKernelGGL(offgrad_cl<1>, grid, dim3(256), 0, s, g, L, xT, off, gcolT, goff, b0);
   }
-  // K5b: bins
-  const int NB = (g.H + 1) * (g.W + 1);
-  const size_t groups = (size_t)nb * g.G;
-  char* w = static_cast<char*>(bins_ws);
-  int* cnt = reinterpret_cast<int*>(w);
-  int* start = cnt + groups * NB;
-  int* cursor = start + groups * (NB + 1);
-  size_t o = (size_t)((char*)(cursor + groups * NB) - w);
-  o = (o + 15) / 16 * 16;
-  float4* rec = reinterpret_cast<float4*>(w + o);
-  int* list = reinterpret_cast<int*>(rec + groups * NS);
-  e = hipMemsetAsync(cnt, 0, groups * NB * sizeof(int), s);
-  if (e != hipSuccess) return e;
-  const long total = (long)groups * NS;
-  const unsigned gs = (unsigned)((total + 255) / 256);
-  hipLaunchKernelGGL(bins_count, dim3(gs), dim3(256), 0, s, g, off, cnt, rec, b0, nb);
-  hipLaunchKernelGGL(bins_scan, dim3((unsigned)groups), dim3(1024), 0, s, NB, cnt, start, cursor);
-  hipLaunchKernelGGL(bins_fill, dim3(gs), dim3(256), 0, s, g, rec, start, cursor, list, nb);
-  const long nbins = (long)groups * NB;
-  hipLaunchKernelGGL(bins_sort, dim3((unsigned)((nbins + 255) / 256)), dim3(256), 0, s, NB, NS,
-                     nbins, start, list);
-  if (fused) {  // one pass over ∂colT: ∂xT tiles + ∂offset of the owned bins
-    // samples in no bin (every corner outside the image) have ∂offset 0
-    e = hipMemsetAsync(goff + (size_t)b0 * g.J * g.HW, 0, (size_t)nb * g.J * g.HW * sizeof(float),
-                       s);
+  if (!bins_ready) {  // K5b (dcn_backward builds the bins on its side stream beforehand)
+    e = launch_bins(g, off, bins_ws, goff, b0, nb, s);
     if (e != hipSuccess) return e;
-    const size_t lend = (size_t)((char*)(list + groups * NS) - w);
-    int4* brec = reinterpret_cast<int4*>(w + (lend + 15) / 16 * 16);  // bins_ws_bytes layout
-    hipLaunchKernelGGL(bins_pack, dim3(gs), dim3(256), 0, s, g, (int)groups, rec, start, list,
-                       brec);
+  }
+  const BinsWs P = bins_ptrs(g, bins_ws, nb);
+  if (fused) {  // one pass over ∂colT: ∂xT tiles + ∂offset of the owned bins
     const int tr_n = (g.H + kTR - 1) / kTR, tq_n = (g.W + kTQ - 1) / kTQ;
     auto go = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3(tr_n * tq_n, 1, nb), dim3(kC2iThreads), 0, s, g, xT, brec,
-                         start, gcolT, gxT, goff, b0, tq_n);
+      hipLaunchKernelGGL(kern, dim3(tr_n * tq_n, 1, nb), dim3(kC2iThreads), 0, s, g, xT, P.brec,
+                         P.start, gcolT, gxT, goff, b0, tq_n);
     };
     // r01 A/B at config 3 (2-deep prefetch pipeline): U=2 0.92 ms col2im, U=4 0.93, U=8 1.50
     switch (exp_flag(3)) {
@@ -1016,11 +1047,11 @@ hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, co
     const int pix_per_block = 4 * L.SP;
     dim3 grid((g.HWi + pix_per_block - 1) / pix_per_block, g.G, nb);
     if (v4)
-      hipLaunchKernelGGL(dx_gather_cl<4>, grid, dim3(256), 0, s, g, L, rec, start, list, gcolT,
-                         gxT, b0);
+      hipLaunchKernelGGL(dx_gather_cl<4>, grid, dim3(256), 0, s, g, L, P.rec, P.start, P.list,
+                         gcolT, gxT, b0);
     else
-      hipLaunchKernelGGL(dx_gather_cl<1>, grid, dim3(256), 0, s, g, L, rec, start, list, gcolT,
-                         gxT, b0);
+      hipLaunchKernelGGL(dx_gather_cl<1>, grid, dim3(256), 0, s, g, L, P.rec, P.start, P.list,
+                         gcolT, gxT, b0);
   }
   return launch_nhwc_to_nchw(gxT + (size_t)b0 * g.HWi * g.C, gx + (size_t)b0 * g.C * g.HWi, nb,
                              g.C, g.HWi, s);
