@@ -6,7 +6,9 @@
 // forward while hipBLASLt wins the NN ∂W and NT ∂col products by 15-25 %. The engine
 // therefore autotunes once per GEMM shape: it times rocBLAS and the top hipBLASLt
 // heuristic candidates on the real operands (HIP events, first call only) and keeps
-// the fastest. DCN_GEMM_BACKEND=rocblas|hipblaslt pins a backend.
+// the fastest. DCN_GEMM_BACKEND=rocblas|hipblaslt pins a backend; DCN_GEMM_CANDIDATES
+// sets how many hipBLASLt heuristic candidates are timed (default 8; 32 found nothing
+// faster at config 3).
 #include <hipblaslt/hipblaslt.h>
 #include <rocblas/rocblas.h>
 
@@ -26,7 +28,7 @@ namespace dcn {
 namespace {
 
 constexpr size_t kLtWorkspace = 64u << 20;
-constexpr int kLtCandidates = 8;
+constexpr int kLtMaxCandidates = 64;
 
 struct Plan {
   int backend = 0;  // 0 rocBLAS, 1 hipBLASLt
@@ -50,6 +52,7 @@ struct GemmEngine {
   void* lt_ws = nullptr;
   std::map<decltype(key_of(GemmSpec())), Plan> plans;
   int force = -1;  // -1 auto, 0 rocBLAS, 1 hipBLASLt
+  int candidates = 8;  // hipBLASLt heuristic candidates timed per shape (DCN_GEMM_CANDIDATES)
 };
 
 int gemm_engine_create(GemmEngine** out, std::string* err) {
@@ -60,6 +63,8 @@ int gemm_engine_create(GemmEngine** out, std::string* err) {
     return -1;
   }
   if (hipblasLtCreate(&e->lt) != HIPBLAS_STATUS_SUCCESS) e->lt = nullptr;  // rocBLAS only
+  if (const char* f = std::getenv("DCN_GEMM_CANDIDATES"))
+    e->candidates = std::max(1, std::min(kLtMaxCandidates, std::atoi(f)));
   if (const char* f = std::getenv("DCN_GEMM_BACKEND")) {
     if (!std::strcmp(f, "rocblas")) e->force = 0;
     if (!std::strcmp(f, "hipblaslt")) e->force = 1;
@@ -172,9 +177,9 @@ static int tune(GemmEngine* e, const GemmSpec& s, const float* A, const float* B
   const uint64_t wsb = kLtWorkspace;
   hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb,
                                         sizeof(wsb));
-  hipblasLtMatmulHeuristicResult_t res[kLtCandidates];
+  hipblasLtMatmulHeuristicResult_t res[kLtMaxCandidates];
   int n = 0;
-  hipblasLtMatmulAlgoGetHeuristic(e->lt, p.desc, p.la, p.lb, p.lc, p.lc, pref, kLtCandidates, res,
+  hipblasLtMatmulAlgoGetHeuristic(e->lt, p.desc, p.la, p.lb, p.lc, p.lc, pref, e->candidates, res,
                                   &n);
   hipblasLtMatmulPreferenceDestroy(pref);
   int pick = -1;

@@ -497,7 +497,7 @@ __global__ __launch_bounds__(256) void bins_sort(int NB, int NS, long nbins,
 // image: zero). ∂offset uses offgrad_cl's op order (per-lane channel sums, fixed xor
 // tree). Used for deform_groups == 1, C % 4 == 0, C <= 256.
 // ---------------------------------------------------------------------------
-constexpr int kTR = 4, kTQ = 4;  // tile rows x cols; kTR+1 waves per block
+constexpr int kTR = 4;  // tile rows; kTR+1 waves per block (tile cols: template TQ)
 constexpr int kC2iThreads = (kTR + 1) * 64;
 
 __device__ __forceinline__ float4 fma4(float w, float4 g, float4 a) {
@@ -507,7 +507,7 @@ __device__ __forceinline__ float4 add4(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
 
-template <int U>
+template <int U, int kTQ>
 __global__ __launch_bounds__(kC2iThreads) void col2im_tile(Geo g, const float* __restrict__ xT,
                                                            const int4* __restrict__ brec,
                                                            const int* __restrict__ start,
@@ -1033,16 +1033,15 @@ hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, co
   }
   const BinsWs P = bins_ptrs(g, bins_ws, nb);
   if (fused) {  // one pass over ∂colT: ∂xT tiles + ∂offset of the owned bins
-    const int tr_n = (g.H + kTR - 1) / kTR, tq_n = (g.W + kTQ - 1) / kTQ;
-    auto go = [&](auto kern) {
+    const int tr_n = (g.H + kTR - 1) / kTR;
+    auto go = [&](auto kern, int tq) {
+      const int tq_n = (g.W + tq - 1) / tq;
       hipLaunchKernelGGL(kern, dim3(tr_n * tq_n, 1, nb), dim3(kC2iThreads), 0, s, g, xT, P.brec,
                          P.start, gcolT, gxT, goff, b0, tq_n);
     };
-    // r01 A/B at config 3 (2-deep prefetch pipeline): U=2 0.92 ms col2im, U=4 0.93, U=8 1.50
-    switch (exp_flag(3)) {
-      case 1: go(col2im_tile<4>); break;
-      default: go(col2im_tile<2>);
-    }
+    // r01 A/B at config 3 (2-deep prefetch pipeline): U=2 0.92 ms col2im, U=4 0.93, U=8 1.50;
+    // 4x6 tiles 1.05x slower, 4x8 tiles no longer unroll (2.7 ms)
+    go(col2im_tile<2, 4>, 4);
   } else {  // gather ∂xT, then back to NCHW (overwrites gx for these images)
     const int pix_per_block = 4 * L.SP;
     dim3 grid((g.HWi + pix_per_block - 1) / pix_per_block, g.G, nb);
