@@ -34,7 +34,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters
 
 CONFIGS = {
     # BASELINE.json configs[2] (config 3): the metric's own workload
-    3: dict(B=64, C=256, O=256, H=56, W=56, k=3, s=1, p=1),
+    3: dict(B=64, C=256, O=256, H=56, W=56, k=3, s=1, p=1, dtype="f32"),
+    # configs[3] (config 4): N=512 batch-sharded over 8 GPUs = 64 images per GPU, bf16
+    4: dict(B=64, C=256, O=256, H=28, W=28, k=3, s=1, p=1, dtype="bf16"),
 }
 
 
@@ -80,9 +82,10 @@ def cpu_baseline(cfg, budget_s=10.0, threads=None):
 K1_KERNEL = "dcn::im2col_lds"  # K1 on the channels-last path (deform_groups 1, C % 4 == 0)
 
 
-def load_traffic(path):
+def load_traffic(path, bf16=False):
     """HBM bytes per K1 launch from the newest committed PMC summary
-    (tools/pmc_pass.sh + tools/pmc_summary.py -> profiles/rNN_pmc_hbm.json)."""
+    (tools/pmc_pass.sh + tools/pmc_summary.py -> profiles/rNN_pmc_hbm.json); the bf16-column
+    instantiation for config 4, the fp32 one otherwise."""
     import glob
     paths = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_hbm.json")))
     if not paths:
@@ -93,7 +96,7 @@ def load_traffic(path):
     except (OSError, ValueError):
         return None, None
     for name, v in doc.get("kernels", {}).items():
-        if name.startswith(K1_KERNEL):
+        if name.startswith(K1_KERNEL) and (("unsigned short" in name) == bf16):
             return int(v["hbm_bytes"]), f"{os.path.relpath(paths[-1], ROOT)}:{name}"
     return None, None
 
@@ -131,8 +134,11 @@ def main():
 
     cfg = CONFIGS[args.config]
     B, C, O_, H, W, k, s, p = (cfg[n] for n in ("B", "C", "O", "H", "W", "k", "s", "p"))
+    bf16 = cfg["dtype"] == "bf16"
+    tdt = torch.bfloat16 if bf16 else torch.float32
     N = k * k
-    desc = rt.make_desc(B, C, H, W, O_, (k, k), (s, s), (p, p))
+    desc = rt.make_desc(B, C, H, W, O_, (k, k), (s, s), (p, p),
+                        dtype=rt.DCN_BF16 if bf16 else rt.DCN_F32)
     Ho, Wo = rt.out_shape(desc)
     J = 2 * N
 
@@ -140,19 +146,19 @@ def main():
     # replicated parameters (same seed on every rank), per-rank batch shard
     g = torch.Generator(device=dev)
     g.manual_seed(1234)
-    w_off = torch.randn(J, C, k, k, device=dev, generator=g) / float(np.sqrt(C * N))
-    b_off = torch.rand(J, device=dev, generator=g) - 0.5
-    w = torch.randn(O_, C, k, k, device=dev, generator=g) * float(np.sqrt(2.0 / (C * N)))
-    b = torch.randn(O_, device=dev, generator=g) * 0.1
+    w_off = (torch.randn(J, C, k, k, device=dev, generator=g) / float(np.sqrt(C * N))).to(tdt)
+    b_off = (torch.rand(J, device=dev, generator=g) - 0.5).to(tdt)
+    w = (torch.randn(O_, C, k, k, device=dev, generator=g) * float(np.sqrt(2.0 / (C * N)))).to(tdt)
+    b = (torch.randn(O_, device=dev, generator=g) * 0.1).to(tdt)
     g.manual_seed(1000 + rank)
-    x = torch.randn(B, C, H, W, device=dev, generator=g)
-    gout = torch.randn(B, O_, Ho, Wo, device=dev, generator=g)
-    out = torch.empty(B, O_, Ho, Wo, device=dev)
-    off = torch.empty(B, J, Ho, Wo, device=dev)
+    x = torch.randn(B, C, H, W, device=dev, generator=g).to(tdt)
+    gout = torch.randn(B, O_, Ho, Wo, device=dev, generator=g).to(tdt)
+    out = torch.empty(B, O_, Ho, Wo, device=dev, dtype=tdt)
+    off = torch.empty(B, J, Ho, Wo, device=dev, dtype=tdt)
     gx = torch.empty_like(x)
     # all parameter grads packed in ONE buffer -> one all-reduce per step (dcn_dp)
     gbuf = dcn_dp.GradBuffer(dcn_dp.param_shapes(C, O_, k, k),
-                             lambda n: torch.empty(n, device=dev))
+                             lambda n: torch.empty(n, device=dev, dtype=tdt))
     gflat = gbuf.flat
     gw, gb, gwo, gbo = (gbuf[n] for n in dcn_dp.PARAM_ORDER)
     goff = torch.empty_like(off)
@@ -214,13 +220,13 @@ def main():
         if cnt:
             kernel_ms[name] = round(tot / cnt, 4)
     k1_ms = kernel_ms.get("im2col")
-    k1_b = k1_bytes(B, C, H, W, N, Ho, Wo)
+    k1_b = k1_bytes(B, C, H, W, N, Ho, Wo, elem=2 if bf16 else 4)
 
     samples = B * Ho * Wo * N * world * args.steps
     value = samples / el / 1e9
     if rank == 0:
         achieved = k1_b / (k1_ms * 1e-3) / 1e9 if k1_ms else None
-        traffic, traffic_src = load_traffic(args.traffic_json)
+        traffic, traffic_src = load_traffic(args.traffic_json, bf16)
         res = {
             "metric": METRIC,
             "value": round(value, 5),
@@ -232,10 +238,11 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": cfg["dtype"],
             "data": "synthetic",
             "config": {"workload": f"config{args.config}: B={B}/GPU C={C}->O={O_} {H}x{W} k{k} s{s} "
-                                   f"p{p} fp32 DeformConv2d fwd+bwd (+RCCL grad all-reduce if N>1)",
+                                   f"p{p} {cfg['dtype']} DeformConv2d fwd+bwd (+RCCL grad "
+                                   f"all-reduce if N>1)",
                        "global_batch": B * world, "B_per_gpu": B, "C": C, "O": O_, "H": H, "W": W,
                        "kernel": k, "stride": s, "padding": p,
                        "parallelism": f"dp{world} (batch-sharded, replicated params)",

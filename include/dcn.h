@@ -9,9 +9,12 @@
  * Conventions
  *  - Every function returns int: 0 = OK, < 0 = dcn_status error code. The
  *    library never aborts; dcn_last_error() returns a thread-local message.
- *  - Tensors are fp32, dense, NCHW (x, out, offsets) or the reference's own
- *    parameter layouts (weights). All device pointers are caller-owned; the
- *    library never frees or retains them.
+ *  - Tensors are dense, NCHW (x, out, offsets) or the reference's own parameter
+ *    layouts (weights), in the descriptor's dtype: fp32 (DCN_F32, the reference's
+ *    type) or bf16 storage (DCN_BF16: every tensor argument then points at 16-bit
+ *    bf16 values despite the float* spelling; internally the columns and GEMM
+ *    operands are bf16 with fp32 accumulation, everything else fp32). All device
+ *    pointers are caller-owned; the library never frees or retains them.
  *  - Calls are ordered on the handle's stream (dcn_set_stream). A handle is not
  *    thread-safe: use one handle per device and per host thread.
  *  - `*_host` variants take host pointers, move data over PCIe themselves and
@@ -58,7 +61,10 @@ typedef struct {
   int ph, pw;     /* padding, deform_conv.py:13 */
   int dil_h, dil_w;  /* extension: offset-conv dilation (1 = reference) */
   int deform_groups; /* extension: offset groups (1 = reference) */
-  int dtype;         /* dcn_dtype; only DCN_F32 in this build */
+  int dtype;         /* dcn_dtype. DCN_BF16 needs deform_groups 1, kh*kw <= 9,
+                        C % 4 == 0, C <= 256, and is supported by dcn_forward /
+                        dcn_backward (+ _host); the standalone kernel entry points
+                        below are DCN_F32 only */
   int has_bias;      /* deform_conv.py:25 */
 } dcn_desc;
 

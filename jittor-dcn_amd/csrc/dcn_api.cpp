@@ -59,9 +59,9 @@ int make_geo(const dcn_desc* d, Geo* g) {
     return fail(DCN_ERR_INVALID, "dilation and deform_groups must be >= 1");
   if (d->C % d->deform_groups != 0)
     return fail(DCN_ERR_INVALID, "in_channels must be divisible by deform_groups");
-  if (d->dtype != DCN_F32)
-    return fail(DCN_ERR_UNSUPPORTED, "only DCN_F32 is implemented in this build");
+  if (d->dtype != DCN_F32 && d->dtype != DCN_BF16) return fail(DCN_ERR_INVALID, "unknown dtype");
   Geo& q = *g;
+  q.dt = d->dtype;
   q.B = d->B; q.C = d->C; q.H = d->H; q.W = d->W; q.O = d->O;
   q.kh = d->kh; q.kw = d->kw; q.sh = d->sh; q.sw = d->sw; q.ph = d->ph; q.pw = d->pw;
   q.dh = d->dil_h; q.dw = d->dil_w; q.G = d->deform_groups;
@@ -82,6 +82,19 @@ int make_geo(const dcn_desc* d, Geo* g) {
     return fail(DCN_ERR_UNSUPPORTED, "per-image column block exceeds 2^31 elements");
   if ((long long)q.O > (1 << 30) || (long long)q.K > (1 << 30))
     return fail(DCN_ERR_UNSUPPORTED, "channel counts too large");
+  if (q.dt == DCN_BF16 && !dcn::bf16_path_ok(q))
+    return fail(DCN_ERR_UNSUPPORTED,
+                "DCN_BF16 needs deform_groups == 1, kh*kw <= 9, C % 4 == 0 and C <= 256");
+  return DCN_OK;
+}
+
+size_t elem_bytes(const Geo& g) { return g.dt == DCN_BF16 ? 2 : 4; }
+
+// The standalone kernel entry points (offset conv, im2col, col2im) are fp32 only.
+int make_geo_f32(const dcn_desc* d, Geo* g) {
+  DCN_TRY(make_geo(d, g));
+  if (g->dt != DCN_F32)
+    return fail(DCN_ERR_UNSUPPORTED, "standalone kernel entry points take DCN_F32 only");
   return DCN_OK;
 }
 
@@ -96,6 +109,10 @@ struct WsLayout {
   size_t gxT = 0;    // [B][H*W][C] channels-last ∂x (sampling route)
   size_t goutT = 0;  // [B][Ho*Wo][O] transposed ∂out (flat ∂col GEMM)
   size_t bins = 0;   // sample bins of K5b
+  // DCN_BF16 only: fp32 working copies (the offset conv, coordinates and reductions run
+  // in fp32; only the columns and the GEMM operands are bf16)
+  size_t x32 = 0, woff32 = 0, boff32 = 0, b32 = 0, off32 = 0, out32 = 0;
+  size_t gout32 = 0, gx32 = 0, gw32 = 0, gb32 = 0, gwo32 = 0, gbo32 = 0, goff32 = 0;
   size_t total = 0;
 };
 
@@ -118,6 +135,24 @@ WsLayout ws_layout(const Geo& g, bool bwd) {
     L.gxT = take((size_t)g.B * g.HWi * g.C * sizeof(float));
     L.goutT = take((size_t)g.B * g.HW * g.O * sizeof(float));
     L.bins = take(dcn::bins_ws_bytes(g, g.B));
+  }
+  if (g.dt == DCN_BF16) {
+    const size_t f = sizeof(float);
+    L.x32 = take((size_t)g.B * g.C * g.HWi * f);
+    L.woff32 = take((size_t)g.J * g.C * g.N * f);
+    L.boff32 = take((size_t)g.J * f);
+    L.b32 = take((size_t)g.O * f);
+    L.off32 = take((size_t)g.B * g.J * g.HW * f);
+    L.out32 = take((size_t)g.B * g.O * g.HW * f);
+    if (bwd) {
+      L.gout32 = take((size_t)g.B * g.O * g.HW * f);
+      L.gx32 = take((size_t)g.B * g.C * g.HWi * f);
+      L.gw32 = take((size_t)g.O * g.K * f);
+      L.gb32 = take((size_t)g.O * f);
+      L.gwo32 = take((size_t)g.J * g.C * g.N * f);
+      L.gbo32 = take((size_t)g.J * f);
+      L.goff32 = take((size_t)g.B * g.J * g.HW * f);
+    }
   }
   L.total = off;
   return L;
@@ -300,6 +335,128 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
   return DCN_OK;
 }
 
+// ---- DCN_BF16 orchestration -------------------------------------------------------
+// Tensors cross the API in bf16. The offset conv, coordinates, interpolation weights,
+// ∂offset / ∂x accumulation and every reduction run in fp32 on working copies; the
+// columns, ∂columns and the three GEMM operands are bf16 (MFMA bf16, fp32 accumulate).
+// The forward rounds its offsets to bf16 BEFORE sampling with them, so a backward that
+// only sees the bf16 offsets samples exactly the same points.
+using dcn::bf16_t;
+#define BF(o) reinterpret_cast<bf16_t*>(base + (o))
+#define F32(o) reinterpret_cast<float*>(base + (o))
+
+int forward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x,
+                 const bf16_t* w_off, const bf16_t* b_off, const bf16_t* w, const bf16_t* b,
+                 bf16_t* out, bf16_t* off, char* base, const WsLayout& L) {
+  hipStream_t st = h->stream;
+  float *x32 = F32(L.x32), *xT = F32(L.xT), *off32 = F32(L.off32), *out32 = F32(L.out32);
+  HIP_TRY(dcn::launch_bf16_to_f32(x, x32, (size_t)g.B * g.C * g.HWi, st));
+  HIP_TRY(dcn::launch_bf16_to_f32(w_off, F32(L.woff32), (size_t)g.J * g.C * g.N, st));
+  HIP_TRY(dcn::launch_bf16_to_f32(b_off, F32(L.boff32), (size_t)g.J, st));
+  if (has_bias) HIP_TRY(dcn::launch_bf16_to_f32(b, F32(L.b32), (size_t)g.O, st));
+  DCN_TRY(fork_aux(h));
+  {
+    ProfScope ps(h, DCN_K_XPOSE, h->aux);
+    HIP_TRY(dcn::launch_nchw_to_nhwc(x32, xT, g.B, g.C, g.HWi, h->aux));
+  }
+  {
+    ProfScope ps(h, DCN_K_OFFSET_FWD);
+    HIP_TRY(dcn::launch_offset_conv_fwd(g, x32, F32(L.woff32), F32(L.boff32), off32, F32(L.wt),
+                                        F32(L.part), st));
+    HIP_TRY(dcn::launch_round_to_bf16(off32, off, (size_t)g.B * g.J * g.HW, st));
+  }
+  DCN_TRY(join_aux(h));
+  {
+    ProfScope ps(h, DCN_K_IM2COL);
+    HIP_TRY(dcn::launch_im2col_bf16(g, xT, off32, BF(L.col), 0, g.B, st));
+  }
+  {
+    ProfScope ps(h, DCN_K_GEMM_FWD);  // C(HW×O) = colT_bᵀ · Wf, bf16 operands, fp32 out
+    dcn::GemmSpec sp;
+    sp.ta = true;
+    sp.m = g.HW; sp.n = g.O; sp.k = g.K;
+    sp.lda = g.K; sp.sa = (long)g.K * g.HW;
+    sp.ldb = g.K; sp.sb = 0;
+    sp.ldc = g.HW; sp.sc = (long)g.O * g.HW;
+    sp.batch = g.B;
+    sp.bf16_ab = true;
+    GEMM_TRY(h, sp, BF(L.col), w, out32);
+  }
+  ProfScope ps(h, DCN_K_BIAS_FWD);
+  HIP_TRY(dcn::launch_bias_to_bf16(g, out32, has_bias ? F32(L.b32) : nullptr, out, st));
+  return DCN_OK;
+}
+
+int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, const bf16_t* off,
+                  const bf16_t* w_off, const bf16_t* w, const bf16_t* gout, bf16_t* gx,
+                  bf16_t* gw, bf16_t* gb, bf16_t* gw_off, bf16_t* gb_off, bf16_t* goff_out,
+                  char* base, const WsLayout& L, bool col_valid) {
+  hipStream_t st = h->stream;
+  float *x32 = F32(L.x32), *xT = F32(L.xT), *off32 = F32(L.off32), *goff32 = F32(L.goff32);
+  float *gx32 = F32(L.gx32), *gout32 = F32(L.gout32);
+  bf16_t* col = BF(L.col);
+  const size_t nx = (size_t)g.B * g.C * g.HWi, noff = (size_t)g.B * g.J * g.HW;
+  const size_t nout = (size_t)g.B * g.O * g.HW, nwo = (size_t)g.J * g.C * g.N;
+  HIP_TRY(dcn::launch_bf16_to_f32(off, off32, noff, st));  // == the forward's rounded offsets
+  HIP_TRY(dcn::launch_bf16_to_f32(w_off, F32(L.woff32), nwo, st));
+  DCN_TRY(fork_aux(h));
+  HIP_TRY(dcn::launch_bins(g, off32, base + L.bins, goff32, 0, g.B, h->aux));
+  if (!col_valid) {
+    HIP_TRY(dcn::launch_bf16_to_f32(x, x32, nx, st));
+    {
+      ProfScope ps(h, DCN_K_XPOSE);
+      HIP_TRY(dcn::launch_nchw_to_nhwc(x32, xT, g.B, g.C, g.HWi, st));
+    }
+    ProfScope ps(h, DCN_K_IM2COL);
+    HIP_TRY(dcn::launch_im2col_bf16(g, xT, off32, col, 0, g.B, st));
+  }
+  if (has_bias) {
+    ProfScope ps(h, DCN_K_BWD_BIAS);
+    HIP_TRY(dcn::launch_bf16_to_f32(gout, gout32, nout, st));
+    HIP_TRY(dcn::launch_bias_grad(g, gout32, F32(L.gb32), st));
+    HIP_TRY(dcn::launch_f32_to_bf16(F32(L.gb32), gb, (size_t)g.O, st));
+  }
+  {
+    ProfScope ps(h, DCN_K_GEMM_DW);  // P_b(K×O) = colT_b · ∂out_b (NN), bf16 in, fp32 out
+    dcn::GemmSpec sp;
+    sp.m = g.K; sp.n = g.O; sp.k = g.HW;
+    sp.lda = g.K; sp.sa = (long)g.K * g.HW;
+    sp.ldb = g.HW; sp.sb = (long)g.O * g.HW;
+    sp.ldc = g.K; sp.sc = (long)g.K * g.O;
+    sp.batch = g.B;
+    sp.bf16_ab = true;
+    GEMM_TRY(h, sp, col, gout, F32(L.parts));
+    HIP_TRY(dcn::launch_sum_partials(F32(L.parts), g.B, (size_t)g.K * g.O, F32(L.gw32), st));
+    HIP_TRY(dcn::launch_f32_to_bf16(F32(L.gw32), gw, (size_t)g.O * g.K, st));
+  }
+  {
+    ProfScope ps(h, DCN_K_GEMM_DCOL);  // ∂colT = ∂outT · Wf, one flat GEMM, bf16 out
+    bf16_t* goutT = BF(L.goutT);
+    HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(gout, goutT, g.B, g.O, g.HW, st));
+    dcn::GemmSpec sp;
+    sp.m = g.K; sp.n = g.B * g.HW; sp.k = g.O;
+    sp.lda = g.K; sp.ldb = g.O; sp.ldc = g.K;
+    sp.bf16_ab = sp.bf16_c = true;
+    GEMM_TRY(h, sp, w, goutT, col);
+  }
+  DCN_TRY(join_aux(h));
+  {
+    ProfScope ps(h, DCN_K_COL2IM);
+    HIP_TRY(dcn::launch_col2im_bf16(g, xT, off32, col, gx32, F32(L.gxT), goff32, base + L.bins, 0,
+                                    g.B, true, st));
+  }
+  ProfScope ps(h, DCN_K_OFFSET_BWD);
+  HIP_TRY(dcn::launch_offset_conv_bwd(g, x32, xT, F32(L.woff32), goff32, F32(L.goffT), F32(L.wt),
+                                      gx32, F32(L.gwo32), F32(L.gbo32), st));
+  HIP_TRY(dcn::launch_f32_to_bf16(gx32, gx, nx, st));
+  HIP_TRY(dcn::launch_f32_to_bf16(F32(L.gwo32), gw_off, nwo, st));
+  HIP_TRY(dcn::launch_f32_to_bf16(F32(L.gbo32), gb_off, (size_t)g.J, st));
+  if (goff_out) HIP_TRY(dcn::launch_f32_to_bf16(goff32, goff_out, noff, st));
+  return DCN_OK;
+}
+#undef BF
+#undef F32
+
 int ensure_scratch(dcn_handle* h, size_t bytes) {
   if (h->scratch_bytes >= bytes) return DCN_OK;
   if (h->scratch) {
@@ -453,7 +610,7 @@ int dcn_workspace_bytes(const dcn_desc* d, int with_backward, size_t* bytes) {
 int dcn_offset_conv_fwd(dcn_handle* h, const dcn_desc* d, const float* x, const float* w_off,
                         const float* b_off, float* off) {
   Geo g;
-  DCN_TRY(make_geo(d, &g));
+  DCN_TRY(make_geo_f32(d, &g));
   DCN_TRY(set_device(h));
   const size_t wbytes = align_up(dcn::offset_conv_wt_floats(g) * sizeof(float), 256);
   DCN_TRY(ensure_scratch(h, wbytes + dcn::offset_conv_fpart_floats(g) * sizeof(float)));
@@ -468,7 +625,7 @@ int dcn_offset_conv_bwd(dcn_handle* h, const dcn_desc* d, const float* x, const 
                         const float* grad_off, float* grad_x, float* grad_w_off,
                         float* grad_b_off) {
   Geo g;
-  DCN_TRY(make_geo(d, &g));
+  DCN_TRY(make_geo_f32(d, &g));
   DCN_TRY(set_device(h));
   const size_t xbytes = align_up((size_t)g.B * g.HWi * g.C * sizeof(float), 256);
   const size_t gbytes = align_up(dcn::offset_conv_goffT_floats(g) * sizeof(float), 256);
@@ -487,7 +644,7 @@ int dcn_offset_conv_bwd(dcn_handle* h, const dcn_desc* d, const float* x, const 
 int dcn_im2col_fwd(dcn_handle* h, const dcn_desc* d, const float* x, const float* off,
                    float* col, int b0, int nb) {
   Geo g;
-  DCN_TRY(make_geo(d, &g));
+  DCN_TRY(make_geo_f32(d, &g));
   DCN_TRY(set_device(h));
   if (b0 < 0 || nb < 0 || b0 + nb > g.B) return fail(DCN_ERR_INVALID, "image range out of bounds");
   DCN_TRY(ensure_scratch(h, (size_t)g.B * g.HWi * g.C * sizeof(float)));
@@ -502,7 +659,7 @@ int dcn_im2col_fwd(dcn_handle* h, const dcn_desc* d, const float* x, const float
 int dcn_col2im_coord_bwd(dcn_handle* h, const dcn_desc* d, const float* x, const float* off,
                          const float* grad_col, float* grad_x, float* grad_off, int b0, int nb) {
   Geo g;
-  DCN_TRY(make_geo(d, &g));
+  DCN_TRY(make_geo_f32(d, &g));
   DCN_TRY(set_device(h));
   if (b0 < 0 || nb < 0 || b0 + nb > g.B) return fail(DCN_ERR_INVALID, "image range out of bounds");
   const size_t xbytes = align_up((size_t)g.B * g.HWi * g.C * sizeof(float), 256);
@@ -529,6 +686,14 @@ int dcn_forward(dcn_handle* h, const dcn_desc* d, const float* x, const float* w
   if (!ws || ws_bytes < L.total) return fail(DCN_ERR_WORKSPACE, "workspace too small for dcn_forward");
   if (d->has_bias && !b) return fail(DCN_ERR_INVALID, "has_bias set but bias is NULL");
   char* base = static_cast<char*>(ws);
+  if (g.dt == DCN_BF16) {
+    using dcn::bf16_t;
+    return forward_bf16(h, g, d->has_bias != 0, reinterpret_cast<const bf16_t*>(x),
+                        reinterpret_cast<const bf16_t*>(w_off),
+                        reinterpret_cast<const bf16_t*>(b_off), reinterpret_cast<const bf16_t*>(w),
+                        reinterpret_cast<const bf16_t*>(b), reinterpret_cast<bf16_t*>(out),
+                        reinterpret_cast<bf16_t*>(off), base, L);
+  }
   float* xT = reinterpret_cast<float*>(base + L.xT);
   // x -> channels-last on the side stream, beside the offset conv (both only read x)
   DCN_TRY(fork_aux(h));
@@ -558,6 +723,14 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
   if (!ws || ws_bytes < L.total) return fail(DCN_ERR_WORKSPACE, "workspace too small for dcn_backward");
   if (d->has_bias && !grad_b) return fail(DCN_ERR_INVALID, "has_bias set but grad_b is NULL");
   char* base = static_cast<char*>(ws);
+  if (g.dt == DCN_BF16) {
+    using dcn::bf16_t;
+    auto C = [](const float* p) { return reinterpret_cast<const bf16_t*>(p); };
+    auto M = [](float* p) { return reinterpret_cast<bf16_t*>(p); };
+    return backward_bf16(h, g, d->has_bias != 0, C(x), C(off), C(w_off), C(w), C(grad_out),
+                         M(grad_x), M(grad_w), M(grad_b), M(grad_w_off), M(grad_b_off),
+                         M(grad_off_out), base, L, (flags & DCN_BWD_COL_IN_WS) != 0);
+  }
   auto F = [&](size_t o) { return reinterpret_cast<float*>(base + o); };
   float* goff = grad_off_out ? grad_off_out : F(L.goff);
   DCN_TRY(core_backward(h, g, x, off, w, grad_out, grad_x, grad_w, grad_b, d->has_bias != 0, goff,
@@ -596,12 +769,12 @@ int ensure_ws(dcn_handle* h, size_t bytes) {
   return DCN_OK;
 }
 
-int h2d(dcn_handle* h, float* dst, const float* src, size_t n) {
-  HIP_TRY(hipMemcpyAsync(dst, src, n * sizeof(float), hipMemcpyHostToDevice, h->stream));
+int h2d(dcn_handle* h, float* dst, const float* src, size_t bytes) {
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->stream));
   return DCN_OK;
 }
-int d2h(dcn_handle* h, float* dst, const float* src, size_t n) {
-  HIP_TRY(hipMemcpyAsync(dst, src, n * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+int d2h(dcn_handle* h, float* dst, const float* src, size_t bytes) {
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
   return DCN_OK;
 }
 }  // namespace
@@ -613,25 +786,26 @@ int dcn_forward_host(dcn_handle* h, const dcn_desc* d, const float* x, const flo
   DCN_TRY(set_device(h));
   const size_t nx = (size_t)g.B * g.C * g.HWi, nwo = (size_t)g.J * g.C * g.N, nw = (size_t)g.O * g.K;
   const size_t nout = (size_t)g.B * g.O * g.HW, noff = (size_t)g.B * g.J * g.HW;
+  const size_t es = elem_bytes(g);
   DevBufs db;
   float *dx, *dwo, *dbo, *dw, *db_ = nullptr, *dout, *doff;
-  DCN_TRY(db.alloc(nx * 4, &dx));
-  DCN_TRY(db.alloc(nwo * 4, &dwo));
-  DCN_TRY(db.alloc((size_t)g.J * 4, &dbo));
-  DCN_TRY(db.alloc(nw * 4, &dw));
-  if (d->has_bias) DCN_TRY(db.alloc((size_t)g.O * 4, &db_));
-  DCN_TRY(db.alloc(nout * 4, &dout));
-  DCN_TRY(db.alloc(noff * 4, &doff));
-  DCN_TRY(h2d(h, dx, x, nx));
-  DCN_TRY(h2d(h, dwo, w_off, nwo));
-  DCN_TRY(h2d(h, dbo, b_off, g.J));
-  DCN_TRY(h2d(h, dw, w, nw));
-  if (d->has_bias) DCN_TRY(h2d(h, db_, b, g.O));
+  DCN_TRY(db.alloc(nx * es, &dx));
+  DCN_TRY(db.alloc(nwo * es, &dwo));
+  DCN_TRY(db.alloc((size_t)g.J * es, &dbo));
+  DCN_TRY(db.alloc(nw * es, &dw));
+  if (d->has_bias) DCN_TRY(db.alloc((size_t)g.O * es, &db_));
+  DCN_TRY(db.alloc(nout * es, &dout));
+  DCN_TRY(db.alloc(noff * es, &doff));
+  DCN_TRY(h2d(h, dx, x, nx * es));
+  DCN_TRY(h2d(h, dwo, w_off, nwo * es));
+  DCN_TRY(h2d(h, dbo, b_off, g.J * es));
+  DCN_TRY(h2d(h, dw, w, nw * es));
+  if (d->has_bias) DCN_TRY(h2d(h, db_, b, g.O * es));
   const size_t wsb = ws_layout(g, false).total;
   DCN_TRY(ensure_ws(h, wsb));
   DCN_TRY(dcn_forward(h, d, dx, dwo, dbo, dw, db_, dout, doff, h->ws, h->ws_bytes));
-  DCN_TRY(d2h(h, out, dout, nout));
-  if (off) DCN_TRY(d2h(h, off, doff, noff));
+  DCN_TRY(d2h(h, out, dout, nout * es));
+  if (off) DCN_TRY(d2h(h, off, doff, noff * es));
   HIP_TRY(hipStreamSynchronize(h->stream));
   return DCN_OK;
 }
@@ -645,34 +819,35 @@ int dcn_backward_host(dcn_handle* h, const dcn_desc* d, const float* x, const fl
   DCN_TRY(set_device(h));
   const size_t nx = (size_t)g.B * g.C * g.HWi, nwo = (size_t)g.J * g.C * g.N, nw = (size_t)g.O * g.K;
   const size_t nout = (size_t)g.B * g.O * g.HW, noff = (size_t)g.B * g.J * g.HW;
+  const size_t es = elem_bytes(g);
   DevBufs db;
   float *dx, *doff, *dwo, *dw, *dgo, *dgx, *dgw, *dgb = nullptr, *dgwo, *dgbo, *dgoff;
-  DCN_TRY(db.alloc(nx * 4, &dx));
-  DCN_TRY(db.alloc(noff * 4, &doff));
-  DCN_TRY(db.alloc(nwo * 4, &dwo));
-  DCN_TRY(db.alloc(nw * 4, &dw));
-  DCN_TRY(db.alloc(nout * 4, &dgo));
-  DCN_TRY(db.alloc(nx * 4, &dgx));
-  DCN_TRY(db.alloc(nw * 4, &dgw));
-  if (d->has_bias) DCN_TRY(db.alloc((size_t)g.O * 4, &dgb));
-  DCN_TRY(db.alloc(nwo * 4, &dgwo));
-  DCN_TRY(db.alloc((size_t)g.J * 4, &dgbo));
-  DCN_TRY(db.alloc(noff * 4, &dgoff));
-  DCN_TRY(h2d(h, dx, x, nx));
-  DCN_TRY(h2d(h, doff, off, noff));
-  DCN_TRY(h2d(h, dwo, w_off, nwo));
-  DCN_TRY(h2d(h, dw, w, nw));
-  DCN_TRY(h2d(h, dgo, grad_out, nout));
+  DCN_TRY(db.alloc(nx * es, &dx));
+  DCN_TRY(db.alloc(noff * es, &doff));
+  DCN_TRY(db.alloc(nwo * es, &dwo));
+  DCN_TRY(db.alloc(nw * es, &dw));
+  DCN_TRY(db.alloc(nout * es, &dgo));
+  DCN_TRY(db.alloc(nx * es, &dgx));
+  DCN_TRY(db.alloc(nw * es, &dgw));
+  if (d->has_bias) DCN_TRY(db.alloc((size_t)g.O * es, &dgb));
+  DCN_TRY(db.alloc(nwo * es, &dgwo));
+  DCN_TRY(db.alloc((size_t)g.J * es, &dgbo));
+  DCN_TRY(db.alloc(noff * es, &dgoff));
+  DCN_TRY(h2d(h, dx, x, nx * es));
+  DCN_TRY(h2d(h, doff, off, noff * es));
+  DCN_TRY(h2d(h, dwo, w_off, nwo * es));
+  DCN_TRY(h2d(h, dw, w, nw * es));
+  DCN_TRY(h2d(h, dgo, grad_out, nout * es));
   const size_t wsb = ws_layout(g, true).total;
   DCN_TRY(ensure_ws(h, wsb));
   DCN_TRY(dcn_backward(h, d, dx, doff, dwo, dw, dgo, dgx, dgw, dgb, dgwo, dgbo, dgoff, h->ws,
                        h->ws_bytes, 0));
-  DCN_TRY(d2h(h, grad_x, dgx, nx));
-  DCN_TRY(d2h(h, grad_w, dgw, nw));
-  if (d->has_bias) DCN_TRY(d2h(h, grad_b, dgb, g.O));
-  DCN_TRY(d2h(h, grad_w_off, dgwo, nwo));
-  DCN_TRY(d2h(h, grad_b_off, dgbo, g.J));
-  if (grad_off_out) DCN_TRY(d2h(h, grad_off_out, dgoff, noff));
+  DCN_TRY(d2h(h, grad_x, dgx, nx * es));
+  DCN_TRY(d2h(h, grad_w, dgw, nw * es));
+  if (d->has_bias) DCN_TRY(d2h(h, grad_b, dgb, g.O * es));
+  DCN_TRY(d2h(h, grad_w_off, dgwo, nwo * es));
+  DCN_TRY(d2h(h, grad_b_off, dgbo, g.J * es));
+  if (grad_off_out) DCN_TRY(d2h(h, grad_off_out, dgoff, noff * es));
   HIP_TRY(hipStreamSynchronize(h->stream));
   return DCN_OK;
 }

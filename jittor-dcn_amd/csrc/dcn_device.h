@@ -16,6 +16,45 @@ namespace dcn {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// ---- bf16 storage (DCN_BF16): round-to-nearest-even conversions (v_cvt_pk_bf16_f32) and
+// 4-channel loads / stores, so kernels can be templated on the element type.
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  return __builtin_bit_cast(bf16_t, (__bf16)f);
+}
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float((unsigned)v << 16); }
+
+__device__ __forceinline__ float4 ld4(const float* p) {
+  return *reinterpret_cast<const float4*>(p);
+}
+__device__ __forceinline__ float4 ld4(const bf16_t* p) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                     __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+}
+template <bool NT>
+__device__ __forceinline__ void st4(float* p, float4 v) {
+  if constexpr (NT) {
+    __builtin_nontemporal_store(v.x, p);
+    __builtin_nontemporal_store(v.y, p + 1);
+    __builtin_nontemporal_store(v.z, p + 2);
+    __builtin_nontemporal_store(v.w, p + 3);
+  } else {
+    *reinterpret_cast<float4*>(p) = v;
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void st4(bf16_t* p, float4 v) {
+  uint2 u;
+  u.x = (unsigned)f2bf(v.x) | ((unsigned)f2bf(v.y) << 16);
+  u.y = (unsigned)f2bf(v.z) | ((unsigned)f2bf(v.w) << 16);
+  if constexpr (NT) {
+    __builtin_nontemporal_store(u.x, reinterpret_cast<unsigned*>(p));
+    __builtin_nontemporal_store(u.y, reinterpret_cast<unsigned*>(p) + 1);
+  } else {
+    *reinterpret_cast<uint2*>(p) = u;
+  }
+}
+
 // deform_conv.py:64-68 (grid (w,h) + offset), :37-39 (norm by (W_out-1),(H_out-1);
 // grid = [norm_y, norm_x]) and grid_sample's align_corners=True unnormalisation
 // ((g+1)/2)*(size-1): grid[...,0] = norm_y indexes the input COLUMN, grid[...,1]

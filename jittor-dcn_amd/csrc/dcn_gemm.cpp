@@ -41,7 +41,7 @@ struct Plan {
 
 auto key_of(const GemmSpec& s) {
   return std::make_tuple(s.ta, s.tb, s.m, s.n, s.k, s.lda, s.ldb, s.ldc, s.sa, s.sb, s.sc,
-                         s.batch);
+                         s.batch, s.bf16_ab, s.bf16_c);
 }
 
 }  // namespace
@@ -88,22 +88,34 @@ void gemm_engine_destroy(GemmEngine* e) {
   delete e;
 }
 
-static int run_rocblas(GemmEngine* e, const GemmSpec& s, const float* A, const float* B,
-                       float* C, hipStream_t st, std::string* err) {
+static int run_rocblas(GemmEngine* e, const GemmSpec& s, const void* A, const void* B, void* C,
+                       hipStream_t st, std::string* err) {
   const float one = 1.f, zero = 0.f;
   (void)rocblas_set_stream(e->rb, st);
-  rocblas_status r = rocblas_sgemm_strided_batched(
-      e->rb, s.ta ? rocblas_operation_transpose : rocblas_operation_none,
-      s.tb ? rocblas_operation_transpose : rocblas_operation_none, s.m, s.n, s.k, &one, A, s.lda,
-      s.sa, B, s.ldb, s.sb, &zero, C, s.ldc, s.sc, s.batch);
+  const rocblas_operation oa = s.ta ? rocblas_operation_transpose : rocblas_operation_none;
+  const rocblas_operation ob = s.tb ? rocblas_operation_transpose : rocblas_operation_none;
+  rocblas_status r;
+  if (!s.bf16_ab && !s.bf16_c) {
+    r = rocblas_sgemm_strided_batched(e->rb, oa, ob, s.m, s.n, s.k, &one,
+                                      static_cast<const float*>(A), s.lda, s.sa,
+                                      static_cast<const float*>(B), s.ldb, s.sb, &zero,
+                                      static_cast<float*>(C), s.ldc, s.sc, s.batch);
+  } else {
+    const rocblas_datatype tab = s.bf16_ab ? rocblas_datatype_bf16_r : rocblas_datatype_f32_r;
+    const rocblas_datatype tc = s.bf16_c ? rocblas_datatype_bf16_r : rocblas_datatype_f32_r;
+    r = rocblas_gemm_strided_batched_ex(e->rb, oa, ob, s.m, s.n, s.k, &one, A, tab, s.lda, s.sa,
+                                        B, tab, s.ldb, s.sb, &zero, C, tc, s.ldc, s.sc, C, tc,
+                                        s.ldc, s.sc, s.batch, rocblas_datatype_f32_r,
+                                        rocblas_gemm_algo_standard, 0, 0);
+  }
   if (r != rocblas_status_success) {
-    *err = std::string("rocblas_sgemm_strided_batched: ") + rocblas_status_to_string(r);
+    *err = std::string("rocblas gemm: ") + rocblas_status_to_string(r);
     return -1;
   }
   return 0;
 }
 
-static int run_lt(GemmEngine* e, const Plan& p, const float* A, const float* B, float* C,
+static int run_lt(GemmEngine* e, const Plan& p, const void* A, const void* B, void* C,
                   hipStream_t st, std::string* err) {
   const float one = 1.f, zero = 0.f;
   hipblasStatus_t r = hipblasLtMatmul(e->lt, p.desc, &one, A, p.la, B, p.lb, &zero, C, p.lc, C,
@@ -123,8 +135,9 @@ static bool lt_describe(GemmEngine* e, const GemmSpec& s, Plan& p) {
   const int32_t ta = s.ta ? HIPBLAS_OP_T : HIPBLAS_OP_N, tb = s.tb ? HIPBLAS_OP_T : HIPBLAS_OP_N;
   hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
   hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
-  auto mk = [&](hipblasLtMatrixLayout_t* L, int rows, int cols, int ld, long stride) {
-    if (hipblasLtMatrixLayoutCreate(L, HIP_R_32F, rows, cols, ld) != HIPBLAS_STATUS_SUCCESS)
+  auto mk = [&](hipblasLtMatrixLayout_t* L, int rows, int cols, int ld, long stride, bool bf) {
+    if (hipblasLtMatrixLayoutCreate(L, bf ? HIP_R_16BF : HIP_R_32F, rows, cols, ld) !=
+        HIPBLAS_STATUS_SUCCESS)
       return false;
     const int32_t bc = s.batch;
     const int64_t so = stride;
@@ -134,9 +147,9 @@ static bool lt_describe(GemmEngine* e, const GemmSpec& s, Plan& p) {
     return true;
   };
   // stored shapes (column-major): A is m×k (or k×m when transposed), B is k×n (n×k)
-  return mk(&p.la, s.ta ? s.k : s.m, s.ta ? s.m : s.k, s.lda, s.sa) &&
-         mk(&p.lb, s.tb ? s.n : s.k, s.tb ? s.k : s.n, s.ldb, s.sb) &&
-         mk(&p.lc, s.m, s.n, s.ldc, s.sc);
+  return mk(&p.la, s.ta ? s.k : s.m, s.ta ? s.m : s.k, s.lda, s.sa, s.bf16_ab) &&
+         mk(&p.lb, s.tb ? s.n : s.k, s.tb ? s.k : s.n, s.ldb, s.sb, s.bf16_ab) &&
+         mk(&p.lc, s.m, s.n, s.ldc, s.sc, s.bf16_c);
 }
 
 static float time_ms(hipStream_t st, const std::function<int()>& fn) {
@@ -160,7 +173,7 @@ static float time_ms(hipStream_t st, const std::function<int()>& fn) {
   return best;
 }
 
-static int tune(GemmEngine* e, const GemmSpec& s, const float* A, const float* B, float* C,
+static int tune(GemmEngine* e, const GemmSpec& s, const void* A, const void* B, void* C,
                 hipStream_t st, Plan& best, std::string* err) {
   std::string e1;
   best.backend = 0;
@@ -212,7 +225,7 @@ static int tune(GemmEngine* e, const GemmSpec& s, const float* A, const float* B
   return 0;
 }
 
-int gemm_run(GemmEngine* e, const GemmSpec& s, const float* A, const float* B, float* C,
+int gemm_run(GemmEngine* e, const GemmSpec& s, const void* A, const void* B, void* C,
              hipStream_t st, std::string* err) {
   auto it = e->plans.find(key_of(s));
   if (it == e->plans.end()) {

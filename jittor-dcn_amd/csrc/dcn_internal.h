@@ -10,6 +10,8 @@
 
 namespace dcn {
 
+typedef unsigned short bf16_t;  // bf16 storage (DCN_BF16)
+
 // Derived geometry of one call. All fields are plain ints so the struct is
 // passed to kernels by value (kernarg segment, scalar registers).
 struct Geo {
@@ -22,12 +24,22 @@ struct Geo {
   int HWi;     // H*W
   int Cg;      // channels per deform group
   int J;       // offset channels = 2*N*G
+  int dt;      // DCN_F32 / DCN_BF16 (tensor storage type of the call)
 };
 
 // Launchers. All stream-ordered, return hipError_t.
 // dcn_sampling.hip (channels-last columns colT[b][m][n*C + c]):
 hipError_t launch_nchw_to_nhwc(const float* in, float* out, int B, int C, int P, hipStream_t s);
 hipError_t launch_nhwc_to_nchw(const float* in, float* out, int B, int C, int P, hipStream_t s);
+hipError_t launch_nchw_to_nhwc_bf16(const bf16_t* in, bf16_t* out, int B, int C, int P,
+                                    hipStream_t s);
+// bf16 columns / ∂columns (DCN_BF16; needs bf16_path_ok(g)): same kernels, bf16 rows.
+bool bf16_path_ok(const Geo& g);
+hipError_t launch_im2col_bf16(const Geo& g, const float* xT, const float* off, bf16_t* colT,
+                              int b0, int nb, hipStream_t s);
+hipError_t launch_col2im_bf16(const Geo& g, const float* xT, const float* off,
+                              const bf16_t* gcolT, float* gx, float* gxT, float* goff,
+                              void* bins_ws, int b0, int nb, bool bins_ready, hipStream_t s);
 hipError_t launch_im2col(const Geo& g, const float* x, const float* xT, const float* off,
                          float* colT, int b0, int nb, hipStream_t s);
 size_t bins_ws_bytes(const Geo& g, int nb);
@@ -54,7 +66,14 @@ hipError_t launch_offset_conv_fwd(const Geo& g, const float* x, const float* w_o
 hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
                                   const float* w_off, const float* goff, float* goffT, float* wt2,
                                   float* gx, float* gw_off, float* gb_off, hipStream_t s);
-// dcn_reduce.hip:
+// dcn_reduce.hip conversions: bf16 <-> f32 (RNE), and the bf16 rounding of a f32 tensor
+// in place (out = bf16(v), v = f32(out)) so later f32 work sees exactly the bf16 value.
+hipError_t launch_bf16_to_f32(const bf16_t* in, float* out, size_t n, hipStream_t s);
+hipError_t launch_f32_to_bf16(const float* in, bf16_t* out, size_t n, hipStream_t s);
+hipError_t launch_round_to_bf16(float* v, bf16_t* out, size_t n, hipStream_t s);
+// out_bf[b][o][m] = bf16(out32[b][o][m] + bias[o]) (bias may be null)
+hipError_t launch_bias_to_bf16(const Geo& g, const float* out32, const float* bias, bf16_t* out,
+                               hipStream_t s);
 void launch_channel_sum(const float* in, int B, int Cn, int HW, float* out, hipStream_t s);
 hipError_t launch_bias_add(const Geo& g, float* out, const float* bias, int b0, int nb,
                            hipStream_t s);
@@ -68,11 +87,14 @@ struct GemmSpec {
   int m = 0, n = 0, k = 0, lda = 0, ldb = 0, ldc = 0;
   long sa = 0, sb = 0, sc = 0;
   int batch = 1;
+  bool bf16_ab = false;  // A and B are bf16 (DCN_BF16); compute is always fp32
+  bool bf16_c = false;   // C is bf16 (else fp32)
 };
 struct GemmEngine;
 int gemm_engine_create(GemmEngine** out, std::string* err);
 void gemm_engine_destroy(GemmEngine* e);
-int gemm_run(GemmEngine* e, const GemmSpec& s, const float* A, const float* B, float* C,
+// A, B, C point to fp32 or bf16 elements as the spec says
+int gemm_run(GemmEngine* e, const GemmSpec& s, const void* A, const void* B, void* C,
              hipStream_t st, std::string* err);
 int gemm_backend_of(GemmEngine* e, const GemmSpec& s);  // -1 untuned, 0 rocBLAS, 1 hipBLASLt
 

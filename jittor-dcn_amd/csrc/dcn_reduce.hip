@@ -105,4 +105,73 @@ hipError_t launch_sum_partials(const float* parts, int nparts, size_t n, float* 
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// DCN_BF16 conversions (elementwise; grid-stride, 4 per thread).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bf16_to_f32_kernel(const bf16_t* __restrict__ in,
+                                                          float* __restrict__ out, size_t n) {
+  for (size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n;
+       i += (size_t)gridDim.x * 256 * 4) {
+    if (i + 4 <= n && (((uintptr_t)(in + i) & 7) | ((uintptr_t)(out + i) & 15)) == 0) {
+      *reinterpret_cast<float4*>(out + i) = ld4(in + i);
+    } else {
+      for (size_t k = i; k < n && k < i + 4; ++k) out[k] = bf2f(in[k]);
+    }
+  }
+}
+__global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float* __restrict__ in,
+                                                          bf16_t* __restrict__ out, size_t n) {
+  for (size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n;
+       i += (size_t)gridDim.x * 256 * 4) {
+    if (i + 4 <= n && (((uintptr_t)(in + i) & 15) | ((uintptr_t)(out + i) & 7)) == 0) {
+      st4<false>(out + i, *reinterpret_cast<const float4*>(in + i));
+    } else {
+      for (size_t k = i; k < n && k < i + 4; ++k) out[k] = f2bf(in[k]);
+    }
+  }
+}
+__global__ __launch_bounds__(256) void round_bf16_kernel(float* __restrict__ v,
+                                                         bf16_t* __restrict__ out, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    const bf16_t r = f2bf(v[i]);
+    out[i] = r;
+    v[i] = bf2f(r);
+  }
+}
+__global__ __launch_bounds__(256) void bias_to_bf16_kernel(const float* __restrict__ in,
+                                                           const float* __restrict__ bias,
+                                                           bf16_t* __restrict__ out, int O, int HW,
+                                                           size_t n) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    float v = in[i];
+    if (bias) v += bias[(i / HW) % O];
+    out[i] = f2bf(v);
+  }
+}
+
+static unsigned grid_for(size_t n, size_t per_thread) {
+  const size_t b = (n + 256 * per_thread - 1) / (256 * per_thread);
+  return (unsigned)(b < 16384 ? (b ? b : 1) : 16384);
+}
+
+hipError_t launch_bf16_to_f32(const bf16_t* in, float* out, size_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(bf16_to_f32_kernel, dim3(grid_for(n, 4)), dim3(256), 0, s, in, out, n);
+  return hipGetLastError();
+}
+hipError_t launch_f32_to_bf16(const float* in, bf16_t* out, size_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(grid_for(n, 4)), dim3(256), 0, s, in, out, n);
+  return hipGetLastError();
+}
+hipError_t launch_round_to_bf16(float* v, bf16_t* out, size_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(round_bf16_kernel, dim3(grid_for(n, 1)), dim3(256), 0, s, v, out, n);
+  return hipGetLastError();
+}
+hipError_t launch_bias_to_bf16(const Geo& g, const float* out32, const float* bias, bf16_t* out,
+                               hipStream_t s) {
+  const size_t n = (size_t)g.B * g.O * g.HW;
+  hipLaunchKernelGGL(bias_to_bf16_kernel, dim3(grid_for(n, 1)), dim3(256), 0, s, out32, bias, out,
+                     g.O, g.HW, n);
+  return hipGetLastError();
+}
+
 }  // namespace dcn

@@ -207,10 +207,10 @@ struct Win {
   static constexpr int PIX = R * Q;
 };
 
-template <int TH, int TW, int MAR, int CS, bool NT>
+template <int TH, int TW, int MAR, int CS, bool NT, typename OT = float>
 __global__ __launch_bounds__(256) void im2col_lds(Geo g, const float* __restrict__ xT,
                                                   const float* __restrict__ off,
-                                                  float* __restrict__ colT, int b0, int tw_n) {
+                                                  OT* __restrict__ colT, int b0, int tw_n) {
   typedef Win<TH, TW, MAR> Wn;
   constexpr int kTP = TH * TW;
   constexpr int LPS = CS / 4, GS = 256 / LPS;  // lanes per sample, samples per block step
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(256) void im2col_lds(Geo g, const float* __restrict
     rec[sidx] = r;
   }
   const float* xb = xT + (size_t)b * g.HWi * g.C;
-  float* cb = colT + (size_t)bl * g.HW * g.K;
+  OT* cb = colT + (size_t)bl * g.HW * g.K;
   const int grp = tid / LPS, cl = tid % LPS;  // GS sample groups of LPS lanes
   for (int cs = 0; cs < g.C; cs += CS) {
     const int c = cs + cl * 4;
@@ -288,17 +288,7 @@ __global__ __launch_bounds__(256) void im2col_lds(Geo g, const float* __restrict
         }
         o = bilerp4(fr, fc, a, bq, cq, d);
       }
-      if (cok) {
-        float4* dst = reinterpret_cast<float4*>(cb + (size_t)m * g.K + (size_t)n * g.C + c);
-        if constexpr (NT) {
-          __builtin_nontemporal_store(o.x, &dst->x);
-          __builtin_nontemporal_store(o.y, &dst->y);
-          __builtin_nontemporal_store(o.z, &dst->z);
-          __builtin_nontemporal_store(o.w, &dst->w);
-        } else {
-          *dst = o;
-        }
-      }
+      if (cok) st4<NT>(cb + (size_t)m * g.K + (size_t)n * g.C + c, o);
     }
   }
 }
@@ -507,11 +497,11 @@ __device__ __forceinline__ float4 add4(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
 
-template <int U, int kTQ>
+template <int U, int kTQ, typename GT = float>
 __global__ __launch_bounds__(kC2iThreads) void col2im_tile(Geo g, const float* __restrict__ xT,
                                                            const int4* __restrict__ brec,
                                                            const int* __restrict__ start,
-                                                           const float* __restrict__ gcolT,
+                                                           const GT* __restrict__ gcolT,
                                                            float* __restrict__ gxT,
                                                            float* __restrict__ goff, int b0,
                                                            int tq_n) {
@@ -540,7 +530,7 @@ __global__ __launch_bounds__(kC2iThreads) void col2im_tile(Geo g, const float* _
   const int NB = (g.H + 1) * (g.W + 1);
   const int* st = start + (size_t)bl * (NB + 1);
   const int4* rb = brec + (size_t)bl * g.HW * g.N;
-  const float* gb = gcolT + (size_t)bl * g.HW * g.K;
+  const GT* gb = gcolT + (size_t)bl * g.HW * g.K;
   float* gob = goff + (size_t)b * g.J * g.HW;
   const float sy = (float)(g.H - 1) / (float)(g.Wo - 1);
   const float sx = (float)(g.W - 1) / (float)(g.Ho - 1);
@@ -582,7 +572,7 @@ __global__ __launch_bounds__(kC2iThreads) void col2im_tile(Geo g, const float* _
                           __builtin_amdgcn_readlane(pg.z, l), __builtin_amdgcn_readlane(pg.w, l));
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) nx[u] = *reinterpret_cast<const float4*>(gb + nR[u].x + cc);
+      for (int u = 0; u < U; ++u) nx[u] = ld4(gb + nR[u].x + cc);
     };
     issue(rowlo);
 #pragma unroll
@@ -767,12 +757,13 @@ __global__ __launch_bounds__(256) void dx_gather_cl(Geo g, LaneMap L,
 // Transposes (64x64 tiles through LDS, odd pitch).
 // ---------------------------------------------------------------------------
 // out[b][p][c] = in[b][c][p]
-__global__ __launch_bounds__(256) void nchw_to_nhwc(const float* __restrict__ in,
-                                                    float* __restrict__ out, int C, int P) {
-  __shared__ float t[64][65];
+template <typename T>
+__global__ __launch_bounds__(256) void nchw_to_nhwc(const T* __restrict__ in, T* __restrict__ out,
+                                                    int C, int P) {
+  __shared__ T t[64][65];
   const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64, b = blockIdx.z;
-  const float* ib = in + (size_t)b * C * P;
-  float* ob = out + (size_t)b * C * P;
+  const T* ib = in + (size_t)b * C * P;
+  T* ob = out + (size_t)b * C * P;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   for (int i = ty; i < 64; i += 4) {
     const int c = c0 + i, p = p0 + tx;
@@ -806,7 +797,14 @@ __global__ __launch_bounds__(256) void nhwc_to_nchw(const float* __restrict__ in
 
 hipError_t launch_nchw_to_nhwc(const float* in, float* out, int B, int C, int P, hipStream_t s) {
   dim3 grid((P + 63) / 64, (C + 63) / 64, B);
-  hipLaunchKernelGGL(nchw_to_nhwc, grid, dim3(256), 0, s, in, out, C, P);
+  hipLaunchKernelGGL(nchw_to_nhwc<float>, grid, dim3(256), 0, s, in, out, C, P);
+  return hipGetLastError();
+}
+
+hipError_t launch_nchw_to_nhwc_bf16(const bf16_t* in, bf16_t* out, int B, int C, int P,
+                                    hipStream_t s) {
+  dim3 grid((P + 63) / 64, (C + 63) / 64, B);
+  hipLaunchKernelGGL(nchw_to_nhwc<bf16_t>, grid, dim3(256), 0, s, in, out, C, P);
   return hipGetLastError();
 }
 
@@ -948,7 +946,7 @@ hipError_t launch_im2col(const Geo& g, const float* x, const float* xT, const fl
 }
 
 static bool k5_fused(const Geo& g) {
-  return g.G == 1 && g.C % 4 == 0 && g.C <= 256 && exp_flag(2) == 0;
+  return g.G == 1 && g.C % 4 == 0 && g.C <= 256 && (g.dt == DCN_BF16 || exp_flag(2) == 0);
 }
 
 // Pointers into the bins workspace (bins_ws_bytes layout).
@@ -1052,6 +1050,44 @@ hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, co
       hipLaunchKernelGGL(dx_gather_cl<1>, grid, dim3(256), 0, s, g, L, P.rec, P.start, P.list,
                          gcolT, gxT, b0);
   }
+  return launch_nhwc_to_nchw(gxT + (size_t)b0 * g.HWi * g.C, gx + (size_t)b0 * g.C * g.HWi, nb,
+                             g.C, g.HWi, s);
+}
+
+// ---- DCN_BF16: bf16 column rows through the same LDS-window / fused kernels ----------
+bool bf16_path_ok(const Geo& g) { return g.G == 1 && g.N <= kMaxTaps && g.C % 4 == 0 && g.C <= 256; }
+
+hipError_t launch_im2col_bf16(const Geo& g, const float* xT, const float* off, bf16_t* colT,
+                              int b0, int nb, hipStream_t s) {
+  if (nb <= 0) return hipSuccess;
+  auto go = [&](auto kern, int TH, int TW) {
+    const int th_n = (g.Ho + TH - 1) / TH, tw_n = (g.Wo + TW - 1) / TW;
+    hipLaunchKernelGGL(kern, dim3(th_n * tw_n, 1, nb), dim3(256), 0, s, g, xT, off, colT, b0,
+                       tw_n);
+  };
+  if (g.C <= 32)
+    go(im2col_lds<8, 8, 2, 32, true, bf16_t>, 8, 8);
+  else if (g.C <= 64)
+    go(im2col_lds<8, 8, 2, 64, true, bf16_t>, 8, 8);
+  else if (g.C <= 128)
+    go(im2col_lds<4, 4, 1, 128, true, bf16_t>, 4, 4);
+  else
+    go(im2col_lds<4, 4, 1, 256, true, bf16_t>, 4, 4);
+  return hipGetLastError();
+}
+
+hipError_t launch_col2im_bf16(const Geo& g, const float* xT, const float* off,
+                              const bf16_t* gcolT, float* gx, float* gxT, float* goff,
+                              void* bins_ws, int b0, int nb, bool bins_ready, hipStream_t s) {
+  if (nb <= 0) return hipSuccess;
+  if (!bins_ready) {
+    const hipError_t e = launch_bins(g, off, bins_ws, goff, b0, nb, s);
+    if (e != hipSuccess) return e;
+  }
+  const BinsWs P = bins_ptrs(g, bins_ws, nb);
+  const int tr_n = (g.H + kTR - 1) / kTR, tq_n = (g.W + 4 - 1) / 4;
+  hipLaunchKernelGGL((col2im_tile<2, 4, bf16_t>), dim3(tr_n * tq_n, 1, nb), dim3(kC2iThreads), 0,
+                     s, g, xT, P.brec, P.start, gcolT, gxT, goff, b0, tq_n);
   return launch_nhwc_to_nchw(gxT + (size_t)b0 * g.HWi * g.C, gx + (size_t)b0 * g.C * g.HWi, nb,
                              g.C, g.HWi, s);
 }

@@ -75,7 +75,9 @@ def test_out_shape_and_workspace():
     (dict(H=2, W=2, padding=(0, 0)), "empty output"),
     (dict(H=3, W=8, padding=(0, 1)), "divides"),        # H_out == 1 (deform_conv.py:38)
     (dict(deform_groups=3), "divisible"),
-    (dict(dtype=rt.DCN_BF16), "only DCN_F32"),
+    (dict(dtype=7), "unknown dtype"),
+    (dict(dtype=rt.DCN_BF16, C=6), "DCN_BF16 needs"),      # C % 4 != 0
+    (dict(dtype=rt.DCN_BF16, C=512), "DCN_BF16 needs"),    # C > 256
 ])
 def test_invalid_descriptors_are_rejected(bad, msg):
     with pytest.raises(RuntimeError, match=msg):
