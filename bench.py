@@ -95,7 +95,7 @@ def load_traffic(path, bf16=False):
             doc = json.load(f)
     except (OSError, ValueError):
         return None, None
-    for name, v in doc.get("kernels", {}).items():
+    for name, v in doc.get("config4" if bf16 else "kernels", {}).items():
         if name.startswith(K1_KERNEL) and (("unsigned short" in name) == bf16):
             return int(v["hbm_bytes"]), f"{os.path.relpath(paths[-1], ROOT)}:{name}"
     return None, None
