@@ -193,14 +193,15 @@ __global__ __launch_bounds__(256) void offset_conv_combine(const float* __restri
   off[i] = v;
 }
 
-constexpr int kWgradPpw = 256;  // pixels per wave in offset_wgrad_valu
+constexpr int kWgradRpw = 4;  // output rows per wave in offset_wgrad_valu
 
 struct WgradGrid {
   unsigned nbx, ny, nz;
   int cper;  // channels per wave (64 lanes x VEC)
 };
-static WgradGrid wgrad_grid(const Geo& g) {
-  const long waves = ((long)g.B * g.HW + kWgradPpw - 1) / kWgradPpw;
+static int wgrad_rpw() { return exp_flag(7) ? exp_flag(7) : kWgradRpw; }
+static WgradGrid wgrad_grid(const Geo& g, int rpw) {
+  const long waves = ((long)g.B * g.Ho + rpw - 1) / rpw;
   WgradGrid w;
   w.cper = g.C % 4 == 0 ? 256 : 64;
   w.nbx = (unsigned)((waves + 3) / 4);
@@ -220,7 +221,7 @@ static size_t goffT_rows_floats(const Geo& g) {
 template <int VEC>
 __global__ __launch_bounds__(256) void offset_wgrad_valu(Geo g, const float* __restrict__ xT,
                                                          const float* __restrict__ goffT,
-                                                         float* __restrict__ part, int ppw,
+                                                         float* __restrict__ part, int rpw,
                                                          int nbx, int ny, int nz) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably wave-uniform
@@ -233,58 +234,57 @@ __global__ __launch_bounds__(256) void offset_wgrad_valu(Geo g, const float* __r
   const int tap = by % KK, j0 = (by / KK) * kJB;
   const int c = (bz * 64 + lane) * VEC;
   const bool cok = c < g.C;
-  const long Mtot = (long)g.B * g.HW;
-  const long pstart = ((long)bx * 4 + wave) * ppw;
-  const long pend = max(pstart, min(pstart + (long)ppw, Mtot));  // empty for tail waves
+  // this wave's output rows (flattened (b, ho)); a tap's valid pixels in a row are one
+  // contiguous wo range, so the inner loop is branch-free pointer strides (the per-pixel
+  // (b, ho, wo) walk cost more scalar instructions than the FMAs)
+  const int rows = g.B * g.Ho;
+  const int rstart = min(rows, (bx * 4 + wave) * rpw), rend = min(rows, rstart + rpw);
   const int ti = tap / g.kw, tx = tap - ti * g.kw;
   const int dyo = ti * g.dh - g.ph, dxo = tx * g.dw - g.pw;
-  int b = (int)(pstart / g.HW);
-  int mm = (int)(pstart - (long)b * g.HW);
-  int ho = mm / g.Wo, wo = mm - (mm / g.Wo) * g.Wo;
+  const int wlo = dxo >= 0 ? 0 : (-dxo + g.sw - 1) / g.sw;
+  const int whi = g.W - 1 - dxo < 0 ? 0 : min(g.Wo, (g.W - 1 - dxo) / g.sw + 1);
+  const int cc = cok ? c : 0;
+  const long sstep = (long)g.sw * g.C;
   float acc[kJB][VEC];
 #pragma unroll
   for (int jj = 0; jj < kJB; ++jj)
 #pragma unroll
     for (int e = 0; e < VEC; ++e) acc[jj][e] = 0.f;
-  // 4-pixel batches: the batch's xT rows (1 KiB each) and ∂offT rows (scalar) are all
-  // in flight before its 4*kJB*VEC FMAs consume them
-  constexpr int U = 4;
-  for (long p0 = pstart; p0 < pend; p0 += U) {
-    float v[U][VEC];
-    const float* gp[U];
+  constexpr int U = 4;  // pixels whose xT rows / ∂offT rows are in flight together
+  for (int row = rstart; row < rend; ++row) {
+    const int b = row / g.Ho, ho = row - b * g.Ho;
+    const int y = ho * g.sh + dyo;
+    if (y < 0 || y >= g.H || wlo >= whi) continue;  // wave-uniform
+    const float* src = xT + (((size_t)b * g.H + y) * g.W + (wlo * g.sw + dxo)) * g.C + cc;
+    const float* gp = goffT + ((size_t)b * g.HW + (size_t)ho * g.Wo + wlo) * Jp + j0;
+    const int n = whi - wlo;
+    for (int i = 0; i < n; i += U) {
+      float v[U][VEC];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long p = p0 + u;
-      const int y = ho * g.sh + dyo, xx = wo * g.sw + dxo;
-      const bool ok = p < pend && y >= 0 && y < g.H && xx >= 0 && xx < g.W;  // wave-uniform
-      gp[u] = goffT + (size_t)(p < pend ? p : pstart) * Jp + j0;  // wave-uniform, zero-padded
-      const float* src = xT + (((size_t)b * g.H + (ok ? y : 0)) * g.W + (ok ? xx : 0)) * g.C + c;
-      if constexpr (VEC == 4) {
-        float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (ok && cok) t = *reinterpret_cast<const float4*>(src);
-        v[u][0] = t.x;
-        v[u][1] = t.y;
-        v[u][2] = t.z;
-        v[u][3] = t.w;
-      } else {
-        v[u][0] = (ok && cok) ? *src : 0.f;
+      for (int u = 0; u < U; ++u) {
+        const float* sp = src + min(i + u, n - 1) * sstep;
+        if constexpr (VEC == 4) {
+          const float4 t = *reinterpret_cast<const float4*>(sp);
+          v[u][0] = cok ? t.x : 0.f;
+          v[u][1] = cok ? t.y : 0.f;
+          v[u][2] = cok ? t.z : 0.f;
+          v[u][3] = cok ? t.w : 0.f;
+        } else {
+          v[u][0] = cok ? *sp : 0.f;
+        }
       }
-      if (++wo == g.Wo) {
-        wo = 0;
-        if (++ho == g.Ho) {
-          ho = 0;
-          ++b;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (i + u >= n) break;
+        const float* gq = gp + (size_t)(i + u) * Jp;  // wave-uniform, zero-padded
+#pragma unroll
+        for (int jj = 0; jj < kJB; ++jj) {
+          const float gv = gq[jj];
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) acc[jj][e] = fmaf(gv, v[u][e], acc[jj][e]);
         }
       }
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int jj = 0; jj < kJB; ++jj) {
-        const float gv = gp[u][jj];
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) acc[jj][e] = fmaf(gv, v[u][e], acc[jj][e]);
-      }
   }
   // The block's 4 waves cover consecutive pixel ranges of the same (tap, j pass, chunk):
   // fold waves 1..3 into wave 0 through LDS (fixed order), then write one partial per
@@ -462,7 +462,7 @@ size_t offset_conv_fpart_floats(const Geo& g) { return (size_t)kSplit * g.B * g.
 
 // goffT rows, then offset_wgrad_valu's per-block partials.
 size_t offset_conv_goffT_floats(const Geo& g) {
-  const WgradGrid w = wgrad_grid(g);
+  const WgradGrid w = wgrad_grid(g, 1);  // sized for the smallest row count per wave
   return goffT_rows_floats(g) + (size_t)w.nbx * w.ny * w.nz * kJB * w.cper;
 }
 
@@ -524,16 +524,17 @@ hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
                        goffT, g.J, pad_j(g.J), g.HW, total);
   }
   {
-    const WgradGrid w = wgrad_grid(g);
+    const int rpw = wgrad_rpw();
+    const WgradGrid w = wgrad_grid(g, rpw);
     float* part = goffT + goffT_rows_floats(g);
     dim3 grid(w.nbx * w.ny * w.nz), rgrid(kJB * w.cper / 64, w.ny * w.nz);
     const int nbx = (int)w.nbx, ny = (int)w.ny, nz = (int)w.nz;
     if (w.cper == 256) {
-      hipLaunchKernelGGL(offset_wgrad_valu<4>, grid, dim3(256), 0, s, g, xT, goffT, part, kWgradPpw,
+      hipLaunchKernelGGL(offset_wgrad_valu<4>, grid, dim3(256), 0, s, g, xT, goffT, part, rpw,
                          nbx, ny, nz);
       hipLaunchKernelGGL(wgrad_reduce<4>, rgrid, dim3(1024), 0, s, g, part, gw_off, w.nbx, w.nz);
     } else {
-      hipLaunchKernelGGL(offset_wgrad_valu<1>, grid, dim3(256), 0, s, g, xT, goffT, part, kWgradPpw,
+      hipLaunchKernelGGL(offset_wgrad_valu<1>, grid, dim3(256), 0, s, g, xT, goffT, part, rpw,
                          nbx, ny, nz);
       hipLaunchKernelGGL(wgrad_reduce<1>, rgrid, dim3(1024), 0, s, g, part, gw_off, w.nbx, w.nz);
     }
