@@ -76,8 +76,12 @@ const char* dcn_last_error(void);
 int dcn_device_count(int* n);
 int dcn_create(int device, dcn_handle** out);
 int dcn_destroy(dcn_handle* h);
-/* Bind the handle to an existing hipStream_t (NULL = handle's own stream). */
+/* Bind the handle to an existing hipStream_t. NULL is the HIP null (legacy default)
+ * stream, as in every HIP library, so a framework running on its default stream
+ * (e.g. torch's, whose handle is 0) passes it through unchanged. A new handle uses its
+ * own non-blocking stream; dcn_use_own_stream returns to it. */
 int dcn_set_stream(dcn_handle* h, void* hip_stream);
+int dcn_use_own_stream(dcn_handle* h);
 int dcn_get_stream(dcn_handle* h, void** hip_stream);
 int dcn_synchronize(dcn_handle* h);
 

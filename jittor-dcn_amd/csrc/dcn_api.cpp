@@ -542,7 +542,13 @@ int dcn_destroy(dcn_handle* h) {
 
 int dcn_set_stream(dcn_handle* h, void* s) {
   DCN_TRY(set_device(h));
-  h->stream = s ? reinterpret_cast<hipStream_t>(s) : h->own;
+  h->stream = reinterpret_cast<hipStream_t>(s);  // NULL = the HIP null stream
+  return DCN_OK;
+}
+
+int dcn_use_own_stream(dcn_handle* h) {
+  DCN_TRY(set_device(h));
+  h->stream = h->own;
   return DCN_OK;
 }
 

@@ -42,6 +42,7 @@ SIGNATURES = {
     "dcn_create": [ctypes.c_int, ctypes.POINTER(_vp)],
     "dcn_destroy": [_vp],
     "dcn_set_stream": [_vp, _vp],
+    "dcn_use_own_stream": [_vp],
     "dcn_get_stream": [_vp, ctypes.POINTER(_vp)],
     "dcn_synchronize": [_vp],
     "dcn_malloc": [_vp, _sz, ctypes.POINTER(_vp)],
@@ -157,7 +158,12 @@ class Handle:
 
     # --- streams / memory -----------------------------------------------------
     def set_stream(self, stream_ptr: int | None):
+        """Bind to a hipStream_t handle; 0 / None is the HIP null stream (torch's default
+        stream reports 0). use_own_stream() returns to the handle's own stream."""
         check(self.lib.dcn_set_stream(self.h, ctypes.c_void_p(stream_ptr or 0)), "dcn_set_stream")
+
+    def use_own_stream(self):
+        check(self.lib.dcn_use_own_stream(self.h), "dcn_use_own_stream")
 
     def synchronize(self):
         check(self.lib.dcn_synchronize(self.h), "dcn_synchronize")
