@@ -37,18 +37,24 @@ CONFIGS = {
     3: dict(B=64, C=256, O=256, H=56, W=56, k=3, s=1, p=1, dtype="f32"),
     # configs[3] (config 4): N=512 batch-sharded over 8 GPUs = 64 images per GPU, bf16
     4: dict(B=64, C=256, O=256, H=28, W=28, k=3, s=1, p=1, dtype="bf16"),
+    # configs[1] (config 2): forward only, vs the CPU path
+    2: dict(B=8, C=64, O=128, H=56, W=56, k=3, s=1, p=1, dtype="f32", fwd_only=True),
+    # configs[4] (config 5): the DCNv1 option set (extension: dilation 2, 4 deform groups;
+    # parity against our own restatement only)
+    5: dict(B=64, C=512, O=512, H=14, W=14, k=3, s=2, p=1, dil=2, G=4, dtype="f32"),
 }
 
 
-def k1_bytes(B, C, H, W, N, Ho, Wo, elem=4):
+def k1_bytes(B, C, H, W, N, Ho, Wo, elem=4, J=None):
     """Algorithmic HBM bytes of one deformable-im2col launch:
-    read x + read offsets + write columns."""
-    return elem * (B * C * H * W + B * 2 * N * Ho * Wo + B * Ho * Wo * N * C)
+    read x + read offsets (J = 2·N·deform_groups channels) + write columns."""
+    J = 2 * N if J is None else J
+    return elem * (B * C * H * W + B * J * Ho * Wo + B * Ho * Wo * N * C)
 
 
-def cpu_baseline(cfg, budget_s=10.0, threads=None):
+def cpu_baseline(cfg, budget_s=10.0, threads=None, name="config3"):
     """Time the fp32 C restatement (oracle/dcn_ref.c, 'port') on a bounded sample:
-    whole config-3 images, fwd+bwd, one at a time until ~budget_s of CPU work."""
+    whole images of the configuration, fwd(+bwd), one at a time until ~budget_s."""
     import ref_lib as R
     R.build()
     ncpu = os.cpu_count() or 1
@@ -56,26 +62,29 @@ def cpu_baseline(cfg, budget_s=10.0, threads=None):
     R.set_threads(threads)
     rng = np.random.default_rng(0)
     C, O_, H, W, k = cfg["C"], cfg["O"], cfg["H"], cfg["W"], cfg["k"]
+    dil, G, fwd_only = cfg.get("dil", 1), cfg.get("G", 1), cfg.get("fwd_only", False)
     N = k * k
     x = rng.standard_normal((1, C, H, W)).astype(np.float32)
-    wo = (rng.standard_normal((2 * N, C, k, k)) / np.sqrt(C * N)).astype(np.float32)
-    bo = rng.uniform(-0.5, 0.5, 2 * N).astype(np.float32)
+    wo = (rng.standard_normal((2 * N * G, C, k, k)) / np.sqrt(C * N)).astype(np.float32)
+    bo = rng.uniform(-0.5, 0.5, 2 * N * G).astype(np.float32)
     w = (rng.standard_normal((O_, C, k, k)) * np.sqrt(2 / (C * N))).astype(np.float32)
     b = (rng.standard_normal(O_) * 0.1).astype(np.float32)
-    desc = R.make_desc(x.shape, w.shape, (cfg["s"],) * 2, (cfg["p"],) * 2)
+    desc = R.make_desc(x.shape, w.shape, (cfg["s"],) * 2, (cfg["p"],) * 2, (dil, dil), G)
     Ho, Wo = R.out_shape(desc)
     gout = rng.standard_normal((1, O_, Ho, Wo)).astype(np.float32)
     n_img, t0 = 0, time.perf_counter()
     while True:
         out, off = R.forward(desc, x, wo, bo, w, b)
-        R.backward(desc, x, off, wo, w, gout)
+        if not fwd_only:
+            R.backward(desc, x, off, wo, w, gout)
         n_img += 1
         el = time.perf_counter() - t0
         if el >= budget_s or n_img >= 64:
             break
     samples = n_img * Ho * Wo * N
     return {"value": samples / el / 1e9, "unit": "Gsamples/s", "cores": threads, "kind": "port",
-            "sample": f"{n_img} config-3 image(s) (1x{C}x{H}x{W} -> {O_}, k{k}) fwd+bwd, "
+            "sample": f"{n_img} {name} image(s) (1x{C}x{H}x{W} -> {O_}, k{k}) "
+                      f"{'fwd' if fwd_only else 'fwd+bwd'}, "
                       f"oracle/dcn_ref.c fp32 OpenMP, {el:.1f} s on {threads} of {ncpu} host threads"}
 
 
@@ -137,10 +146,12 @@ def main():
     bf16 = cfg["dtype"] == "bf16"
     tdt = torch.bfloat16 if bf16 else torch.float32
     N = k * k
-    desc = rt.make_desc(B, C, H, W, O_, (k, k), (s, s), (p, p),
+    dil, G = cfg.get("dil", 1), cfg.get("G", 1)
+    fwd_only = cfg.get("fwd_only", False)
+    desc = rt.make_desc(B, C, H, W, O_, (k, k), (s, s), (p, p), (dil, dil), G,
                         dtype=rt.DCN_BF16 if bf16 else rt.DCN_F32)
     Ho, Wo = rt.out_shape(desc)
-    J = 2 * N
+    J = 2 * N * G
 
     # synthetic inputs: x ~ N(0,1); offset conv σ = 1/sqrt(C·9) so Δ ~ N(0,1) px;
     # replicated parameters (same seed on every rank), per-rank batch shard
@@ -157,7 +168,7 @@ def main():
     off = torch.empty(B, J, Ho, Wo, device=dev, dtype=tdt)
     gx = torch.empty_like(x)
     # all parameter grads packed in ONE buffer -> one all-reduce per step (dcn_dp)
-    gbuf = dcn_dp.GradBuffer(dcn_dp.param_shapes(C, O_, k, k),
+    gbuf = dcn_dp.GradBuffer(dcn_dp.param_shapes(C, O_, k, k, deform_groups=G),
                              lambda n: torch.empty(n, device=dev, dtype=tdt))
     gflat = gbuf.flat
     gw, gb, gwo, gbo = (gbuf[n] for n in dcn_dp.PARAM_ORDER)
@@ -185,6 +196,8 @@ def main():
     def step():
         rt.check(L.dcn_forward(h.h, desc, P(x), P(w_off), P(b_off), P(w), P(b), P(out), P(off),
                                P(ws), wsb), "dcn_forward")
+        if fwd_only:
+            return
         rt.check(L.dcn_backward(h.h, desc, P(x), P(off), P(w_off), P(w), P(gout), P(gx), P(gw),
                                 P(gb), P(gwo), P(gbo), P(goff), P(ws), wsb, rt.DCN_BWD_COL_IN_WS),
                  "dcn_backward")
@@ -220,15 +233,20 @@ def main():
         if cnt:
             kernel_ms[name] = round(tot / cnt, 4)
     k1_ms = kernel_ms.get("im2col")
-    k1_b = k1_bytes(B, C, H, W, N, Ho, Wo, elem=2 if bf16 else 4)
+    k1_b = k1_bytes(B, C, H, W, N, Ho, Wo, elem=2 if bf16 else 4, J=J)
+    k1_name = K1_KERNEL if (G == 1 and C % 4 == 0) else "dcn::im2col_cl"
 
     samples = B * Ho * Wo * N * world * args.steps
     value = samples / el / 1e9
     if rank == 0:
         achieved = k1_b / (k1_ms * 1e-3) / 1e9 if k1_ms else None
-        traffic, traffic_src = load_traffic(args.traffic_json, bf16)
+        # the committed PMC summary covers the config-3 (fp32) and config-4 (bf16) K1 only
+        traffic, traffic_src = (load_traffic(args.traffic_json, bf16) if args.config in (3, 4)
+                                else (None, None))
         res = {
-            "metric": METRIC,
+            "metric": METRIC if args.config == 3 else
+            f"DCN {'fwd' if fwd_only else 'fwd+bwd'} Gsamples/s (N·H·W·K²/s), BASELINE "
+            f"config {args.config}",
             "value": round(value, 5),
             "unit": "Gsamples/s",
             "n_gpus": world,
@@ -241,14 +259,15 @@ def main():
             "dtype": cfg["dtype"],
             "data": "synthetic",
             "config": {"workload": f"config{args.config}: B={B}/GPU C={C}->O={O_} {H}x{W} k{k} s{s} "
-                                   f"p{p} {cfg['dtype']} DeformConv2d fwd+bwd (+RCCL grad "
-                                   f"all-reduce if N>1)",
+                                   f"p{p} dil{dil} G{G} {cfg['dtype']} DeformConv2d "
+                                   + ("fwd only" if fwd_only else
+                                      "fwd+bwd (+RCCL grad all-reduce if N>1)"),
                        "global_batch": B * world, "B_per_gpu": B, "C": C, "O": O_, "H": H, "W": W,
                        "kernel": k, "stride": s, "padding": p,
                        "parallelism": f"dp{world} (batch-sharded, replicated params)",
                        "grad_allreduce": (args.comm if world > 1 else None)},
             "roofline": {
-                "kernel": f"{K1_KERNEL} (K1, LDS-staged deformable bilinear im2col)",
+                "kernel": f"{k1_name} (K1, deformable bilinear im2col)",
                 "bound": "hbm",
                 "achieved": round(achieved, 1) if achieved else None,
                 "peak": HBM_PEAK_GBS,
@@ -263,7 +282,7 @@ def main():
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_budget)
+            res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_budget, name=f"config{args.config}")
         print(json.dumps(res), flush=True)
     if comm is not None:
         comm.close()

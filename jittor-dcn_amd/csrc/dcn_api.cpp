@@ -289,18 +289,30 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
     ProfScope ps(h, DCN_K_BWD_BIAS);
     HIP_TRY(dcn::launch_bias_grad(g, gout, gb, h->stream));
   }
+  const bool flat = (long)g.B * g.HW * g.K < (1l << 31);
+  const bool flat_dw = flat && g.HW < 256;
   {
-    // ∂Wf[O][K] = Σ_b ∂out_b[O][HW] · colT_b[HW][K]; column-major per image:
-    // P_b(K×O) = colT_b(K×HW) · ∂out_b(HW×O) (NN); then a deterministic Σ_b.
+    // ∂Wf[O][K] = Σ_b ∂out_b[O][HW] · colT_b[HW][K]. Per image, column-major
+    // P_b(K×O) = colT_b(K×HW) · ∂out_b(HW×O) (NN), then a deterministic Σ_b: 1.68 ms at
+    // config 3 against 1.82 ms as one flat GEMM. When the per-image depth HW is tiny
+    // (config 5: HW = 49) the flat NT GEMM over k = B·HW against ∂outT wins instead.
     ProfScope ps(h, DCN_K_GEMM_DW);
     dcn::GemmSpec sp;
-    sp.m = g.K; sp.n = g.O; sp.k = g.HW;
-    sp.lda = g.K; sp.sa = (long)g.K * g.HW;
-    sp.ldb = g.HW; sp.sb = (long)g.O * g.HW;
-    sp.ldc = g.K; sp.sc = (long)g.K * g.O;
-    sp.batch = g.B;
-    GEMM_TRY(h, sp, colT, gout, parts);
-    HIP_TRY(dcn::launch_sum_partials(parts, g.B, (size_t)g.K * g.O, gw, h->stream));
+    if (flat_dw) {
+      HIP_TRY(dcn::launch_nchw_to_nhwc(gout, goutT, g.B, g.O, g.HW, h->stream));
+      sp.tb = true;
+      sp.m = g.K; sp.n = g.O; sp.k = g.B * g.HW;
+      sp.lda = g.K; sp.ldb = g.O; sp.ldc = g.K;
+      GEMM_TRY(h, sp, colT, goutT, gw);
+    } else {
+      sp.m = g.K; sp.n = g.O; sp.k = g.HW;
+      sp.lda = g.K; sp.sa = (long)g.K * g.HW;
+      sp.ldb = g.HW; sp.sb = (long)g.O * g.HW;
+      sp.ldc = g.K; sp.sc = (long)g.K * g.O;
+      sp.batch = g.B;
+      GEMM_TRY(h, sp, colT, gout, parts);
+      HIP_TRY(dcn::launch_sum_partials(parts, g.B, (size_t)g.K * g.O, gw, h->stream));
+    }
   }
   {
     // ∂colT[B·HW][K] = ∂outT · Wf as ONE GEMM over the whole batch (r01 probe: 1.68 ms
@@ -309,8 +321,8 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
     // (NN). Overwrites the columns (no longer needed after ∂W).
     ProfScope ps(h, DCN_K_GEMM_DCOL);
     dcn::GemmSpec sp;
-    if ((long)g.B * g.HW * g.K < (1l << 31)) {
-      HIP_TRY(dcn::launch_nchw_to_nhwc(gout, goutT, g.B, g.O, g.HW, h->stream));
+    if (flat) {
+      if (!flat_dw) HIP_TRY(dcn::launch_nchw_to_nhwc(gout, goutT, g.B, g.O, g.HW, h->stream));
       sp.m = g.K; sp.n = g.B * g.HW; sp.k = g.O;
       sp.lda = g.K; sp.ldb = g.O; sp.ldc = g.K;
       sp.batch = 1;
