@@ -7,6 +7,7 @@
 // Backward = Jittor autodiff of the same graph (train.py:414): ∂b, ∂W (per-image
 //            GEMM partials + deterministic sum), ∂col = Wᵀ·∂out, K5 col2im +
 //            coordinate gradient, offset-conv backward.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -129,7 +130,9 @@ WsLayout ws_layout(const Geo& g, bool bwd) {
   L.part = take(dcn::offset_conv_fpart_floats(g) * sizeof(float));
   L.col = take((size_t)g.B * g.HW * g.K * sizeof(float));
   if (bwd) {
-    L.parts = take((size_t)g.B * g.O * g.K * sizeof(float));
+    // ∂W partials; first also the ∂b tile sums of the fused ∂out transpose
+    L.parts = take(std::max((size_t)g.B * g.O * g.K, dcn::xpose_chsum_floats(g.B, g.O, g.HW)) *
+                   sizeof(float));
     L.goff = take((size_t)g.B * g.J * g.HW * sizeof(float));
     L.goffT = take(dcn::offset_conv_goffT_floats(g) * sizeof(float));
     L.gxT = take((size_t)g.B * g.HWi * g.C * sizeof(float));
@@ -285,12 +288,18 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
     ProfScope ps(h, DCN_K_IM2COL);
     HIP_TRY(dcn::launch_im2col(g, x, xT, off, colT, 0, g.B, h->stream));
   }
-  if (has_bias) {
-    ProfScope ps(h, DCN_K_BWD_BIAS);
-    HIP_TRY(dcn::launch_bias_grad(g, gout, gb, h->stream));
-  }
   const bool flat = (long)g.B * g.HW * g.K < (1l << 31);
   const bool flat_dw = flat && g.HW < 256;
+  {
+    // ∂outT (for the flat GEMMs) and ∂b from one pass over ∂out
+    ProfScope ps(h, DCN_K_BWD_BIAS);
+    if (flat && has_bias)
+      HIP_TRY(dcn::launch_xpose_chsum(gout, goutT, parts, gb, g.B, g.O, g.HW, h->stream));
+    else if (flat)
+      HIP_TRY(dcn::launch_nchw_to_nhwc(gout, goutT, g.B, g.O, g.HW, h->stream));
+    else if (has_bias)
+      HIP_TRY(dcn::launch_bias_grad(g, gout, gb, h->stream));
+  }
   {
     // ∂Wf[O][K] = Σ_b ∂out_b[O][HW] · colT_b[HW][K]. Per image, column-major
     // P_b(K×O) = colT_b(K×HW) · ∂out_b(HW×O) (NN), then a deterministic Σ_b: 1.68 ms at
@@ -299,7 +308,6 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
     ProfScope ps(h, DCN_K_GEMM_DW);
     dcn::GemmSpec sp;
     if (flat_dw) {
-      HIP_TRY(dcn::launch_nchw_to_nhwc(gout, goutT, g.B, g.O, g.HW, h->stream));
       sp.tb = true;
       sp.m = g.K; sp.n = g.O; sp.k = g.B * g.HW;
       sp.lda = g.K; sp.ldb = g.O; sp.ldc = g.K;
@@ -322,7 +330,6 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
     ProfScope ps(h, DCN_K_GEMM_DCOL);
     dcn::GemmSpec sp;
     if (flat) {
-      if (!flat_dw) HIP_TRY(dcn::launch_nchw_to_nhwc(gout, goutT, g.B, g.O, g.HW, h->stream));
       sp.m = g.K; sp.n = g.B * g.HW; sp.k = g.O;
       sp.lda = g.K; sp.ldb = g.O; sp.ldc = g.K;
       sp.batch = 1;

@@ -75,6 +75,11 @@ hipError_t launch_round_to_bf16(float* v, bf16_t* out, size_t n, hipStream_t s);
 hipError_t launch_bias_to_bf16(const Geo& g, const float* out32, const float* bias, bf16_t* out,
                                hipStream_t s);
 void launch_channel_sum(const float* in, int B, int Cn, int HW, float* out, hipStream_t s);
+// in[b][c][p] -> out[b][p][c] and chsum[c] = Σ_{b,p} in[b][c][p] (deterministic); tsum is
+// scratch of xpose_chsum_floats(B, C, P) floats.
+size_t xpose_chsum_floats(int B, int C, int P);
+hipError_t launch_xpose_chsum(const float* in, float* out, float* tsum, float* chsum, int B,
+                              int C, int P, hipStream_t s);
 hipError_t launch_bias_add(const Geo& g, float* out, const float* bias, int b0, int nb,
                            hipStream_t s);
 hipError_t launch_bias_grad(const Geo& g, const float* gout, float* gb, hipStream_t s);

@@ -174,4 +174,60 @@ hipError_t launch_bias_to_bf16(const Geo& g, const float* out32, const float* bi
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// ∂out -> ∂outT (channels-last, B operand of the flat ∂col GEMM) fused with ∂b: each
+// 64-pixel x 64-channel tile also writes its per-channel sum (fixed order), and
+// tile_sum_to_channels folds the B x ceil(HW/64) tile sums per channel in order.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void xpose_chsum(const float* __restrict__ in,
+                                                   float* __restrict__ out,
+                                                   float* __restrict__ tsum, int C, int P) {
+  __shared__ float t[64][65];
+  const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64, b = blockIdx.z;
+  const float* ib = in + (size_t)b * C * P;
+  float* ob = out + (size_t)b * C * P;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int c = c0 + i, p = p0 + tx;
+    t[i][tx] = (c < C && p < P) ? ib[(size_t)c * P + p] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int p = p0 + i, c = c0 + tx;
+    if (c < C && p < P) ob[(size_t)p * C + c] = t[tx][i];
+  }
+  if (threadIdx.x < 64 && c0 + threadIdx.x < C) {
+    float s = 0.f;
+    for (int k = 0; k < 64; ++k) s += t[threadIdx.x][k];
+    tsum[((size_t)b * gridDim.x + blockIdx.x) * C + c0 + threadIdx.x] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void tile_sum_to_channels(const float* __restrict__ tsum,
+                                                            int ntiles, int C,
+                                                            float* __restrict__ out) {
+  __shared__ float red[256];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  float s = 0.f;
+  for (int i = tid; i < ntiles; i += 256) s += tsum[(size_t)i * C + c];
+  red[tid] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] += red[tid + o];
+    __syncthreads();
+  }
+  if (tid == 0) out[c] = red[0];
+}
+
+size_t xpose_chsum_floats(int B, int C, int P) { return (size_t)B * ((P + 63) / 64) * C; }
+
+hipError_t launch_xpose_chsum(const float* in, float* out, float* tsum, float* chsum, int B,
+                              int C, int P, hipStream_t s) {
+  dim3 grid((P + 63) / 64, (C + 63) / 64, B);
+  hipLaunchKernelGGL(xpose_chsum, grid, dim3(256), 0, s, in, out, tsum, C, P);
+  hipLaunchKernelGGL(tile_sum_to_channels, dim3(C), dim3(256), 0, s, tsum, B * ((P + 63) / 64), C,
+                     chsum);
+  return hipGetLastError();
+}
+
 }  // namespace dcn
