@@ -348,8 +348,9 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
     // K5 overwrites grad_x (sampling route) and grad_off
     DCN_TRY(join_aux(h));
     ProfScope ps(h, DCN_K_COL2IM);
-    HIP_TRY(dcn::launch_col2im_coord(g, x, xT, off, colT, gx, gxT, goff, bins, 0, g.B, true,
-                                     h->stream));
+    // ∂x stays channels-last in gxT; the offset-conv ∂x pass finalises it (one write)
+    HIP_TRY(dcn::launch_col2im_coord(g, x, xT, off, colT, dcn::get_force_generic() ? gx : nullptr,
+                                     gxT, goff, bins, 0, g.B, true, h->stream));
   }
   return DCN_OK;
 }
@@ -461,12 +462,12 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
   DCN_TRY(join_aux(h));
   {
     ProfScope ps(h, DCN_K_COL2IM);
-    HIP_TRY(dcn::launch_col2im_bf16(g, xT, off32, col, gx32, F32(L.gxT), goff32, base + L.bins, 0,
+    HIP_TRY(dcn::launch_col2im_bf16(g, xT, off32, col, nullptr, F32(L.gxT), goff32, base + L.bins, 0,
                                     g.B, true, st));
   }
   ProfScope ps(h, DCN_K_OFFSET_BWD);
   HIP_TRY(dcn::launch_offset_conv_bwd(g, x32, xT, F32(L.woff32), goff32, F32(L.goffT), F32(L.wt),
-                                      gx32, F32(L.gwo32), F32(L.gbo32), st));
+                                      gx32, F32(L.gwo32), F32(L.gbo32), F32(L.gxT), st));
   HIP_TRY(dcn::launch_f32_to_bf16(gx32, gx, nx, st));
   HIP_TRY(dcn::launch_f32_to_bf16(F32(L.gwo32), gw_off, nwo, st));
   HIP_TRY(dcn::launch_f32_to_bf16(F32(L.gbo32), gb_off, (size_t)g.J, st));
@@ -662,7 +663,7 @@ int dcn_offset_conv_bwd(dcn_handle* h, const dcn_desc* d, const float* x, const 
   ProfScope ps(h, DCN_K_OFFSET_BWD);
   HIP_TRY(dcn::launch_nchw_to_nhwc(x, xT, g.B, g.C, g.HWi, h->stream));
   HIP_TRY(dcn::launch_offset_conv_bwd(g, x, xT, w_off, grad_off, goffT, wt2, grad_x, grad_w_off,
-                                      grad_b_off, h->stream));
+                                      grad_b_off, nullptr, h->stream));
   return DCN_OK;
 }
 
@@ -763,7 +764,8 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
                         (flags & DCN_BWD_COL_IN_WS) != 0));
   ProfScope ps(h, DCN_K_OFFSET_BWD);
   HIP_TRY(dcn::launch_offset_conv_bwd(g, x, F(L.xT), w_off, goff, F(L.goffT), F(L.wt), grad_x,
-                                      grad_w_off, grad_b_off, h->stream));
+                                      grad_w_off, grad_b_off,
+                                      dcn::get_force_generic() ? nullptr : F(L.gxT), h->stream));
   return DCN_OK;
 }
 

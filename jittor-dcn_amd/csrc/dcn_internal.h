@@ -49,6 +49,8 @@ size_t bins_ws_bytes(const Geo& g, int nb);
 hipError_t launch_bins(const Geo& g, const float* off, void* bins_ws, float* goff, int b0, int nb,
                        hipStream_t s);
 // Overwrites gx (NCHW) and goff for images [b0, b0+nb); gxT is scratch [B][HWi][C].
+// gx == NULL: leave ∂x (sampling route) channels-last in gxT only, for
+// launch_offset_conv_bwd to finalise (not with the generic kernels).
 // bins_ready: launch_bins already ran on bins_ws for these images.
 hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, const float* off,
                                const float* gcolT, float* gx, float* gxT, float* goff,
@@ -62,10 +64,13 @@ size_t offset_conv_fpart_floats(const Geo& g);  // forward channel-slice partial
 hipError_t launch_offset_conv_fwd(const Geo& g, const float* x, const float* w_off,
                                   const float* b_off, float* off, float* wt, float* part,
                                   hipStream_t s);
-// xT: channels-last x; goffT: scratch of offset_conv_goffT_floats(g). grad_x is accumulated.
+// xT: channels-last x; goffT: scratch of offset_conv_goffT_floats(g). gxT_in == NULL:
+// grad_x is accumulated; else grad_x = transpose(gxT_in) + the offset-conv route, written
+// once (gxT_in: the sampling-route ∂x left channels-last by launch_col2im_*).
 hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
                                   const float* w_off, const float* goff, float* goffT, float* wt2,
-                                  float* gx, float* gw_off, float* gb_off, hipStream_t s);
+                                  float* gx, float* gw_off, float* gb_off, const float* gxT_in,
+                                  hipStream_t s);
 // dcn_reduce.hip conversions: bf16 <-> f32 (RNE), and the bf16 rounding of a f32 tensor
 // in place (out = bf16(v), v = f32(out)) so later f32 work sees exactly the bf16 value.
 hipError_t launch_bf16_to_f32(const bf16_t* in, float* out, size_t n, hipStream_t s);

@@ -348,13 +348,14 @@ __global__ __launch_bounds__(1024) void wgrad_reduce(Geo g, const float* __restr
 }
 
 // ---------------------------------------------------------------------------
-// K7b: ∂x[b][c][y][x] += Σ_{j,tap} w_off[j][c][tap] · ∂off[b][j][(y+pad-tap·dil)/s]
+// K7b: ∂x[b][c][y][x] (+)= Σ_{j,tap} w_off[j][c][tap] · ∂off[b][j][(y+pad-tap·dil)/s]
 // One thread per input pixel and kCB channels (grid.y); weights wave-uniform.
 // ---------------------------------------------------------------------------
 template <int KK>
 __global__ __launch_bounds__(256) void offset_dgrad_valu(Geo g, const float* __restrict__ wt2,
                                                          const float* __restrict__ goff,
-                                                         float* __restrict__ gx) {
+                                                         float* __restrict__ gx,
+                                                         const float* __restrict__ gxT_in) {
   const long Mi = (long)g.B * g.HWi;
   const long p = (long)blockIdx.x * 256 + threadIdx.x;
   const bool pok = p < Mi;
@@ -376,8 +377,22 @@ __global__ __launch_bounds__(256) void offset_dgrad_valu(Geo g, const float* __r
   const int cn = min(kCB, g.C - c0);
   const int Cp = pad_c(g.C);
   float acc[kCB];
+  if (gxT_in) {  // start from the sampling-route ∂x (channels-last): one 128-B run per pixel
+    const float* src = gxT_in + ((size_t)b * g.HWi + yx) * g.C + c0;
+    if (pok && cn == kCB && (g.C & 3) == 0) {  // 16-B aligned: 8 dwordx4 loads
 #pragma unroll
-  for (int cc = 0; cc < kCB; ++cc) acc[cc] = 0.f;
+      for (int q = 0; q < kCB / 4; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(src + 4 * q);
+        acc[4 * q] = v.x, acc[4 * q + 1] = v.y, acc[4 * q + 2] = v.z, acc[4 * q + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int cc = 0; cc < kCB; ++cc) acc[cc] = (pok && cc < cn) ? src[cc] : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int cc = 0; cc < kCB; ++cc) acc[cc] = 0.f;
+  }
   const float* gb = goff + (size_t)b * g.J * g.HW;
   for (int j = 0; j < g.J; ++j) {
     const float* gj = gb + (size_t)j * g.HW;
@@ -394,7 +409,10 @@ __global__ __launch_bounds__(256) void offset_dgrad_valu(Geo g, const float* __r
   if (!pok) return;
 #pragma unroll
   for (int cc = 0; cc < kCB; ++cc)
-    if (cc < cn) gx[((size_t)b * g.C + c0 + cc) * g.HWi + yx] += acc[cc];
+    if (cc < cn) {
+      float* d = gx + ((size_t)b * g.C + c0 + cc) * g.HWi + yx;
+      *d = gxT_in ? acc[cc] : *d + acc[cc];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -502,10 +520,12 @@ hipError_t launch_offset_conv_fwd(const Geo& g, const float* x, const float* w_o
   return hipGetLastError();
 }
 
-// xT: channels-last x; goffT, wt2: scratch ([B][HW][J], [J][KK][C]). grad_x is accumulated.
+// xT: channels-last x; goffT, wt2: scratch ([B][HW][J], [J][KK][C]). grad_x is accumulated,
+// or (gxT_in) overwritten with transpose(gxT_in) + the offset-conv route.
 hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
                                   const float* w_off, const float* goff, float* goffT, float* wt2,
-                                  float* gx, float* gw_off, float* gb_off, hipStream_t s) {
+                                  float* gx, float* gw_off, float* gb_off, const float* gxT_in,
+                                  hipStream_t s) {
   const int KK = g.kh * g.kw;
   launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
   bool generic = false;
@@ -513,6 +533,10 @@ hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
   if (generic) {
     hipError_t e = hipMemsetAsync(gw_off, 0, (size_t)g.J * g.C * KK * sizeof(float), s);
     if (e != hipSuccess) return e;
+    if (gxT_in) {  // the generic kernel accumulates into NCHW ∂x
+      e = launch_nhwc_to_nchw(gxT_in, gx, g.B, g.C, g.HWi, s);
+      if (e != hipSuccess) return e;
+    }
     const long total = (long)g.B * g.J * g.HW;
     hipLaunchKernelGGL(offset_bwd_generic, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
                        g, x, w_off, goff, gx, gw_off);
@@ -547,7 +571,7 @@ hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
     {
       dim3 grid((unsigned)((Mi + 255) / 256), (g.C + kCB - 1) / kCB);
       DCN_KK_DISPATCH(KK, hipLaunchKernelGGL(offset_dgrad_valu<KKc>, grid, dim3(256), 0, s, g,
-                                             wt2, goff, gx));
+                                             wt2, goff, gx, gxT_in));
     }
   }
   return hipGetLastError();

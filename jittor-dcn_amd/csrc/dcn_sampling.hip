@@ -1006,6 +1006,7 @@ hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, co
   if (nb <= 0) return hipSuccess;
   hipError_t e;
   if (g_force_generic) {
+    if (!gx) return hipErrorInvalidValue;  // the generic kernels accumulate into NCHW gx
     e = hipMemsetAsync(gx + (size_t)b0 * g.C * g.HWi, 0, (size_t)nb * g.C * g.HWi * sizeof(float),
                        s);
     if (e != hipSuccess) return e;
@@ -1050,6 +1051,7 @@ hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, co
       hipLaunchKernelGGL(dx_gather_cl<1>, grid, dim3(256), 0, s, g, L, P.rec, P.start, P.list,
                          gcolT, gxT, b0);
   }
+  if (!gx) return hipGetLastError();  // caller finalises ∂x from gxT (offset-conv ∂x pass)
   return launch_nhwc_to_nchw(gxT + (size_t)b0 * g.HWi * g.C, gx + (size_t)b0 * g.C * g.HWi, nb,
                              g.C, g.HWi, s);
 }
@@ -1088,6 +1090,7 @@ hipError_t launch_col2im_bf16(const Geo& g, const float* xT, const float* off,
   const int tr_n = (g.H + kTR - 1) / kTR, tq_n = (g.W + 4 - 1) / 4;
   hipLaunchKernelGGL((col2im_tile<2, 4, bf16_t>), dim3(tr_n * tq_n, 1, nb), dim3(kC2iThreads), 0,
                      s, g, xT, P.brec, P.start, gcolT, gxT, goff, b0, tq_n);
+  if (!gx) return hipGetLastError();
   return launch_nhwc_to_nchw(gxT + (size_t)b0 * g.HWi * g.C, gx + (size_t)b0 * g.C * g.HWi, nb,
                              g.C, g.HWi, s);
 }
