@@ -174,6 +174,33 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+// D(16x16) += A(16x4)·B(4x16), exact f32 (k-ordered fmaf chain). Lane l holds A[l&15][l>>4],
+// B[l>>4][l&15] and D[4*(l>>4) + r][l&15] in register r.
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// Four 16x16x4 f32 MFMAs sharing the B operand, accumulators pinned in place ("+a": the
+// compiler's own MFMA code rotated loop-carried accumulators through AGPR copies). Wait
+// states (cdna_hip_programming.md §5.7 item 2): s_nop 1 for the just-written A/B VGPRs;
+// an accumulate chain D -> C needs none; mfma_drain() before anything else reads D.
+__device__ __forceinline__ void mfma16x4_acc(f32x4& c0, f32x4& c1, f32x4& c2, f32x4& c3, float a0,
+                                             float a1, float a2, float a3, float b) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_mfma_f32_16x16x4_f32 %0, %4, %8, %0\n\t"
+      "v_mfma_f32_16x16x4_f32 %1, %5, %8, %1\n\t"
+      "v_mfma_f32_16x16x4_f32 %2, %6, %8, %2\n\t"
+      "v_mfma_f32_16x16x4_f32 %3, %7, %8, %3"
+      : "+a"(c0), "+a"(c1), "+a"(c2), "+a"(c3)
+      : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(b));
+}
+// 12 wait states (8-pass XDL) between the last asm MFMA and any other access to its D.
+__device__ __forceinline__ void mfma_drain(f32x4& c0, f32x4& c1, f32x4& c2, f32x4& c3) {
+  asm volatile("s_nop 11" : "+a"(c0), "+a"(c1), "+a"(c2), "+a"(c3));
+}
+
 // Row of D[row][col] held in register r by lane half hi, for 32x32 MFMA tiles.
 __device__ __forceinline__ int drow(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
 

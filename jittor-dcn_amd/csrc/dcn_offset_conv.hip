@@ -35,15 +35,16 @@ __global__ __launch_bounds__(256) void woff_to_ctj(const float* __restrict__ w,
   const int c = r / KK, tap = r - c * KK;
   wt[i] = j < J ? w[((size_t)j * C + c) * KK + tap] : 0.f;
 }
-// wT2[(j*KK + tap)*Cp + c] = w_off[j][c][tap] (0 for c >= C)
+// wT2[(j*KK + tap)*Cp + c] = w_off[j][c][tap] for rows < J*KK (0 for c >= C and for the
+// padding rows up to `rows`)
 __global__ __launch_bounds__(256) void woff_to_jtc(const float* __restrict__ w,
                                                    float* __restrict__ wt, int J, int C, int Cp,
-                                                   int KK) {
+                                                   int KK, int rows) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= J * KK * Cp) return;
+  if (i >= rows * Cp) return;
   const int r = i / Cp, c = i - r * Cp;  // r = j*KK + tap
   const int j = r / KK, tap = r - j * KK;
-  wt[i] = c < C ? w[((size_t)j * C + c) * KK + tap] : 0.f;
+  wt[i] = (c < C && r < J * KK) ? w[((size_t)j * C + c) * KK + tap] : 0.f;
 }
 // goffT[(b*HW + p)*Jp + j] = goff[b][j][p] (0 for j >= J)
 __global__ __launch_bounds__(256) void goff_to_pj(const float* __restrict__ goff,
@@ -416,6 +417,350 @@ __global__ __launch_bounds__(256) void offset_dgrad_valu(Geo g, const float* __r
 }
 
 // ---------------------------------------------------------------------------
+// K7 on MFMA (stride 1). Both backward products contract against the same shifted
+// ∂offset operand G[p][tj] = ∂off[b][j][y+ph-i·dh][x+pw-k·dw] (0 outside the output),
+// indexed by INPUT pixel p = (y, x) and tj = j·KK + tap (tap = i·kw + k):
+//   ∂w_off[j][c][tap] = Σ_p xT[p][c] · G[p][tj]          M = c, N = tj, K = pixels
+//   ∂x[c][p]          = Σ_tj w_off[j][c][tap] · G[p][tj]  M = c, N = pixels, K = tj
+// With the channels on the MFMA rows, the J·KK = 162 (j, tap) columns pad only to 176
+// (92 % useful) instead of J = 18 -> 32. G is never materialised: a block stages the
+// ∂offset rows its pixels reach into LDS as S[sr][sc][j] (zero where the output has no
+// pixel), and G[p][tj] = S[base(p) + toff(tj)] with base(p) = ((y-y0)·SW + x)·J and
+// toff(tj) = ((kh-1-i)·dh·SW + (kw-1-k)·dw)·J + j. 16x16x4 f32 MFMA = exact f32 products
+// accumulated in k order (deterministic, no atomics).
+// ---------------------------------------------------------------------------
+struct MfmaStage {
+  int SW;      // staged columns: W + (kw-1)·dw
+  int rowsB;   // input rows per ∂W chunk
+  int cpi;     // ∂W chunks per image
+  int spi;     // ∂x pixel strips (64 px) per image
+  int SRx;     // staged rows bound for a ∂x strip
+  size_t lds_w, lds_x;  // dynamic LDS bytes
+};
+constexpr int kMfmaLds = 64 * 1024;
+constexpr int kDgPx = 64;  // ∂x pixels per block (4 waves = 4 x 64 channels)
+constexpr int kWgMfmaRows = 7;  // config 3: 56 rows = 8 chunks, 2048 blocks = 2 full rounds
+
+static int tj_pad4(const Geo& g) { return (g.J * g.kh * g.kw + 3) / 4 * 4; }
+
+// geometry the MFMA kernels take (stride 1, C % 4 == 0, C <= 256, J*KK <= 176, LDS fits)
+static bool mfma_stage(const Geo& g, MfmaStage* m) {
+  if (g.sh != 1 || g.sw != 1 || g.C % 4 != 0 || g.C > 256 || g.J * g.kh * g.kw > 176)
+    return false;
+  m->SW = g.W + (g.kw - 1) * g.dw;
+  const size_t row_bytes = (size_t)m->SW * g.J * sizeof(float);
+  const int halo = (g.kh - 1) * g.dh;
+  int rows = std::min(kWgMfmaRows, g.H);
+  while (rows > 0 && (size_t)(rows + halo) * row_bytes > kMfmaLds) --rows;
+  if (rows == 0) return false;
+  m->cpi = (g.H + rows - 1) / rows;
+  m->rowsB = (g.H + m->cpi - 1) / m->cpi;  // balanced chunks
+  m->lds_w = (size_t)(m->rowsB + halo) * row_bytes;
+  m->spi = (g.HWi + kDgPx - 1) / kDgPx;
+  m->SRx = (kDgPx - 1) / g.W + 2 + halo;
+  m->lds_x = (size_t)tj_pad4(g) * sizeof(int) + (size_t)m->SRx * row_bytes;
+  return m->lds_x <= kMfmaLds;
+}
+static size_t wgrad_mfma_part_floats(const Geo& g, const MfmaStage& m) {
+  return (size_t)g.B * m.cpi * g.C * g.J * g.kh * g.kw;
+}
+
+// S[(sr*SW + sc)*J + j] = ∂off[b][j][y0 + sr - (kh-1)·dh + ph][sc - (kw-1)·dw + pw]
+// kU loads per thread are in flight together (clamped in-bounds addresses, masked after),
+// so staging costs a few memory latencies per block, not one per element.
+__device__ __forceinline__ void stage_goff(const Geo& g, const float* __restrict__ goff, int b,
+                                           int y0, int SR, int SW, float* S) {
+  constexpr int kU = 8;
+  const int plane = SR * SW, n = plane * g.J;
+  // n <= 16384 (64 KiB of LDS) and plane <= 8192: umulhi by ceil(2^32/d) is the exact
+  // quotient there (checked for every d <= 8192, idx < 65536), instead of ~40-instruction
+  // integer divides per element
+  const unsigned mp = 0xffffffffu / (unsigned)plane + 1u, ms = 0xffffffffu / (unsigned)SW + 1u;
+  const float* gb = goff + (size_t)b * g.J * g.HW;
+  for (int i0 = threadIdx.x; i0 < n; i0 += blockDim.x * kU) {
+    float v[kU];
+    int dst[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {  // sc fastest: coalesced reads
+      const int idx = min(i0 + u * (int)blockDim.x, n - 1);
+      const int j = (int)__umulhi((unsigned)idx, mp), rem = idx - j * plane;
+      const int sr = (int)__umulhi((unsigned)rem, ms), sc = rem - sr * SW;
+      const int ho = y0 + sr - (g.kh - 1) * g.dh + g.ph, wo = sc - (g.kw - 1) * g.dw + g.pw;
+      const bool ok = ho >= 0 && ho < g.Ho && wo >= 0 && wo < g.Wo;
+      const int hc = min(max(ho, 0), g.Ho - 1), wc = min(max(wo, 0), g.Wo - 1);
+      v[u] = gb[(size_t)j * g.HW + hc * g.Wo + wc];
+      v[u] = ok ? v[u] : 0.f;
+      dst[u] = rem * g.J + j;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (i0 + u * (int)blockDim.x < n) S[dst[u]] = v[u];
+  }
+}
+
+__device__ __forceinline__ int g_toff(const Geo& g, int tj, int SW) {
+  const int KK = g.kh * g.kw;
+  if (tj >= g.J * KK) return 0;  // padding column: any finite staged value
+  const int j = tj / KK, t = tj - j * KK;
+  const int i = t / g.kw, k = t - i * g.kw;
+  return ((g.kh - 1 - i) * g.dh * SW + (g.kw - 1 - k) * g.dw) * g.J + j;
+}
+
+// ∂W_off partials: block = (chunk of rowsB input rows of one image, 64 channels); wave w
+// owns N-tiles w, w+4, w+8 (all 4 channel tiles), so no cross-wave reduction. Lane
+// (n = l&15, q = l>>4) loads channels c0+4n..+3 of pixel x0+q as one float4: element e
+// is row n of M-tile e (tile e = channels c0+4r+e). part[chunk][c][tj].
+template <int NTW, bool W4>
+__global__ __launch_bounds__(256) void offset_wgrad_mfma(Geo g, const float* __restrict__ xT,
+                                                        const float* __restrict__ goff,
+                                                        float* __restrict__ part, int rowsB,
+                                                        int cpi) {
+  extern __shared__ float S[];
+  const int chunk = blockIdx.x;
+  const int b = chunk / cpi, y0 = (chunk - b * cpi) * rowsB;
+  const int nrows = min(rowsB, g.H - y0);
+  const int SW = g.W + (g.kw - 1) * g.dw;
+  stage_goff(g, goff, b, y0, nrows + (g.kh - 1) * g.dh, SW, S);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n = lane & 15, q = lane >> 4;
+  const int TJ = g.J * g.kh * g.kw;
+  int toff[NTW];
+#pragma unroll
+  for (int u = 0; u < NTW; ++u) toff[u] = g_toff(g, 16 * (w + 4 * u) + n, SW);
+  const int cb = blockIdx.y * 64;
+  const bool cok = cb + 4 * n < g.C;
+  f32x4 acc[4][NTW];
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int u = 0; u < NTW; ++u) acc[e][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // The chunk's K-steps (4 pixels of one row each) run through a kPf-deep register ring of
+  // xT loads; buffer loads (clamped in-bounds offsets, masked after) keep the prefetch from
+  // being folded back into a load-then-wait per step. The step count is padded to a
+  // multiple of kPf with zero-operand steps, so the unrolled body has no early exit.
+  constexpr int kPf = 4;
+  const int nq = (g.W + 3) / 4, nsteps = nrows * nq;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(xT + ((size_t)b * g.H + y0) * g.W * g.C), 0,
+      (int)((size_t)max(nrows, 1) * g.W * g.C * sizeof(float)), 0x00020000);
+  const int cl = cok ? cb + 4 * n : 0;
+  float4 ring[kPf];
+  auto f4 = [](decltype(__builtin_amdgcn_raw_buffer_load_b128(rsrc, 0, 0, 0)) v) {
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+                       __uint_as_float(v[3]));
+  };
+  if (W4) {
+    // W % 4 == 0: step ks covers pixels 4ks..4ks+3 of the chunk, so the xT offset is
+    // linear in ks and a row change is wave-uniform: all per-step addressing is one
+    // scalar add (no per-lane divides, clamps or multiplies in the loop)
+    const unsigned lane_x = (unsigned)((q * g.C + cl) * 4);
+    const int step_x = 16 * g.C, last = (nsteps - 1) * step_x;
+    int lo = 0;  // scalar byte offset of the step being loaded
+#pragma unroll
+    for (int d = 0; d < kPf; ++d, lo += step_x)
+      ring[d] = f4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, lane_x, min(lo, last), 0));
+    int bv0[NTW];  // lane part of the B addresses
+#pragma unroll
+    for (int u = 0; u < NTW; ++u) bv0[u] = q * g.J + toff[u];
+    int sb = 0, sx = 0;  // S offset (floats) of the step being multiplied, its step in row
+    const int row_skip = (SW - g.W) * g.J;
+    for (int ks0 = 0; ks0 < nsteps; ks0 += kPf) {
+#pragma unroll
+      for (int d = 0; d < kPf; ++d) {
+        const unsigned keep = ks0 + d < nsteps ? 0xffffffffu : 0u;  // wave-uniform
+        const float ax = __uint_as_float(__float_as_uint(ring[d].x) & keep);
+        const float ay = __uint_as_float(__float_as_uint(ring[d].y) & keep);
+        const float az = __uint_as_float(__float_as_uint(ring[d].z) & keep);
+        const float aw = __uint_as_float(__float_as_uint(ring[d].w) & keep);
+        float bv[NTW];
+#pragma unroll
+        for (int u = 0; u < NTW; ++u) bv[u] = S[sb + bv0[u]];
+        sb += 4 * g.J;
+        if (++sx == nq) sx = 0, sb += row_skip;
+#pragma unroll
+        for (int u = 0; u < NTW; ++u)
+          mfma16x4_acc(acc[0][u], acc[1][u], acc[2][u], acc[3][u], ax, ay, az, aw, bv[u]);
+        ring[d] = f4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, lane_x, min(lo, last), 0));
+        lo += step_x;
+      }
+    }
+  } else {
+    // (row, column) of the step being loaded, kPf steps ahead of the one being multiplied
+    int ly = 0, lx = q;
+    auto load_next = [&]() {
+      const unsigned off =
+          (unsigned)(((min(ly, nrows - 1) * g.W + min(lx, g.W - 1)) * g.C + cl) * 4);
+      lx += 4;
+      if (lx >= nq * 4) lx = q, ++ly;
+      return f4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
+    };
+#pragma unroll
+    for (int d = 0; d < kPf; ++d) ring[d] = load_next();
+    int cy = 0, cx = q;  // the step being multiplied
+    for (int ks0 = 0; ks0 < nsteps; ks0 += kPf) {
+#pragma unroll
+      for (int d = 0; d < kPf; ++d) {
+        // bitwise mask: exact zeros (also for the padding steps past nsteps), no branch
+        const unsigned keep = (cok && cx < g.W && cy < nrows) ? 0xffffffffu : 0u;
+        const float ax = __uint_as_float(__float_as_uint(ring[d].x) & keep);
+        const float ay = __uint_as_float(__float_as_uint(ring[d].y) & keep);
+        const float az = __uint_as_float(__float_as_uint(ring[d].z) & keep);
+        const float aw = __uint_as_float(__float_as_uint(ring[d].w) & keep);
+        const float* sp = S + (min(cy, nrows - 1) * SW + min(cx, g.W - 1)) * g.J;
+        cx += 4;
+        if (cx >= nq * 4) cx = q, ++cy;
+        float bv[NTW];
+#pragma unroll
+        for (int u = 0; u < NTW; ++u) bv[u] = sp[toff[u]];
+#pragma unroll
+        for (int u = 0; u < NTW; ++u)
+          mfma16x4_acc(acc[0][u], acc[1][u], acc[2][u], acc[3][u], ax, ay, az, aw, bv[u]);
+        ring[d] = load_next();  // after the slot's last use: no register copy
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NTW; ++u) mfma_drain(acc[0][u], acc[1][u], acc[2][u], acc[3][u]);
+  float* pp = part + (size_t)chunk * g.C * TJ;
+#pragma unroll
+  for (int u = 0; u < NTW; ++u) {
+    const int tj = 16 * (w + 4 * u) + n;
+    if (tj >= TJ) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = cb + 4 * (4 * q + r) + e;
+        if (c < g.C) pp[(size_t)c * TJ + tj] = acc[e][u][r];
+      }
+  }
+}
+
+// ∂w_off[j][c][tap] = Σ_chunk part[chunk][c][j·KK + tap], chunks in order: 64 elements per
+// 1024-thread block, wave w sums chunks ≡ w (mod 16), the 16 wave sums fold in order.
+__global__ __launch_bounds__(1024) void wgrad_mfma_reduce(Geo g, const float* __restrict__ part,
+                                                         int nchunk, float* __restrict__ gw) {
+  const int KK = g.kh * g.kw, TJ = g.J * KK;
+  const long E = (long)g.C * TJ;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long i = (long)blockIdx.x * 64 + lane;
+  const long ic = i < E ? i : 0;
+  float s = 0.f;
+#pragma unroll 4
+  for (int ch = w; ch < nchunk; ch += 16) s += part[(size_t)ch * E + ic];
+  __shared__ float red[16][64];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w != 0 || i >= E) return;
+  s = red[0][lane];
+#pragma unroll
+  for (int k = 1; k < 16; ++k) s += red[k][lane];
+  const int c = (int)(i / TJ), tj = (int)(i - (long)c * TJ);
+  const int j = tj / KK, t = tj - j * KK;
+  gw[((size_t)j * g.C + c) * KK + t] = s;
+}
+
+// ∂x (+)= convᵀ: block = one 64-pixel strip of an image, wave w = channels 64w..64w+63
+// (4 M-tiles) x the strip's 4 pixel N-tiles; K = tj in steps of 4. A = w_off from wt2
+// (L2-resident, buffer loads two K-steps ahead), B = the staged ∂offset rows.
+// D lane map: pixel p0+16u+(l&15), channels c+16m+4(l>>4)+r: the ∂x row store is 16 lanes
+// x 4 B contiguous per channel, and the ∂xT add is one float4 per lane.
+__global__ __launch_bounds__(256) void offset_dgrad_mfma(Geo g, const float* __restrict__ wt2,
+                                                        int Cp, const float* __restrict__ goff,
+                                                        float* __restrict__ gx,
+                                                        const float* __restrict__ gxT_in,
+                                                        int spi) {
+  extern __shared__ float smem[];
+  const int TJp = (g.J * g.kh * g.kw + 3) / 4 * 4;
+  int* T = reinterpret_cast<int*>(smem);
+  float* S = smem + TJp;
+  const int b = blockIdx.x / spi, p0 = (blockIdx.x - b * spi) * kDgPx;
+  const int np = min(kDgPx, g.HWi - p0);
+  const int y0 = p0 / g.W, y1 = (p0 + np - 1) / g.W;
+  const int SW = g.W + (g.kw - 1) * g.dw;
+  stage_goff(g, goff, b, y0, y1 - y0 + 1 + (g.kh - 1) * g.dh, SW, S);
+  for (int t = threadIdx.x; t < TJp; t += blockDim.x) T[t] = g_toff(g, t, SW);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n = lane & 15, q = lane >> 4;
+  const int cw = 64 * w;
+  if (cw >= g.C) return;
+  int base[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int p = p0 + min(16 * u + n, np - 1);
+    const int y = p / g.W, x = p - y * g.W;
+    base[u] = ((y - y0) * SW + x) * g.J;
+  }
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[m][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int KS = TJp / 4;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wt2), 0,
+                                                      TJp * Cp * (int)sizeof(float), 0x00020000);
+  const unsigned lo = (unsigned)((q * Cp + cw + n) * 4);
+  // A[c = n (+16m)][k = tj = 4ks + q]; slot d of the ring holds K-step ks0 + d
+  auto lda = [&](int ks, float (&a)[4]) {
+    const int so = min(ks, KS - 1) * 4 * Cp * 4;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      a[m] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, lo + 64 * m, so, 0));
+  };
+  constexpr int kPf = 2;
+  float ra[kPf][4];
+#pragma unroll
+  for (int d = 0; d < kPf; ++d) lda(d, ra[d]);
+  for (int ks0 = 0; ks0 < KS; ks0 += kPf) {
+#pragma unroll
+    for (int d = 0; d < kPf; ++d) {
+      const int ks = ks0 + d;
+      // a padding step past KS multiplies zero weights (wt2 rows >= J*KK are zero, and
+      // the clamped load re-reads the last row: masked here)
+      const unsigned keep = ks < KS ? 0xffffffffu : 0u;
+      const int to = T[min(ks, KS - 1) * 4 + q];
+      float bv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) bv[u] = S[base[u] + to];
+      float a[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) a[m] = __uint_as_float(__float_as_uint(ra[d][m]) & keep);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        mfma16x4_acc(acc[0][u], acc[1][u], acc[2][u], acc[3][u], a[0], a[1], a[2], a[3], bv[u]);
+      lda(ks + kPf, ra[d]);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) mfma_drain(acc[0][u], acc[1][u], acc[2][u], acc[3][u]);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int pl = 16 * u + n;
+    if (pl >= np) continue;
+    const size_t p = (size_t)p0 + pl;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int c = cw + 16 * m + 4 * q;
+      if (c >= g.C) continue;  // C % 4 == 0: c..c+3 all in or all out
+      const f32x4 v = acc[m][u];
+      float* d = gx + ((size_t)b * g.C + c) * g.HWi + p;
+      if (gxT_in) {
+        const float4 t = *reinterpret_cast<const float4*>(gxT_in + ((size_t)b * g.HWi + p) * g.C + c);
+        d[0] = t.x + v[0];
+        d[g.HWi] = t.y + v[1];
+        d[2 * (size_t)g.HWi] = t.z + v[2];
+        d[3 * (size_t)g.HWi] = t.w + v[3];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) d[r * (size_t)g.HWi] += v[r];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Generic fallbacks (kernel sizes without an instantiation): plain per-thread loops.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void offset_conv_fwd_generic(Geo g, const float* __restrict__ x,
@@ -474,14 +819,18 @@ __global__ __launch_bounds__(256) void offset_bwd_generic(Geo g, const float* __
 
 size_t offset_conv_wt_floats(const Geo& g) {
   const size_t KK = (size_t)g.kh * g.kw;
-  return std::max((size_t)pad_j(g.J) * g.C * KK, (size_t)g.J * KK * pad_c(g.C));
+  return std::max((size_t)pad_j(g.J) * g.C * KK, (size_t)tj_pad4(g) * pad_c(g.C));
 }
 size_t offset_conv_fpart_floats(const Geo& g) { return (size_t)kSplit * g.B * g.J * g.HW; }
 
 // goffT rows, then offset_wgrad_valu's per-block partials.
+// (or, on the MFMA path, offset_wgrad_mfma's per-chunk partials)
 size_t offset_conv_goffT_floats(const Geo& g) {
   const WgradGrid w = wgrad_grid(g, 1);  // sized for the smallest row count per wave
-  return goffT_rows_floats(g) + (size_t)w.nbx * w.ny * w.nz * kJB * w.cper;
+  size_t n = goffT_rows_floats(g) + (size_t)w.nbx * w.ny * w.nz * kJB * w.cper;
+  MfmaStage ms;
+  if (mfma_stage(g, &ms)) n = std::max(n, wgrad_mfma_part_floats(g, ms));
+  return n;
 }
 
 hipError_t launch_offset_conv_fwd(const Geo& g, const float* x, const float* w_off,
@@ -530,6 +879,29 @@ hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
   launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
   bool generic = false;
   DCN_KK_DISPATCH(KK, (void)KKc);
+  MfmaStage ms;
+  if (!generic && mfma_stage(g, &ms) && !get_force_generic() && !exp_flag(6)) {
+    const int TJ = g.J * KK, NT = (TJ + 15) / 16;
+    dim3 grid(g.B * ms.cpi, (g.C + 63) / 64);
+    auto wg = [&](auto kern) {
+      hipLaunchKernelGGL(kern, grid, dim3(256), ms.lds_w, s, g, xT, goff, goffT, ms.rowsB,
+                         ms.cpi);
+    };
+    // W % 4 == 0 and C % 64 == 0: linear K-step addressing (see the kernel)
+    const bool w4 = g.W % 4 == 0 && g.C % 64 == 0;
+    if (NT <= 4) w4 ? wg(offset_wgrad_mfma<1, true>) : wg(offset_wgrad_mfma<1, false>);
+    else if (NT <= 8) w4 ? wg(offset_wgrad_mfma<2, true>) : wg(offset_wgrad_mfma<2, false>);
+    else w4 ? wg(offset_wgrad_mfma<3, true>) : wg(offset_wgrad_mfma<3, false>);
+    const long E = (long)g.C * TJ;
+    hipLaunchKernelGGL(wgrad_mfma_reduce, dim3((unsigned)((E + 63) / 64)), dim3(1024), 0, s, g,
+                       goffT, g.B * ms.cpi, gw_off);
+    const int rows = tj_pad4(g), Cp = pad_c(g.C);
+    hipLaunchKernelGGL(woff_to_jtc, dim3((rows * Cp + 255) / 256), dim3(256), 0, s, w_off, wt2,
+                       g.J, g.C, Cp, KK, rows);
+    hipLaunchKernelGGL(offset_dgrad_mfma, dim3(g.B * ms.spi), dim3(256), ms.lds_x, s, g, wt2, Cp,
+                       goff, gx, gxT_in, ms.spi);
+    return hipGetLastError();
+  }
   if (generic) {
     hipError_t e = hipMemsetAsync(gw_off, 0, (size_t)g.J * g.C * KK * sizeof(float), s);
     if (e != hipSuccess) return e;
@@ -566,7 +938,7 @@ hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
   {
     const int n = g.J * KK * pad_c(g.C);
     hipLaunchKernelGGL(woff_to_jtc, dim3((n + 255) / 256), dim3(256), 0, s, w_off, wt2, g.J, g.C,
-                       pad_c(g.C), KK);
+                       pad_c(g.C), KK, g.J * KK);
     const long Mi = (long)g.B * g.HWi;
     {
       dim3 grid((unsigned)((Mi + 255) / 256), (g.C + kCB - 1) / kCB);

@@ -230,6 +230,48 @@ def test_channels_last_kernels_match_generic_kernels(gpu_handle, C, H, W, s, off
     assert_close(col_w, O.im2col(x, off_w, 3, 3).transpose(0, 2, 1), what="im2col vs oracle")
 
 
+@pytest.mark.parametrize("B,C,H,W,k,s,p,dil", [
+    (2, 64, 20, 20, (3, 3), (1, 1), (1, 1), (1, 1)),   # MFMA kernels
+    (3, 100, 21, 19, (3, 3), (1, 1), (1, 1), (1, 1)),  # partial 64-channel group, W % 4 != 0
+    (2, 8, 9, 3, (3, 3), (1, 1), (2, 2), (2, 2)),      # dilation 2, rows narrower than a K-step
+    (2, 12, 7, 5, (3, 2), (1, 1), (1, 0), (1, 1)),     # rect kernel, Wo < W
+    (1, 16, 6, 200, (3, 3), (1, 1), (1, 1), (1, 1)),   # wide rows: 2-row ∂W chunks
+    (2, 68, 23, 25, (3, 3), (2, 2), (1, 1), (1, 1)),   # stride 2: VALU kernels only
+])
+def test_offset_conv_bwd_mfma_and_valu_vs_oracle(gpu_handle, B, C, H, W, k, s, p, dil):
+    """Offset-conv backward (∂W_off, ∂b_off, ∂x accumulated) on the MFMA kernels (stride 1)
+    and on the VALU kernels (dcn_debug_force_generic) against the oracle."""
+    h = gpu_handle
+    rng = np.random.default_rng(17)
+    N = k[0] * k[1]
+    x = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    wo = (rng.standard_normal((2 * N, C, *k)) / np.sqrt(C * N)).astype(np.float32)
+    desc = rt.make_desc(B, C, H, W, 4, k, s, p, dil)
+    Ho, Wo = rt.out_shape(desc)
+    goff = rng.standard_normal((B, 2 * N, Ho, Wo)).astype(np.float32)
+    gx0 = rng.standard_normal(x.shape).astype(np.float32)  # ∂x is accumulated into
+    ref_gw, ref_gb, ref_gx = O.offset_conv_backward(x, wo, goff, s, p, dil)
+    vp = ctypes.c_void_p
+    res = {}
+    for generic in (0, 1):
+        D = Dev(h)
+        try:
+            px, pwo, pgoff, pgx = D.up(x), D.up(wo), D.up(goff), D.up(gx0)
+            pgw, pgb = D.zeros(wo.nbytes), D.zeros(2 * N * 4)
+            rt.check(h.lib.dcn_debug_force_generic(generic))
+            rt.check(h.lib.dcn_offset_conv_bwd(h.h, desc, vp(px), vp(pwo), vp(pgoff), vp(pgx),
+                                               vp(pgw), vp(pgb)), "dcn_offset_conv_bwd")
+            res[generic] = (D.down(pgx, x.shape), D.down(pgw, wo.shape), D.down(pgb, (2 * N,)))
+        finally:
+            rt.check(h.lib.dcn_debug_force_generic(0))
+            D.free()
+    for generic, (gx, gw, gb) in res.items():
+        tag = f"{'valu' if generic else 'default'}"
+        assert_close(gx, gx0 + ref_gx, what=f"{tag} ∂x")
+        assert_close_reduction(gw, ref_gw, what=f"{tag} ∂w_off")
+        assert_close_reduction(gb, ref_gb, what=f"{tag} ∂b_off")
+
+
 def test_module_numpy_backend_on_gpu():
     d = load_golden("nonsquare_stride2")
     m = DeformConv2dNumpy(d["x"].shape[1], d["w"].shape[0], 3, 2, 1)

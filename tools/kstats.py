@@ -1,11 +1,23 @@
 #!/usr/bin/env python3
-"""Print a rocprofv3 kernel_stats.csv as a short table (avg µs per kernel)."""
+"""Print rocprofv3 kernel stats (µs) of one or more profile dirs, filtered by substring.
+Usage: kstats.py DIR [DIR ...] [--match=a,b]"""
 import csv
+import glob
 import sys
 
-rows = list(csv.DictReader(open(sys.argv[1])))
-tot = sum(float(r["TotalDurationNs"]) for r in rows)
-for r in rows[: int(sys.argv[2]) if len(sys.argv) > 2 else 20]:
-    n = r["Name"].split("(")[0].replace("void ", "")[:58]
-    print(f"{n:58s} calls={r['Calls']:>4} avg_us={float(r['AverageNs'])/1e3:9.1f} "
-          f"share={float(r['TotalDurationNs'])/tot*100:5.1f}%")
+dirs = [a for a in sys.argv[1:] if not a.startswith("--")]
+match = None
+for a in sys.argv[1:]:
+    if a.startswith("--match="):
+        match = a.split("=", 1)[1].split(",")
+for d in dirs:
+    f = glob.glob(d + "/**/*kernel_stats.csv", recursive=True)
+    if not f:
+        print(d, "(no stats)")
+        continue
+    print(d)
+    for r in csv.DictReader(open(f[0])):
+        n = r["Name"]
+        if match and not any(m in n for m in match):
+            continue
+        print(f"  {int(r['Calls']):4d} {float(r['AverageNs']) / 1e3:9.1f} us  {n[:90]}")
