@@ -175,57 +175,81 @@ hipError_t launch_bias_to_bf16(const Geo& g, const float* out32, const float* bi
 }
 
 // ---------------------------------------------------------------------------
-// ∂out -> ∂outT (channels-last, B operand of the flat ∂col GEMM) fused with ∂b: each
-// 64-pixel x 64-channel tile also writes its per-channel sum (fixed order), and
-// tile_sum_to_channels folds the B x ceil(HW/64) tile sums per channel in order.
+// ∂out -> ∂outT (channels-last, B operand of the flat ∂col GEMM) fused with ∂b, through
+// 64x65 LDS tiles. A block walks kXpSub consecutive 64-pixel tiles of one (image,
+// 64-channel) slab with the next tile's loads in flight while the current one is
+// written, and accumulates each channel's sum while writing; its 4 row-groups' sums fold
+// in order into one partial per (block, channel), and tile_sum_to_channels folds the
+// B x ceil(HW/(64*kXpSub)) partials per channel in order (deterministic, no atomics).
 // ---------------------------------------------------------------------------
+constexpr int kXpSub = 8;
+
 __global__ __launch_bounds__(256) void xpose_chsum(const float* __restrict__ in,
                                                    float* __restrict__ out,
                                                    float* __restrict__ tsum, int C, int P) {
   __shared__ float t[64][65];
-  const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64, b = blockIdx.z;
+  __shared__ float red[4][64];
+  const int c0 = blockIdx.y * 64, b = blockIdx.z;
   const float* ib = in + (size_t)b * C * P;
   float* ob = out + (size_t)b * C * P;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  for (int i = ty; i < 64; i += 4) {
-    const int c = c0 + i, p = p0 + tx;
-    t[i][tx] = (c < C && p < P) ? ib[(size_t)c * P + p] : 0.f;
-  }
-  __syncthreads();
-  for (int i = ty; i < 64; i += 4) {
-    const int p = p0 + i, c = c0 + tx;
-    if (c < C && p < P) ob[(size_t)p * C + c] = t[tx][i];
-  }
-  if (threadIdx.x < 64 && c0 + threadIdx.x < C) {
-    float s = 0.f;
-    for (int k = 0; k < 64; ++k) s += t[threadIdx.x][k];
-    tsum[((size_t)b * gridDim.x + blockIdx.x) * C + c0 + threadIdx.x] = s;
-  }
-}
-
-__global__ __launch_bounds__(256) void tile_sum_to_channels(const float* __restrict__ tsum,
-                                                            int ntiles, int C,
-                                                            float* __restrict__ out) {
-  __shared__ float red[256];
-  const int c = blockIdx.x, tid = threadIdx.x;
-  float s = 0.f;
-  for (int i = tid; i < ntiles; i += 256) s += tsum[(size_t)i * C + c];
-  red[tid] = s;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (tid < o) red[tid] += red[tid + o];
+  const int pb = blockIdx.x * 64 * kXpSub;
+  const int nsub = min(kXpSub, (P - pb + 63) / 64);
+  float r[16];
+  auto load = [&](int p0) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int c = c0 + ty + 4 * k, p = p0 + tx;
+      r[k] = (c < C && p < P) ? ib[(size_t)c * P + p] : 0.f;
+    }
+  };
+  load(pb);
+  float csum = 0.f;  // channel c0+tx over this thread's pixels (rows ty, ty+4, ... of a tile)
+  for (int sub = 0; sub < nsub; ++sub) {
+    const int p0 = pb + 64 * sub;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t[ty + 4 * k][tx] = r[k];
+    __syncthreads();
+    if (sub + 1 < nsub) load(p0 + 64);  // in flight while this tile is written
+    const int c = c0 + tx;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int i = ty + 4 * k, p = p0 + i;
+      const float v = t[tx][i];
+      csum += v;  // zero outside [0, P) x [0, C)
+      if (c < C && p < P) ob[(size_t)p * C + c] = v;
+    }
     __syncthreads();
   }
-  if (tid == 0) out[c] = red[0];
+  red[ty][tx] = csum;
+  __syncthreads();
+  if (ty == 0 && c0 + tx < C)
+    tsum[(size_t)(c0 + tx) * gridDim.x * gridDim.z + (size_t)b * gridDim.x + blockIdx.x] =
+        ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];  // [C][partials]
 }
 
-size_t xpose_chsum_floats(int B, int C, int P) { return (size_t)B * ((P + 63) / 64) * C; }
+// One wave per channel: lane l sums partials i ≡ l (mod 64) (all loads in flight
+// together), then a fixed DPP tree (wave_sum) folds the 64 lane sums: deterministic.
+__global__ __launch_bounds__(64) void tile_sum_to_channels(const float* __restrict__ tsum,
+                                                           int ntiles, int C,
+                                                           float* __restrict__ out) {
+  const int c = blockIdx.x, lane = threadIdx.x;
+  float s = 0.f;
+#pragma unroll 8
+  for (int i = lane; i < ntiles; i += 64) s += tsum[(size_t)c * ntiles + i];  // coalesced
+  s = wave_sum(s);
+  if (lane == 0) out[c] = s;
+}
+
+static int xpose_blocks_x(int P) { return (P + 64 * kXpSub - 1) / (64 * kXpSub); }
+
+size_t xpose_chsum_floats(int B, int C, int P) { return (size_t)B * xpose_blocks_x(P) * C; }
 
 hipError_t launch_xpose_chsum(const float* in, float* out, float* tsum, float* chsum, int B,
                               int C, int P, hipStream_t s) {
-  dim3 grid((P + 63) / 64, (C + 63) / 64, B);
+  dim3 grid(xpose_blocks_x(P), (C + 63) / 64, B);
   hipLaunchKernelGGL(xpose_chsum, grid, dim3(256), 0, s, in, out, tsum, C, P);
-  hipLaunchKernelGGL(tile_sum_to_channels, dim3(C), dim3(256), 0, s, tsum, B * ((P + 63) / 64), C,
+  hipLaunchKernelGGL(tile_sum_to_channels, dim3(C), dim3(64), 0, s, tsum, B * xpose_blocks_x(P), C,
                      chsum);
   return hipGetLastError();
 }
