@@ -171,6 +171,9 @@ struct dcn_handle {
   // sample bins beside the GEMMs); forked from / joined back into `stream` with events
   hipStream_t aux = nullptr;
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  // backward pipeline: chunk k's ∂offset is ready (main -> aux)
+  static constexpr int kChunkEvents = 8;
+  hipEvent_t chunk_ev[kChunkEvents] = {};
   dcn::GemmEngine* gemm = nullptr;
   // handle-owned workspace (host-pointer API) and scratch (standalone kernel API)
   void* ws = nullptr;
@@ -272,10 +275,16 @@ int core_forward(dcn_handle* h, const Geo& g, const float* x, const float* off, 
   return DCN_OK;
 }
 
+// The offset-conv backward, when core_backward runs it interleaved with col2im.
+struct OffsetBwd {
+  const float* w_off;
+  float *gw_off, *gb_off, *goffT, *wt2;
+};
+
 int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off, const float* w,
                   const float* gout, float* gx, float* gw, float* gb, bool has_bias, float* goff,
                   float* xT, float* colT, float* parts, float* gxT, float* goutT, void* bins,
-                  bool col_valid) {
+                  bool col_valid, const OffsetBwd* ob = nullptr, bool* ob_done = nullptr) {
   // the sample bins depend only on the offsets: build them on the side stream while the
   // main stream runs the ∂W / ∂col GEMMs
   DCN_TRY(fork_aux(h));
@@ -344,9 +353,40 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
       GEMM_TRY(h, sp, w, gout, colT);
     }
   }
+  DCN_TRY(join_aux(h));  // bins ready
+  if (ob && ob_done && dcn::col2im_chunkable(g) && dcn::offset_bwd_chunkable(g) && g.B >= 2 &&
+      dcn::exp_flag(3) >= 2) {
+    // Batch-chunk pipeline (A/B knob DCN_EXP slot 3 = chunk count, off by default): K5
+    // (col2im, HBM-latency bound) of chunk k+1 on the main stream beside K7 (offset-conv
+    // ∂W_off / ∂x on MFMA) of chunk k on the side stream, which waits for chunk k's
+    // ∂offset. Same kernels and per-image results as the serial order. r01 at config 3:
+    // serial 0.668 + 0.470 ms; 2 / 4 / 8 chunks 1.18 / 1.23 / 1.32 ms (the two contend for
+    // the CUs instead of overlapping).
+    // (profile scopes: "col2im" = the whole interleaved region, "offset_bwd" = the fold)
+    {
+      ProfScope ps(h, DCN_K_COL2IM);
+      static_assert(dcn_handle::kChunkEvents >= 8, "one event per chunk");
+      const int nc = std::min(g.B, std::min(dcn::exp_flag(3), 8));
+      const int cb = (g.B + nc - 1) / nc;
+      HIP_TRY(dcn::launch_offset_bwd_prep(g, ob->w_off, ob->wt2, h->aux));
+      for (int k = 0; k * cb < g.B; ++k) {
+        const int b0 = k * cb, nb = std::min(cb, g.B - b0);
+        HIP_TRY(dcn::launch_col2im_coord(g, x, xT, off, colT + (size_t)b0 * g.HW * g.K, nullptr,
+                                         gxT, goff, bins, b0, nb, true, h->stream, g.B));
+        HIP_TRY(hipEventRecord(h->chunk_ev[k], h->stream));
+        HIP_TRY(hipStreamWaitEvent(h->aux, h->chunk_ev[k], 0));
+        HIP_TRY(dcn::launch_offset_bwd_chunk(g, xT, goff, ob->goffT, ob->wt2, gx, gxT, b0, nb,
+                                             h->aux));
+      }
+      DCN_TRY(join_aux(h));
+    }
+    ProfScope ps2(h, DCN_K_OFFSET_BWD);
+    HIP_TRY(dcn::launch_offset_bwd_finish(g, goff, ob->goffT, ob->gw_off, ob->gb_off, h->stream));
+    *ob_done = true;
+    return DCN_OK;
+  }
   {
     // K5 overwrites grad_x (sampling route) and grad_off
-    DCN_TRY(join_aux(h));
     ProfScope ps(h, DCN_K_COL2IM);
     // ∂x stays channels-last in gxT; the offset-conv ∂x pass finalises it (one write)
     HIP_TRY(dcn::launch_col2im_coord(g, x, xT, off, colT, dcn::get_force_generic() ? gx : nullptr,
@@ -528,6 +568,8 @@ int dcn_create(int device, dcn_handle** out) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming);
+  for (auto& ce : h->chunk_ev)
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ce, hipEventDisableTiming);
   if (e != hipSuccess) {
     dcn_destroy(h);
     return fail(DCN_ERR_HIP, std::string("dcn_create: ") + hipGetErrorString(e));
@@ -554,6 +596,8 @@ int dcn_destroy(dcn_handle* h) {
   dcn::gemm_engine_destroy(h->gemm);
   if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
   if (h->join_ev) (void)hipEventDestroy(h->join_ev);
+  for (hipEvent_t ce : h->chunk_ev)
+    if (ce) (void)hipEventDestroy(ce);
   if (h->aux) (void)hipStreamDestroy(h->aux);
   if (h->own) (void)hipStreamDestroy(h->own);
   delete h;
@@ -759,9 +803,12 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
   }
   auto F = [&](size_t o) { return reinterpret_cast<float*>(base + o); };
   float* goff = grad_off_out ? grad_off_out : F(L.goff);
+  const OffsetBwd ob{w_off, grad_w_off, grad_b_off, F(L.goffT), F(L.wt)};
+  bool ob_done = false;
   DCN_TRY(core_backward(h, g, x, off, w, grad_out, grad_x, grad_w, grad_b, d->has_bias != 0, goff,
                         F(L.xT), F(L.col), F(L.parts), F(L.gxT), F(L.goutT), base + L.bins,
-                        (flags & DCN_BWD_COL_IN_WS) != 0));
+                        (flags & DCN_BWD_COL_IN_WS) != 0, &ob, &ob_done));
+  if (ob_done) return DCN_OK;
   ProfScope ps(h, DCN_K_OFFSET_BWD);
   HIP_TRY(dcn::launch_offset_conv_bwd(g, x, F(L.xT), w_off, goff, F(L.goffT), F(L.wt), grad_x,
                                       grad_w_off, grad_b_off,

@@ -39,7 +39,8 @@ hipError_t launch_im2col_bf16(const Geo& g, const float* xT, const float* off, b
                               int b0, int nb, hipStream_t s);
 hipError_t launch_col2im_bf16(const Geo& g, const float* xT, const float* off,
                               const bf16_t* gcolT, float* gx, float* gxT, float* goff,
-                              void* bins_ws, int b0, int nb, bool bins_ready, hipStream_t s);
+                              void* bins_ws, int b0, int nb, bool bins_ready, hipStream_t s,
+                              int bins_nb = 0);
 hipError_t launch_im2col(const Geo& g, const float* x, const float* xT, const float* off,
                          float* colT, int b0, int nb, hipStream_t s);
 size_t bins_ws_bytes(const Geo& g, int nb);
@@ -52,9 +53,14 @@ hipError_t launch_bins(const Geo& g, const float* off, void* bins_ws, float* gof
 // gx == NULL: leave ∂x (sampling route) channels-last in gxT only, for
 // launch_offset_conv_bwd to finalise (not with the generic kernels).
 // bins_ready: launch_bins already ran on bins_ws for these images.
+// bins_nb > 0 (with bins_ready): bins_ws holds the bins of images [0, bins_nb) and gcolT
+// points at image b0's ∂columns, so a batch may be processed in chunks (fused path only:
+// col2im_chunkable).
 hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, const float* off,
                                const float* gcolT, float* gx, float* gxT, float* goff,
-                               void* bins_ws, int b0, int nb, bool bins_ready, hipStream_t s);
+                               void* bins_ws, int b0, int nb, bool bins_ready, hipStream_t s,
+                               int bins_nb = 0);
+bool col2im_chunkable(const Geo& g);
 // dcn_offset_conv.hip:
 // wt / wt2: scratch of offset_conv_wt_floats(g) floats (transposed w_off copies).
 size_t offset_conv_wt_floats(const Geo& g);
@@ -71,6 +77,17 @@ hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
                                   const float* w_off, const float* goff, float* goffT, float* wt2,
                                   float* gx, float* gw_off, float* gb_off, const float* gxT_in,
                                   hipStream_t s);
+// The MFMA offset-conv backward (stride 1) in pieces, so that batch chunk k's ∂W_off / ∂x
+// can run on a side stream beside chunk k+1's col2im: prep (w_off transpose) once,
+// chunk(b0, nb) per image range (after that range's ∂offset exists), finish once (∂W_off
+// partial fold and ∂b_off). Same results as launch_offset_conv_bwd with gxT_in.
+bool offset_bwd_chunkable(const Geo& g);
+hipError_t launch_offset_bwd_prep(const Geo& g, const float* w_off, float* wt2, hipStream_t s);
+hipError_t launch_offset_bwd_chunk(const Geo& g, const float* xT, const float* goff,
+                                   float* goffT, const float* wt2, float* gx,
+                                   const float* gxT_in, int b0, int nb, hipStream_t s);
+hipError_t launch_offset_bwd_finish(const Geo& g, const float* goff, const float* goffT,
+                                    float* gw_off, float* gb_off, hipStream_t s);
 // dcn_reduce.hip conversions: bf16 <-> f32 (RNE), and the bf16 rounding of a f32 tensor
 // in place (out = bf16(v), v = f32(out)) so later f32 work sees exactly the bf16 value.
 hipError_t launch_bf16_to_f32(const bf16_t* in, float* out, size_t n, hipStream_t s);

@@ -514,9 +514,9 @@ template <int NTW, bool W4>
 __global__ __launch_bounds__(256) void offset_wgrad_mfma(Geo g, const float* __restrict__ xT,
                                                         const float* __restrict__ goff,
                                                         float* __restrict__ part, int rowsB,
-                                                        int cpi) {
+                                                        int cpi, int chunk0) {
   extern __shared__ float S[];
-  const int chunk = blockIdx.x;
+  const int chunk = chunk0 + blockIdx.x;
   const int b = chunk / cpi, y0 = (chunk - b * cpi) * rowsB;
   const int nrows = min(rowsB, g.H - y0);
   const int SW = g.W + (g.kw - 1) * g.dw;
@@ -672,12 +672,13 @@ __global__ __launch_bounds__(256, 4) void offset_dgrad_mfma(Geo g, const float* 
                                                         int Cp, const float* __restrict__ goff,
                                                         float* __restrict__ gx,
                                                         const float* __restrict__ gxT_in,
-                                                        int spi) {
+                                                        int spi, int blk0) {
   extern __shared__ float smem[];
   const int TJp = (g.J * g.kh * g.kw + 3) / 4 * 4;
   int* T = reinterpret_cast<int*>(smem);
   float* S = smem + TJp;
-  const int b = blockIdx.x / spi, p0 = (blockIdx.x - b * spi) * kDgPx;
+  const int bid = blk0 + blockIdx.x;
+  const int b = bid / spi, p0 = (bid - b * spi) * kDgPx;
   const int np = min(kDgPx, g.HWi - p0);
   const int y0 = p0 / g.W, y1 = (p0 + np - 1) / g.W;
   const int SW = g.W + (g.kw - 1) * g.dw;
@@ -871,6 +872,54 @@ hipError_t launch_offset_conv_fwd(const Geo& g, const float* x, const float* w_o
   return hipGetLastError();
 }
 
+bool offset_bwd_chunkable(const Geo& g) {
+  MfmaStage ms;
+  const int KK = g.kh * g.kw;
+  return (KK == 1 || KK == 4 || KK == 6 || KK == 9) && mfma_stage(g, &ms) &&
+         !get_force_generic() && !exp_flag(6);
+}
+
+hipError_t launch_offset_bwd_prep(const Geo& g, const float* w_off, float* wt2, hipStream_t s) {
+  const int rows = tj_pad4(g), Cp = pad_c(g.C);
+  hipLaunchKernelGGL(woff_to_jtc, dim3((rows * Cp + 255) / 256), dim3(256), 0, s, w_off, wt2, g.J,
+                     g.C, Cp, g.kh * g.kw, rows);
+  return hipGetLastError();
+}
+
+// images [b0, b0+nb): their ∂W_off chunk partials (goffT region) and their ∂x
+hipError_t launch_offset_bwd_chunk(const Geo& g, const float* xT, const float* goff,
+                                   float* goffT, const float* wt2, float* gx,
+                                   const float* gxT_in, int b0, int nb, hipStream_t s) {
+  MfmaStage ms;
+  if (!mfma_stage(g, &ms)) return hipErrorInvalidValue;
+  if (nb <= 0) return hipSuccess;
+  const int TJ = g.J * g.kh * g.kw, NT = (TJ + 15) / 16;
+  dim3 grid(nb * ms.cpi, (g.C + 63) / 64);
+  auto wg = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(256), ms.lds_w, s, g, xT, goff, goffT, ms.rowsB, ms.cpi,
+                       b0 * ms.cpi);
+  };
+  // W % 4 == 0 and C % 64 == 0: linear K-step addressing (see the kernel)
+  const bool w4 = g.W % 4 == 0 && g.C % 64 == 0;
+  if (NT <= 4) w4 ? wg(offset_wgrad_mfma<1, true>) : wg(offset_wgrad_mfma<1, false>);
+  else if (NT <= 8) w4 ? wg(offset_wgrad_mfma<2, true>) : wg(offset_wgrad_mfma<2, false>);
+  else w4 ? wg(offset_wgrad_mfma<3, true>) : wg(offset_wgrad_mfma<3, false>);
+  hipLaunchKernelGGL(offset_dgrad_mfma, dim3(nb * ms.spi), dim3(256), ms.lds_x, s, g, wt2,
+                     pad_c(g.C), goff, gx, gxT_in, ms.spi, b0 * ms.spi);
+  return hipGetLastError();
+}
+
+hipError_t launch_offset_bwd_finish(const Geo& g, const float* goff, const float* goffT,
+                                    float* gw_off, float* gb_off, hipStream_t s) {
+  MfmaStage ms;
+  if (!mfma_stage(g, &ms)) return hipErrorInvalidValue;
+  const long E = (long)g.C * g.J * g.kh * g.kw;
+  hipLaunchKernelGGL(wgrad_mfma_reduce, dim3((unsigned)((E + 63) / 64)), dim3(1024), 0, s, g,
+                     goffT, g.B * ms.cpi, gw_off);
+  launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
+  return hipGetLastError();
+}
+
 // xT: channels-last x; goffT, wt2: scratch ([B][HW][J], [J][KK][C]). grad_x is accumulated,
 // or (gxT_in) overwritten with transpose(gxT_in) + the offset-conv route.
 hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
@@ -878,32 +927,15 @@ hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
                                   float* gx, float* gw_off, float* gb_off, const float* gxT_in,
                                   hipStream_t s) {
   const int KK = g.kh * g.kw;
-  launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
   bool generic = false;
   DCN_KK_DISPATCH(KK, (void)KKc);
-  MfmaStage ms;
-  if (!generic && mfma_stage(g, &ms) && !get_force_generic() && !exp_flag(6)) {
-    const int TJ = g.J * KK, NT = (TJ + 15) / 16;
-    dim3 grid(g.B * ms.cpi, (g.C + 63) / 64);
-    auto wg = [&](auto kern) {
-      hipLaunchKernelGGL(kern, grid, dim3(256), ms.lds_w, s, g, xT, goff, goffT, ms.rowsB,
-                         ms.cpi);
-    };
-    // W % 4 == 0 and C % 64 == 0: linear K-step addressing (see the kernel)
-    const bool w4 = g.W % 4 == 0 && g.C % 64 == 0;
-    if (NT <= 4) w4 ? wg(offset_wgrad_mfma<1, true>) : wg(offset_wgrad_mfma<1, false>);
-    else if (NT <= 8) w4 ? wg(offset_wgrad_mfma<2, true>) : wg(offset_wgrad_mfma<2, false>);
-    else w4 ? wg(offset_wgrad_mfma<3, true>) : wg(offset_wgrad_mfma<3, false>);
-    const long E = (long)g.C * TJ;
-    hipLaunchKernelGGL(wgrad_mfma_reduce, dim3((unsigned)((E + 63) / 64)), dim3(1024), 0, s, g,
-                       goffT, g.B * ms.cpi, gw_off);
-    const int rows = tj_pad4(g), Cp = pad_c(g.C);
-    hipLaunchKernelGGL(woff_to_jtc, dim3((rows * Cp + 255) / 256), dim3(256), 0, s, w_off, wt2,
-                       g.J, g.C, Cp, KK, rows);
-    hipLaunchKernelGGL(offset_dgrad_mfma, dim3(g.B * ms.spi), dim3(256), ms.lds_x, s, g, wt2, Cp,
-                       goff, gx, gxT_in, ms.spi);
-    return hipGetLastError();
+  if (!generic && offset_bwd_chunkable(g)) {
+    hipError_t e = launch_offset_bwd_prep(g, w_off, wt2, s);
+    if (e == hipSuccess) e = launch_offset_bwd_chunk(g, xT, goff, goffT, wt2, gx, gxT_in, 0, g.B, s);
+    if (e == hipSuccess) e = launch_offset_bwd_finish(g, goff, goffT, gw_off, gb_off, s);
+    return e;
   }
+  launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
   if (generic) {
     hipError_t e = hipMemsetAsync(gw_off, 0, (size_t)g.J * g.C * KK * sizeof(float), s);
     if (e != hipSuccess) return e;

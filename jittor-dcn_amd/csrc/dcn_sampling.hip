@@ -1000,10 +1000,24 @@ hipError_t launch_bins(const Geo& g, const float* off, void* bins_ws, float* gof
   return hipGetLastError();
 }
 
+bool col2im_chunkable(const Geo& g) { return !g_force_generic && k5_fused(g); }
+
+// bins of images [0, bins_nb) in bins_ws; the view of images [b0, ...)
+static BinsWs bins_view(const Geo& g, void* bins_ws, int b0, int nb, int bins_nb) {
+  if (bins_nb <= 0) return bins_ptrs(g, bins_ws, nb);
+  BinsWs P = bins_ptrs(g, bins_ws, bins_nb);
+  const size_t NB = (size_t)(g.H + 1) * (g.W + 1), NS = (size_t)g.HW * g.N;
+  P.start += (size_t)b0 * g.G * (NB + 1);
+  P.brec += (size_t)b0 * g.G * NS;
+  return P;
+}
+
 hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, const float* off,
                                const float* gcolT, float* gx, float* gxT, float* goff,
-                               void* bins_ws, int b0, int nb, bool bins_ready, hipStream_t s) {
+                               void* bins_ws, int b0, int nb, bool bins_ready, hipStream_t s,
+                               int bins_nb) {
   if (nb <= 0) return hipSuccess;
+  if (bins_nb > 0 && (!bins_ready || !col2im_chunkable(g))) return hipErrorInvalidValue;
   hipError_t e;
   if (g_force_generic) {
     if (!gx) return hipErrorInvalidValue;  // the generic kernels accumulate into NCHW gx
@@ -1030,7 +1044,7 @@ hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, co
     e = launch_bins(g, off, bins_ws, goff, b0, nb, s);
     if (e != hipSuccess) return e;
   }
-  const BinsWs P = bins_ptrs(g, bins_ws, nb);
+  const BinsWs P = bins_view(g, bins_ws, b0, nb, bins_nb);
   if (fused) {  // one pass over ∂colT: ∂xT tiles + ∂offset of the owned bins
     const int tr_n = (g.H + kTR - 1) / kTR;
     auto go = [&](auto kern, int tq) {
@@ -1080,13 +1094,15 @@ hipError_t launch_im2col_bf16(const Geo& g, const float* xT, const float* off, b
 
 hipError_t launch_col2im_bf16(const Geo& g, const float* xT, const float* off,
                               const bf16_t* gcolT, float* gx, float* gxT, float* goff,
-                              void* bins_ws, int b0, int nb, bool bins_ready, hipStream_t s) {
+                              void* bins_ws, int b0, int nb, bool bins_ready, hipStream_t s,
+                              int bins_nb) {
   if (nb <= 0) return hipSuccess;
+  if (bins_nb > 0 && !bins_ready) return hipErrorInvalidValue;
   if (!bins_ready) {
     const hipError_t e = launch_bins(g, off, bins_ws, goff, b0, nb, s);
     if (e != hipSuccess) return e;
   }
-  const BinsWs P = bins_ptrs(g, bins_ws, nb);
+  const BinsWs P = bins_view(g, bins_ws, b0, nb, bins_nb);
   const int tr_n = (g.H + kTR - 1) / kTR, tq_n = (g.W + 4 - 1) / 4;
   hipLaunchKernelGGL((col2im_tile<2, 4, bf16_t>), dim3(tr_n * tq_n, 1, nb), dim3(kC2iThreads), 0,
                      s, g, xT, P.brec, P.start, gcolT, gxT, goff, b0, tq_n);
