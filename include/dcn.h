@@ -154,6 +154,46 @@ int dcn_backward_host(dcn_handle* h, const dcn_desc* d, const float* x,
                       float* grad_b, float* grad_w_off, float* grad_b_off,
                       float* grad_off_out);
 
+/* ---- deformable RoI pooling -------------------------------- *
+ * DeformRoIPool (deform_conv.py:85-159) and DeformPSRoIPool (:162-241), fp32.
+ * rois[R][5] = (batch index, x1, y1, x2, y2) in input coordinates (scaled by
+ * spatial_scale, :96/:181); offsets[R][P][2] (x, y) per bin, P = ph*pw (for the PS
+ * pool the reference's offsets[R][2P] with x at 2p, y at 2p+1 is the same memory).
+ * Each bin is ONE bilinear sample at its centre + offset, with the reference's corner
+ * clamping (corners clamped to the image, weights from the clamped top-left corner,
+ * :121-135 / :214-228). The reference then sums the weighted corner features over the
+ * bins (`.sum(dim=2)`, :143-157 / :239) before reshaping to [R, C, ph, pw], so its
+ * module only runs for ph*pw == 1: out here is that sum, [R][C] (DeformRoIPool) or
+ * [R][C / P] (DeformPSRoIPool, channel c*P + p for bin p); the shim reshapes (and
+ * fails like the reference for P != 1). */
+typedef struct {
+  int B, C, H, W;          /* features [B][C][H][W] */
+  int R;                   /* number of RoIs */
+  int ph, pw;              /* output_size (:87, :165) */
+  int part_h, part_w;      /* part_size (PS only, :171; = output size when unset) */
+  float spatial_scale;     /* :86 */
+  float trans_std;         /* PS only (:172) */
+  int ps;                  /* 0 = DeformRoIPool, 1 = DeformPSRoIPool */
+  int no_trans;            /* PS only (:169): ignore the offsets */
+} dcn_roi_desc;
+/* out[R][C or C/P] (overwritten). */
+int dcn_roi_pool_fwd(dcn_handle* h, const dcn_roi_desc* d, const float* features,
+                     const float* rois, const float* offsets, float* out);
+/* Autodiff of the forward: grad_features [B][C][H][W] and grad_offsets [R][P][2]
+ * overwritten (grad_offsets may be NULL; zero for no_trans). The RoI boxes get no
+ * gradient (the reference's rois come from the data). grad_features accumulates with
+ * atomics (RoIs may share pixels), so its low bits depend on the summation order. */
+int dcn_roi_pool_bwd(dcn_handle* h, const dcn_roi_desc* d, const float* features,
+                     const float* rois, const float* offsets, const float* grad_out,
+                     float* grad_features, float* grad_offsets);
+/* Host-pointer variants (synchronous). Batch indices outside [0, B) are rejected
+ * (DCN_ERR_INVALID), where the reference would raise an index error. */
+int dcn_roi_pool_fwd_host(dcn_handle* h, const dcn_roi_desc* d, const float* features,
+                          const float* rois, const float* offsets, float* out);
+int dcn_roi_pool_bwd_host(dcn_handle* h, const dcn_roi_desc* d, const float* features,
+                          const float* rois, const float* offsets, const float* grad_out,
+                          float* grad_features, float* grad_offsets);
+
 /* ---- in-library kernel timing (HIP events on the handle's stream) ---------- */
 typedef enum {
   DCN_K_OFFSET_FWD = 0,

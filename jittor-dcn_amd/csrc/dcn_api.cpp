@@ -927,6 +927,111 @@ int dcn_backward_host(dcn_handle* h, const dcn_desc* d, const float* x, const fl
 }
 
 // ---- profiling ------------------------------------------------------------------
+// ---- deformable RoI pooling ------------------------------------------------------
+namespace {
+int make_roi_geo(const dcn_roi_desc* d, dcn::RoiGeo* q) {
+  if (!d || !q) return fail(DCN_ERR_INVALID, "null RoI descriptor");
+  q->B = d->B, q->C = d->C, q->H = d->H, q->W = d->W, q->R = d->R;
+  q->ph = d->ph, q->pw = d->pw;
+  q->part_h = d->part_h > 0 ? d->part_h : d->ph;  // part_size defaults to output_size (:171)
+  q->part_w = d->part_w > 0 ? d->part_w : d->pw;
+  q->P = d->ph * d->pw;
+  q->ps = d->ps != 0, q->no_trans = d->no_trans != 0;
+  q->scale = d->spatial_scale, q->trans_std = d->trans_std;
+  if (d->ph <= 0 || d->pw <= 0) return fail(DCN_ERR_INVALID, "output_size must be positive");
+  q->Cout = q->ps ? d->C / q->P : d->C;  // C_out = C // (ph*pw) (:177)
+  if (!dcn::roi_geo_ok(*q))
+    return fail(DCN_ERR_INVALID, "bad RoI pool shape (empty tensor, C // (ph*pw) == 0, or > 256 bins)");
+  return DCN_OK;
+}
+int check_roi_batch(const dcn::RoiGeo& q, const float* rois) {
+  for (int r = 0; r < q.R; ++r) {
+    const int b = (int)rois[(size_t)r * 5];
+    if (b < 0 || b >= q.B)
+      return fail(DCN_ERR_INVALID, "rois[" + std::to_string(r) + ", 0] = " + std::to_string(b) +
+                                       " is not a batch index in [0, " + std::to_string(q.B) + ")");
+  }
+  return DCN_OK;
+}
+}  // namespace
+
+int dcn_roi_pool_fwd(dcn_handle* h, const dcn_roi_desc* d, const float* features,
+                     const float* rois, const float* offsets, float* out) {
+  dcn::RoiGeo q;
+  DCN_TRY(make_roi_geo(d, &q));
+  DCN_TRY(set_device(h));
+  if (!q.no_trans && !offsets && q.R > 0) return fail(DCN_ERR_INVALID, "offsets is NULL");
+  HIP_TRY(dcn::launch_roi_pool_fwd(q, features, rois, offsets, out, h->stream));
+  return DCN_OK;
+}
+
+int dcn_roi_pool_bwd(dcn_handle* h, const dcn_roi_desc* d, const float* features,
+                     const float* rois, const float* offsets, const float* grad_out,
+                     float* grad_features, float* grad_offsets) {
+  dcn::RoiGeo q;
+  DCN_TRY(make_roi_geo(d, &q));
+  DCN_TRY(set_device(h));
+  if (!q.no_trans && !offsets && q.R > 0) return fail(DCN_ERR_INVALID, "offsets is NULL");
+  HIP_TRY(dcn::launch_roi_pool_bwd(q, features, rois, offsets, grad_out, grad_features,
+                                   grad_offsets, h->stream));
+  return DCN_OK;
+}
+
+int dcn_roi_pool_fwd_host(dcn_handle* h, const dcn_roi_desc* d, const float* features,
+                          const float* rois, const float* offsets, float* out) {
+  dcn::RoiGeo q;
+  DCN_TRY(make_roi_geo(d, &q));
+  DCN_TRY(set_device(h));
+  DCN_TRY(check_roi_batch(q, rois));
+  const size_t nf = (size_t)q.B * q.C * q.H * q.W, nr = (size_t)q.R * 5, no = (size_t)q.R * q.P * 2;
+  const size_t nout = (size_t)q.R * q.Cout;
+  DevBufs db;
+  float *df, *dr, *doffs = nullptr, *dout;
+  DCN_TRY(db.alloc(nf * 4, &df));
+  DCN_TRY(db.alloc(nr * 4, &dr));
+  DCN_TRY(db.alloc(nout * 4, &dout));
+  DCN_TRY(h2d(h, df, features, nf * 4));
+  DCN_TRY(h2d(h, dr, rois, nr * 4));
+  if (offsets) {
+    DCN_TRY(db.alloc(no * 4, &doffs));
+    DCN_TRY(h2d(h, doffs, offsets, no * 4));
+  }
+  DCN_TRY(dcn_roi_pool_fwd(h, d, df, dr, doffs, dout));
+  DCN_TRY(d2h(h, out, dout, nout * 4));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return DCN_OK;
+}
+
+int dcn_roi_pool_bwd_host(dcn_handle* h, const dcn_roi_desc* d, const float* features,
+                          const float* rois, const float* offsets, const float* grad_out,
+                          float* grad_features, float* grad_offsets) {
+  dcn::RoiGeo q;
+  DCN_TRY(make_roi_geo(d, &q));
+  DCN_TRY(set_device(h));
+  DCN_TRY(check_roi_batch(q, rois));
+  const size_t nf = (size_t)q.B * q.C * q.H * q.W, nr = (size_t)q.R * 5, no = (size_t)q.R * q.P * 2;
+  const size_t nout = (size_t)q.R * q.Cout;
+  DevBufs db;
+  float *df, *dr, *doffs = nullptr, *dgo, *dgf, *dgoffs = nullptr;
+  DCN_TRY(db.alloc(nf * 4, &df));
+  DCN_TRY(db.alloc(nr * 4, &dr));
+  DCN_TRY(db.alloc(nout * 4, &dgo));
+  DCN_TRY(db.alloc(nf * 4, &dgf));
+  DCN_TRY(h2d(h, df, features, nf * 4));
+  DCN_TRY(h2d(h, dr, rois, nr * 4));
+  DCN_TRY(h2d(h, dgo, grad_out, nout * 4));
+  if (offsets) {
+    DCN_TRY(db.alloc(no * 4, &doffs));
+    DCN_TRY(h2d(h, doffs, offsets, no * 4));
+  }
+  if (grad_offsets) DCN_TRY(db.alloc(no * 4, &dgoffs));
+  DCN_TRY(dcn_roi_pool_bwd(h, d, df, dr, doffs, dgo, dgf, dgoffs));
+  DCN_TRY(d2h(h, grad_features, dgf, nf * 4));
+  if (grad_offsets) DCN_TRY(d2h(h, grad_offsets, dgoffs, no * 4));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return DCN_OK;
+}
+
 int dcn_prof_enable(dcn_handle* h, int capacity) {
   DCN_TRY(set_device(h));
   if (capacity < 0) return fail(DCN_ERR_INVALID, "negative capacity");

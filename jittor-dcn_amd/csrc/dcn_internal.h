@@ -108,7 +108,24 @@ hipError_t launch_bias_grad(const Geo& g, const float* gout, float* gb, hipStrea
 hipError_t launch_sum_partials(const float* parts, int nparts, size_t n, float* dst,
                                hipStream_t s);
 
-// dcn_gemm.cpp: C = op(A)·op(B) (column-major, alpha 1, beta 0), strided batched.
+// dcn_roi_pool.hip: deformable RoI pooling (deform_conv.py:85-241), see include/dcn.h.
+struct RoiGeo {
+  int B, C, H, W, R;
+  int ph, pw, part_h, part_w;
+  int P;     // ph*pw bins
+  int Cout;  // C (DeformRoIPool) or C / P (DeformPSRoIPool)
+  int ps, no_trans;
+  float scale, trans_std;
+};
+bool roi_geo_ok(const RoiGeo& q);
+hipError_t launch_roi_pool_fwd(const RoiGeo& q, const float* f, const float* rois,
+                               const float* offsets, float* out, hipStream_t s);
+// overwrites gf (memset + atomics) and goffs (may be null)
+hipError_t launch_roi_pool_bwd(const RoiGeo& q, const float* f, const float* rois,
+                               const float* offsets, const float* gout, float* gf, float* goffs,
+                               hipStream_t s);
+
+// dcn_gemm.cpp: C = op(A)·op(B)// dcn_gemm.cpp: C = op(A)·op(B) (column-major, alpha 1, beta 0), strided batched.
 struct GemmSpec {
   bool ta = false, tb = false;
   int m = 0, n = 0, k = 0, lda = 0, ldb = 0, ldc = 0;

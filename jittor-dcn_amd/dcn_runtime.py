@@ -29,6 +29,14 @@ class Desc(ctypes.Structure):
                  "deform_groups", "dtype", "has_bias")]
 
 
+class RoiDesc(ctypes.Structure):
+    """dcn_roi_desc (include/dcn.h): DeformRoIPool / DeformPSRoIPool geometry."""
+    _fields_ = [(n, ctypes.c_int) for n in ("B", "C", "H", "W", "R", "ph", "pw", "part_h",
+                                            "part_w")] + \
+               [("spatial_scale", ctypes.c_float), ("trans_std", ctypes.c_float),
+                ("ps", ctypes.c_int), ("no_trans", ctypes.c_int)]
+
+
 _vp = ctypes.c_void_p
 _ip = ctypes.POINTER(ctypes.c_int)
 _dp = ctypes.POINTER(Desc)
@@ -69,6 +77,10 @@ SIGNATURES = {
     "dcn_comm_destroy": [_vp],
     "dcn_allreduce_grads": [_vp, _vp, _vp, _sz],
     "dcn_debug_force_generic": [ctypes.c_int],
+    "dcn_roi_pool_fwd": [_vp, ctypes.POINTER(RoiDesc), _vp, _vp, _vp, _vp],
+    "dcn_roi_pool_bwd": [_vp, ctypes.POINTER(RoiDesc), _vp, _vp, _vp, _vp, _vp, _vp],
+    "dcn_roi_pool_fwd_host": [_vp, ctypes.POINTER(RoiDesc), _vp, _vp, _vp, _vp],
+    "dcn_roi_pool_bwd_host": [_vp, ctypes.POINTER(RoiDesc), _vp, _vp, _vp, _vp, _vp, _vp],
 }
 _RESTYPES = {"dcn_last_error": ctypes.c_char_p}
 
@@ -113,6 +125,15 @@ def make_desc(B, C, H, W, O, kernel_size, stride, padding, dilation=(1, 1), defo
               bias=True, dtype=DCN_F32) -> Desc:
     return Desc(B, C, H, W, O, kernel_size[0], kernel_size[1], stride[0], stride[1], padding[0],
                 padding[1], dilation[0], dilation[1], deform_groups, dtype, int(bool(bias)))
+
+
+def make_roi_desc(feature_shape, num_rois, output_size, spatial_scale=1.0, ps=False,
+                  part_size=None, trans_std=0.1, no_trans=False) -> RoiDesc:
+    B, C, H, W = feature_shape
+    ph, pw = output_size
+    part_h, part_w = part_size if part_size else (0, 0)
+    return RoiDesc(B, C, H, W, num_rois, ph, pw, part_h, part_w, float(spatial_scale),
+                   float(trans_std), int(bool(ps)), int(bool(no_trans)))
 
 
 def out_shape(desc: Desc):

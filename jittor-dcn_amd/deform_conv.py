@@ -28,6 +28,7 @@ Backends:
 """
 from __future__ import annotations
 
+import ctypes
 import math
 
 import numpy as np
@@ -88,6 +89,61 @@ def dcn_backward_numpy(x, off, w_off, w, has_bias, grad_out, stride, padding, ha
     if has_bias:
         g["bias"] = gb
     return g
+
+
+def _roi_args(features, rois, offsets, output_size, ps, no_trans):
+    features, rois = _f32(features), _f32(rois)
+    R = rois.shape[0]
+    P = output_size[0] * output_size[1]
+    if rois.ndim != 2 or rois.shape[1] != 5:
+        raise ValueError(f"rois must be [R, 5], got {rois.shape}")
+    if ps and no_trans:
+        offsets = None
+    elif ps:  # offsets[:, part_idx*2 (+1)] (deform_conv.py:198-199): the first 2P columns
+        offsets = _f32(np.asarray(offsets, np.float32).reshape(R, -1)[:, :2 * P])
+    else:  # offsets[:, p, 0/1] (deform_conv.py:113-114)
+        offsets = _f32(np.asarray(offsets, np.float32).reshape(R, -1, 2)[:, :P])
+    return features, rois, offsets
+
+
+def roi_pool_forward_numpy(features, rois, offsets, output_size, spatial_scale=1.0, ps=False,
+                           part_size=None, trans_std=0.1, no_trans=False, handle=None):
+    """The reference's value before its final reshape: the bilinear corner sums over all
+    bins, [R, C] (DeformRoIPool, deform_conv.py:92-157) or [R, C // (ph*pw)]
+    (DeformPSRoIPool, :174-239). One libdcn call."""
+    h = handle or rt.default_handle()
+    features, rois, offsets = _roi_args(features, rois, offsets, output_size, ps, no_trans)
+    d = rt.make_roi_desc(features.shape, rois.shape[0], output_size, spatial_scale, ps, part_size,
+                         trans_std, no_trans)
+    P = output_size[0] * output_size[1]
+    Cout = features.shape[1] // P if ps else features.shape[1]
+    out = np.empty((rois.shape[0], Cout), np.float32)
+    rt.check(h.lib.dcn_roi_pool_fwd_host(h.h, ctypes.byref(d), rt.ptr(features), rt.ptr(rois),
+                                         rt.ptr(offsets), rt.ptr(out)), "dcn_roi_pool_fwd_host")
+    return out
+
+
+def roi_pool_backward_numpy(features, rois, offsets, grad_out, output_size, spatial_scale=1.0,
+                            ps=False, part_size=None, trans_std=0.1, no_trans=False,
+                            handle=None):
+    """(∂features, ∂offsets) of roi_pool_forward_numpy; ∂offsets has the caller's offsets
+    shape (zeros when the PS pool ignores them). The RoI boxes get no gradient."""
+    h = handle or rt.default_handle()
+    offsets_in = offsets
+    features, rois, offsets = _roi_args(features, rois, offsets, output_size, ps, no_trans)
+    d = rt.make_roi_desc(features.shape, rois.shape[0], output_size, spatial_scale, ps, part_size,
+                         trans_std, no_trans)
+    R, P = rois.shape[0], output_size[0] * output_size[1]
+    gf = np.empty_like(features)
+    goff = np.zeros((R, P, 2), np.float32)
+    rt.check(h.lib.dcn_roi_pool_bwd_host(h.h, ctypes.byref(d), rt.ptr(features), rt.ptr(rois),
+                                         rt.ptr(offsets), rt.ptr(_f32(grad_out)), rt.ptr(gf),
+                                         rt.ptr(goff)), "dcn_roi_pool_bwd_host")
+    g_in = np.zeros(np.shape(offsets_in), np.float32) if offsets_in is not None else None
+    if g_in is not None:
+        flat = g_in.reshape(R, -1)
+        flat[:, :2 * P] = goff.reshape(R, 2 * P)
+    return gf, g_in
 
 
 # ---------------------------------------------------------------------------
@@ -210,6 +266,68 @@ class DeformConv2dNumpy(Module):
         return g["x"]
 
 
+class _RoIPoolBase(Module):
+    """Shared execute/backward of the two RoI pools (NumPy backend). Like the reference
+    (deform_conv.py:158, :241), execute() reshapes the bin sum to [R, C, ph, pw], which
+    raises for ph*pw != 1 exactly where the reference's reshape does."""
+
+    _ps = False
+
+    def _kw(self):
+        return {}
+
+    def execute(self, features, rois, offsets):
+        s = roi_pool_forward_numpy(features, rois, offsets, self.output_size, self.spatial_scale,
+                                   ps=self._ps, **self._kw())
+        out = s.reshape(np.shape(rois)[0], s.shape[1], *self.output_size)  # :158 / :241
+        if self.training:
+            self._ctx = (features, rois, offsets)
+        return out
+
+    def backward(self, grad_out):
+        """(∂features, ∂offsets) for ∂out of execute's shape."""
+        if getattr(self, "_ctx", None) is None:
+            raise RuntimeError("backward() needs a preceding execute() in training mode")
+        features, rois, offsets = self._ctx
+        g = np.asarray(grad_out, np.float32).reshape(np.shape(rois)[0], -1)
+        return roi_pool_backward_numpy(features, rois, offsets, g, self.output_size,
+                                       self.spatial_scale, ps=self._ps, **self._kw())
+
+
+class DeformRoIPoolNumpy(_RoIPoolBase):
+    """deform_conv.py:85-159: DeformRoIPool(output_size, spatial_scale=1.0,
+    sampling_ratio=1) on libdcn (sampling_ratio is stored, unused, as in the reference)."""
+
+    def __init__(self, output_size, spatial_scale=1.0, sampling_ratio=1):
+        super().__init__()
+        self.output_size = output_size if isinstance(output_size, tuple) else (output_size,
+                                                                              output_size)
+        self.spatial_scale = spatial_scale
+        self.sampling_ratio = sampling_ratio
+
+
+class DeformPSRoIPoolNumpy(_RoIPoolBase):
+    """deform_conv.py:162-241: DeformPSRoIPool(output_size, spatial_scale=1.0,
+    sampling_ratio=1, no_trans=False, group_size=1, part_size=None, trans_std=0.1)."""
+
+    _ps = True
+
+    def __init__(self, output_size, spatial_scale=1.0, sampling_ratio=1, no_trans=False,
+                 group_size=1, part_size=None, trans_std=0.1):
+        super().__init__()
+        self.output_size = output_size if isinstance(output_size, tuple) else (output_size,
+                                                                              output_size)
+        self.spatial_scale = spatial_scale
+        self.sampling_ratio = sampling_ratio
+        self.no_trans = no_trans
+        self.group_size = group_size
+        self.part_size = part_size if part_size else self.output_size
+        self.trans_std = trans_std
+
+    def _kw(self):
+        return dict(part_size=self.part_size, trans_std=self.trans_std, no_trans=self.no_trans)
+
+
 # ---------------------------------------------------------------------------
 # Jittor backend (exercised only where jittor imports; not in the build image)
 # ---------------------------------------------------------------------------
@@ -258,8 +376,62 @@ if HAVE_JITTOR:  # pragma: no cover
         def execute(self, x):
             return _DCNFunction.apply(x, self.offset_conv.weight, self.offset_conv.bias,
                                       self.weight, self.bias, self.stride, self.padding)
+    class _RoIPoolFunction(jt.Function):
+        """jt.Function for both RoI pools: ∂features and ∂offsets reach Jittor autodiff
+        (the boxes get none, as they come from the data)."""
+
+        def execute(self, features, rois, offsets, module):
+            self.m = module
+            self.saved = (features.numpy(), rois.numpy(),
+                          None if offsets is None else offsets.numpy())
+            s = roi_pool_forward_numpy(*self.saved, module.output_size, module.spatial_scale,
+                                       ps=module._ps, **module._kw())
+            return jt.array(s.reshape(rois.shape[0], s.shape[1], *module.output_size))
+
+        def grad(self, grad_out):
+            f, r, o = self.saved
+            m = self.m
+            gf, go = roi_pool_backward_numpy(f, r, o, grad_out.numpy().reshape(r.shape[0], -1),
+                                             m.output_size, m.spatial_scale, ps=m._ps, **m._kw())
+            return jt.array(gf), None, None if go is None else jt.array(go), None
+
+    class DeformRoIPool(jnn.Module):
+        _ps = False
+        _kw = DeformRoIPoolNumpy._kw
+
+        def __init__(self, output_size, spatial_scale=1.0, sampling_ratio=1):
+            super().__init__()
+            self.output_size = output_size if isinstance(output_size, tuple) else (
+                output_size, output_size)
+            self.spatial_scale = spatial_scale
+            self.sampling_ratio = sampling_ratio
+
+        def execute(self, features, rois, offsets):
+            return _RoIPoolFunction.apply(features, rois, offsets, self)
+
+    class DeformPSRoIPool(jnn.Module):
+        _ps = True
+        _kw = DeformPSRoIPoolNumpy._kw
+
+        def __init__(self, output_size, spatial_scale=1.0, sampling_ratio=1, no_trans=False,
+                     group_size=1, part_size=None, trans_std=0.1):
+            super().__init__()
+            self.output_size = output_size if isinstance(output_size, tuple) else (
+                output_size, output_size)
+            self.spatial_scale = spatial_scale
+            self.sampling_ratio = sampling_ratio
+            self.no_trans = no_trans
+            self.group_size = group_size
+            self.part_size = part_size if part_size else self.output_size
+            self.trans_std = trans_std
+
+        def execute(self, features, rois, offsets):
+            return _RoIPoolFunction.apply(features, rois, offsets, self)
 else:
     DeformConv2d = DeformConv2dNumpy
+    DeformRoIPool = DeformRoIPoolNumpy
+    DeformPSRoIPool = DeformPSRoIPoolNumpy
 
-__all__ = ["DeformConv2d", "DeformConv2dNumpy", "dcn_forward_numpy", "dcn_backward_numpy",
-           "HAVE_JITTOR"]
+__all__ = ["DeformConv2d", "DeformConv2dNumpy", "DeformRoIPool", "DeformRoIPoolNumpy",
+           "DeformPSRoIPool", "DeformPSRoIPoolNumpy", "dcn_forward_numpy", "dcn_backward_numpy",
+           "roi_pool_forward_numpy", "roi_pool_backward_numpy", "HAVE_JITTOR"]

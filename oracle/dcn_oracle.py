@@ -273,3 +273,113 @@ def im2col(x, off32, kh, kw, G=1):
     N = kh * kw
     S, _ = deform_sample(x, off32, Ho, Wo, N, G)
     return S.transpose(0, 2, 1, 3, 4).reshape(B, N * C, Ho * Wo)
+
+
+# ---------------------------------------------------------------------------
+# Deformable RoI pooling: deform_conv.py:85-159 (DeformRoIPool) and
+# :162-241 (DeformPSRoIPool). Coordinates in float32 with the reference's op order (the
+# floor decides the corners); feature sums and gradients in float64. Like the reference
+# (`.sum(dim=2)` at :143-157 / :239, before the reshape), the returned forward is the
+# weighted corner sum over ALL bins, [R, C] or [R, C // P]; the reference's module then
+# reshapes it to [R, C, ph, pw], which only succeeds for ph*pw == 1.
+# ---------------------------------------------------------------------------
+def roi_bins(rois, offsets, H, W, output_size, spatial_scale=1.0, ps=False, part_size=None,
+             trans_std=0.1, no_trans=False):
+    """Per (roi, bin): batch index, clamped corners, dx/dy, weights, offset scale."""
+    f = F32
+    ph, pw = output_size
+    P = ph * pw
+    rois = np.asarray(rois, f)
+    R = rois.shape[0]
+    b = np.trunc(rois[:, 0]).astype(np.int64)  # rois[:, 0].long() (:94 / :179)
+    rc = rois[:, 1:5] * f(spatial_scale)  # :96 / :181
+    x1, y1, x2, y2 = rc[:, 0], rc[:, 1], rc[:, 2], rc[:, 3]
+    rw = np.maximum(x2 - x1, f(1e-6))  # :98-99 / :183-184
+    rh = np.maximum(y2 - y1, f(1e-6))
+    hg, wg = np.meshgrid(np.arange(ph, dtype=f), np.arange(pw, dtype=f), indexing="ij")
+    hf, wf = hg.reshape(-1), wg.reshape(-1)  # :101-105 / :186-190
+    bw_div, bh_div = (part_size[1], part_size[0]) if (ps and part_size) else (pw, ph)
+    bw = rw[:, None] / f(bw_div)  # :107-108 / :191-192
+    bh = rh[:, None] / f(bh_div)
+    bcx = x1[:, None] + (wf + f(0.5)) * bw  # :110-111 / :194-195
+    bcy = y1[:, None] + (hf + f(0.5)) * bh
+    sx = np.zeros((R, P), f)
+    sy = np.zeros((R, P), f)
+    if not ps:  # :113-117
+        o = np.asarray(offsets, f).reshape(R, P, 2)
+        cx = bcx + o[:, :, 0] * rw[:, None]
+        cy = bcy + o[:, :, 1] * rh[:, None]
+        sx[:], sy[:] = rw[:, None], rh[:, None]
+    elif not no_trans:  # :197-201
+        o = np.asarray(offsets, f).reshape(R, -1)[:, :2 * P].reshape(R, P, 2)
+        cx = bcx + o[:, :, 0] * rw[:, None] * f(trans_std)
+        cy = bcy + o[:, :, 1] * rh[:, None] * f(trans_std)
+        sx[:], sy[:] = rw[:, None] * f(trans_std), rh[:, None] * f(trans_std)
+    else:
+        cx, cy = bcx, bcy
+    fx = np.floor(cx).astype(np.int64)
+    fy = np.floor(cy).astype(np.int64)
+    x0, x1c = np.clip(fx, 0, W - 1), np.clip(fx + 1, 0, W - 1)  # :121-129 / :214-222
+    y0, y1c = np.clip(fy, 0, H - 1), np.clip(fy + 1, 0, H - 1)
+    dx = cx - x0.astype(f)  # :131-132 / :224-225
+    dy = cy - y0.astype(f)
+    w = ((f(1) - dx) * (f(1) - dy), (f(1) - dx) * dy, dx * (f(1) - dy), dx * dy)  # :134-137
+    return dict(b=b, corners=((y0, x0), (y1c, x0), (y0, x1c), (y1c, x1c)), dx=dx, dy=dy, w=w,
+                sx=sx, sy=sy, P=P)
+
+
+def _roi_channels(C, P, ps):
+    """Feature channel of (output channel co, bin p): co, or co*P + p (:232-233)."""
+    Cout = C // P if ps else C
+    co = np.arange(Cout)[:, None]
+    p = np.arange(P)[None, :]
+    return Cout, (co * P + p) if ps else np.broadcast_to(co, (Cout, P))
+
+
+def roi_pool_forward(features, rois, offsets, output_size, spatial_scale=1.0, ps=False,
+                     part_size=None, trans_std=0.1, no_trans=False):
+    feat = np.asarray(features, np.float64)
+    B, C, H, W = feat.shape
+    bn = roi_bins(rois, offsets, H, W, output_size, spatial_scale, ps, part_size, trans_std,
+                  no_trans)
+    P = bn["P"]
+    Cout, ch = _roi_channels(C, P, ps)
+    R = bn["b"].shape[0]
+    out = np.zeros((R, Cout))
+    for k in range(4):
+        y, x = bn["corners"][k]
+        wk = bn["w"][k].astype(np.float64)
+        for r in range(R):
+            v = feat[bn["b"][r]][ch, y[r][None, :], x[r][None, :]]  # [Cout, P]
+            out[r] += (v * wk[r][None, :]).sum(axis=1)
+    return out
+
+
+def roi_pool_backward(features, rois, offsets, grad_out, output_size, spatial_scale=1.0,
+                      ps=False, part_size=None, trans_std=0.1, no_trans=False):
+    """(∂features [B,C,H,W], ∂offsets [R,P,2]) of roi_pool_forward (float64)."""
+    feat = np.asarray(features, np.float64)
+    B, C, H, W = feat.shape
+    bn = roi_bins(rois, offsets, H, W, output_size, spatial_scale, ps, part_size, trans_std,
+                  no_trans)
+    P = bn["P"]
+    Cout, ch = _roi_channels(C, P, ps)
+    g = np.asarray(grad_out, np.float64).reshape(-1, Cout)
+    R = g.shape[0]
+    gf = np.zeros_like(feat)
+    goff = np.zeros((R, P, 2))
+    dx, dy = bn["dx"].astype(np.float64), bn["dy"].astype(np.float64)
+    for r in range(R):
+        b = bn["b"][r]
+        f = [feat[b][ch, bn["corners"][k][0][r][None, :], bn["corners"][k][1][r][None, :]]
+             for k in range(4)]  # each [Cout, P]
+        for k in range(4):
+            y, x = bn["corners"][k]
+            contrib = g[r][:, None] * bn["w"][k][r].astype(np.float64)[None, :]
+            np.add.at(gf[b], (ch, np.broadcast_to(y[r], ch.shape), np.broadcast_to(x[r], ch.shape)),
+                      contrib)
+        dcx = ((1 - dy[r]) * (f[2] - f[0]) + dy[r] * (f[3] - f[1]))  # [Cout, P]
+        dcy = ((1 - dx[r]) * (f[1] - f[0]) + dx[r] * (f[3] - f[2]))
+        goff[r, :, 0] = (g[r][:, None] * dcx).sum(axis=0) * bn["sx"][r]
+        goff[r, :, 1] = (g[r][:, None] * dcy).sum(axis=0) * bn["sy"][r]
+    return gf, goff
