@@ -120,6 +120,9 @@ def main():
     ap.add_argument("--comm", choices=("torch", "libdcn"), default="torch",
                     help="gradient all-reduce transport for N>1: torch.distributed (RCCL) or "
                          "libdcn's own RCCL communicator (dcn_allreduce_grads)")
+    ap.add_argument("--math", type=int, default=0, choices=(0, 3, 6, 9),
+                    help="GEMM arithmetic (include/dcn.h dcn_math): 0 native f32 MFMA, "
+                         "6/9 split-bf16 fp32 (X6/X9), 3 two-plane opt-in")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (default: newest profiles/r*_pmc_hbm.json)")
@@ -179,6 +182,7 @@ def main():
     h = rt.Handle(local_rank)
     stream = torch.cuda.current_stream(dev)
     h.set_stream(stream.cuda_stream)
+    h.set_math(args.math)
     L = h.lib
     P = lambda t: t.data_ptr()
     comm = None
@@ -257,6 +261,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": cfg["dtype"],
+            "gemm_math": {0: "f32 MFMA (vendor)", 3: "f32 split-bf16 X3", 6: "f32 split-bf16 X6",
+                          9: "f32 split-bf16 X9"}[args.math] if not bf16 else "bf16 MFMA",
             "data": "synthetic",
             "config": {"workload": f"config{args.config}: B={B}/GPU C={C}->O={O_} {H}x{W} k{k} s{s} "
                                    f"p{p} dil{dil} G{G} {cfg['dtype']} DeformConv2d "

@@ -229,7 +229,30 @@ int dcn_comm_destroy(dcn_comm* c);
 /* In-place sum over ranks of `count` fp32 device values, on the handle's stream. */
 int dcn_allreduce_grads(dcn_handle* h, dcn_comm* c, float* grads, size_t count);
 
+/* ---- GEMM arithmetic ------------------------------------------------------------ */
+/* How the three fp32 GEMMs of the op (deform_conv.py:76 and its two autodiff GEMMs)
+ * compute. DCN_MATH_F32 (default): native f32 MFMA in the vendor libraries.
+ * DCN_MATH_F32_BF16X9 / _BF16X6: every fp32 operand split exactly into three bf16 planes
+ * (hi + mid + lo == a), products on the bf16 matrix cores with fp32 accumulation; X9
+ * keeps all nine plane products (each exact), X6 drops the three below 2^-23 relative
+ * (one fp32 rounding). DCN_MATH_F32_BF16X3: two planes, ~2^-17 relative (opt-in).
+ * The bf16 tensor path (dtype DCN_BF16) is unaffected. Env DCN_MATH sets the default of
+ * new handles. No reference counterpart (Jittor matmul in fp32, deform_conv.py:76). */
+typedef enum {
+  DCN_MATH_F32 = 0,
+  DCN_MATH_F32_BF16X3 = 3,
+  DCN_MATH_F32_BF16X6 = 6,
+  DCN_MATH_F32_BF16X9 = 9
+} dcn_math;
+int dcn_set_math(dcn_handle* h, int math);
+int dcn_get_math(dcn_handle* h, int* math);
+
 /* ---- testing ------------------------------------------------------------------ */
+/* One fp32 GEMM through the handle's engine under its current math mode, BLAS
+ * column-major convention: C(m×n) = op(A)·op(B), batched by element strides. */
+int dcn_debug_gemm(dcn_handle* h, int ta, int tb, int m, int n, int k, const float* A,
+                   int lda, long sa, const float* B, int ldb, long sb, float* C, int ldc,
+                   long sc, int batch);
 /* 1 = route K1/K5 through the generic global-gather kernels (independent
  * implementation used by the parity tests to cross-check the LDS-window ones). */
 int dcn_debug_force_generic(int on);

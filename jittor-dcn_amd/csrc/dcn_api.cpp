@@ -244,6 +244,14 @@ int join_aux(dcn_handle* h) {
   return DCN_OK;
 }
 
+// Split-bf16 GEMM arithmetic (dcn_math X3/X6/X9) applies to this call: fp32 tensors and
+// operand strides the split kernel can stage (else the vendor f32 GEMMs run).
+// Split-bf16 GEMM arithmetic (dcn_math X3/X6/X9) for the forward GEMM with its bias fused
+// (the two backward GEMMs reach the split kernels through dcn::gemm_run).
+bool use_split(dcn_handle* h, const Geo& g) {
+  return dcn::gemm_get_math(h->gemm) != 0 && g.dt == DCN_F32;
+}
+
 int core_forward(dcn_handle* h, const Geo& g, const float* x, const float* off, const float* w,
                  const float* b, bool has_bias, float* out, float* xT, float* colT,
                  bool xT_ready) {
@@ -266,6 +274,12 @@ int core_forward(dcn_handle* h, const Geo& g, const float* x, const float* off, 
     sp.ldb = g.K; sp.sb = 0;
     sp.ldc = g.HW; sp.sc = (long)g.O * g.HW;
     sp.batch = g.B;
+    if (use_split(h, g) && dcn::gemm_split_ok(sp, colT, w, out)) {
+      // split-bf16 arithmetic with the bias in the epilogue
+      HIP_TRY(dcn::launch_gemm_split(dcn::gemm_get_math(h->gemm), sp, colT, w, out, h->stream,
+                                     has_bias ? b : nullptr));
+      return DCN_OK;
+    }
     GEMM_TRY(h, sp, colT, w, out);
   }
   if (has_bias) {
@@ -1081,6 +1095,37 @@ __attribute__((visibility("hidden"))) int dcn_internal_bind(dcn_handle* h, void*
 // Test hook: force the generic global-memory im2col/col2im kernels.
 int dcn_debug_force_generic(int on) {
   dcn::set_force_generic(on);
+  return DCN_OK;
+}
+
+int dcn_set_math(dcn_handle* h, int math) {
+  if (!h) return fail(DCN_ERR_INVALID, "dcn_set_math: null handle");
+  if (math != DCN_MATH_F32 && math != DCN_MATH_F32_BF16X3 && math != DCN_MATH_F32_BF16X6 &&
+      math != DCN_MATH_F32_BF16X9)
+    return fail(DCN_ERR_INVALID, "dcn_set_math: unknown mode " + std::to_string(math));
+  dcn::gemm_set_math(h->gemm, math);
+  return DCN_OK;
+}
+
+int dcn_get_math(dcn_handle* h, int* math) {
+  if (!h || !math) return fail(DCN_ERR_INVALID, "dcn_get_math: null argument");
+  *math = dcn::gemm_get_math(h->gemm);
+  return DCN_OK;
+}
+
+int dcn_debug_gemm(dcn_handle* h, int ta, int tb, int m, int n, int k, const float* A, int lda,
+                   long sa, const float* B, int ldb, long sb, float* C, int ldc, long sc,
+                   int batch) {
+  if (!h || !A || !B || !C || m <= 0 || n <= 0 || k <= 0 || batch <= 0)
+    return fail(DCN_ERR_INVALID, "dcn_debug_gemm: bad argument");
+  DCN_TRY(set_device(h));
+  dcn::GemmSpec sp;
+  sp.ta = ta != 0; sp.tb = tb != 0;
+  sp.m = m; sp.n = n; sp.k = k;
+  sp.lda = lda; sp.ldb = ldb; sp.ldc = ldc;
+  sp.sa = sa; sp.sb = sb; sp.sc = sc;
+  sp.batch = batch;
+  GEMM_TRY(h, sp, A, B, C);
   return DCN_OK;
 }
 

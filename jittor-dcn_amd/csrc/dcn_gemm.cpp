@@ -53,6 +53,7 @@ struct GemmEngine {
   std::map<decltype(key_of(GemmSpec())), Plan> plans;
   int force = -1;  // -1 auto, 0 rocBLAS, 1 hipBLASLt
   int candidates = 8;  // hipBLASLt heuristic candidates timed per shape (DCN_GEMM_CANDIDATES)
+  int math = 0;        // dcn_math: 0 native f32, 3/6/9 split-bf16 products (DCN_MATH)
 };
 
 int gemm_engine_create(GemmEngine** out, std::string* err) {
@@ -69,6 +70,7 @@ int gemm_engine_create(GemmEngine** out, std::string* err) {
     if (!std::strcmp(f, "rocblas")) e->force = 0;
     if (!std::strcmp(f, "hipblaslt")) e->force = 1;
   }
+  if (const char* f = std::getenv("DCN_MATH")) gemm_set_math(e, std::atoi(f));
   *out = e;
   return 0;
 }
@@ -225,8 +227,25 @@ static int tune(GemmEngine* e, const GemmSpec& s, const void* A, const void* B, 
   return 0;
 }
 
+void gemm_set_math(GemmEngine* e, int math) {
+  e->math = (math == 3 || math == 6 || math == 9) ? math : 0;
+}
+int gemm_get_math(GemmEngine* e) { return e->math; }
+
 int gemm_run(GemmEngine* e, const GemmSpec& s, const void* A, const void* B, void* C,
              hipStream_t st, std::string* err) {
+  // split-bf16 arithmetic for fp32 operands when selected (the bf16 tensor path keeps the
+  // vendor bf16 GEMMs); shapes the split kernel cannot stage fall back to native f32
+  if (e->math && gemm_split_ok(s, A, B, C)) {
+    const hipError_t r = launch_gemm_split(e->math, s, static_cast<const float*>(A),
+                                           static_cast<const float*>(B), static_cast<float*>(C),
+                                           st);
+    if (r != hipSuccess) {
+      *err = std::string("split GEMM launch: ") + hipGetErrorString(r);
+      return -1;
+    }
+    return 0;
+  }
   auto it = e->plans.find(key_of(s));
   if (it == e->plans.end()) {
     Plan p;
@@ -238,6 +257,7 @@ int gemm_run(GemmEngine* e, const GemmSpec& s, const void* A, const void* B, voi
 }
 
 int gemm_backend_of(GemmEngine* e, const GemmSpec& s) {
+  if (e->math && !s.bf16_ab && !s.bf16_c) return 2;
   auto it = e->plans.find(key_of(s));
   return it == e->plans.end() ? -1 : it->second.backend;
 }

@@ -140,7 +140,18 @@ void gemm_engine_destroy(GemmEngine* e);
 // A, B, C point to fp32 or bf16 elements as the spec says
 int gemm_run(GemmEngine* e, const GemmSpec& s, const void* A, const void* B, void* C,
              hipStream_t st, std::string* err);
-int gemm_backend_of(GemmEngine* e, const GemmSpec& s);  // -1 untuned, 0 rocBLAS, 1 hipBLASLt
+int gemm_backend_of(GemmEngine* e, const GemmSpec& s);  // -1 untuned, 0 rocBLAS, 1 hipBLASLt,
+                                                        // 2 split-bf16 (dcn_gemm_split.hip)
+// GEMM arithmetic of fp32 products (dcn_math): 0 native f32 MFMA (vendor libraries),
+// 3 / 6 / 9 = split-bf16 products on the bf16 matrix cores (dcn_gemm_split.hip).
+void gemm_set_math(GemmEngine* e, int math);
+int gemm_get_math(GemmEngine* e);
+bool gemm_split_ok(const GemmSpec& s, const void* A, const void* B, const void* C);
+// column-major C (+ bias[n] if bias) = op(A)·op(B) in split-bf16 arithmetic (math 3/6/9);
+// form 1 = loads after the MFMAs (3 workgroups/CU, the measured default), 0 = before
+hipError_t launch_gemm_split(int math, const GemmSpec& s, const float* A, const float* B,
+                             float* C, hipStream_t st, const float* bias = nullptr,
+                             int form = 1);
 
 // Selection of the im2col / col2im implementation (tests force the generic
 // global-memory kernels to cross-check the channels-last ones).

@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("DCN_LIB", os.path.join(HERE, "lib", "libdcn.so"))
 
 DCN_F32, DCN_BF16 = 0, 1
 DCN_BWD_COL_IN_WS = 1
+DCN_MATH_F32, DCN_MATH_F32_BF16X3, DCN_MATH_F32_BF16X6, DCN_MATH_F32_BF16X9 = 0, 3, 6, 9
 KERNEL_IDS = {
     "offset_fwd": 0, "im2col": 1, "gemm_fwd": 2, "bias_fwd": 3, "bwd_bias": 4,
     "gemm_dw": 5, "gemm_dcol": 6, "col2im": 7, "offset_bwd": 8, "xpose": 9,
@@ -77,6 +78,11 @@ SIGNATURES = {
     "dcn_comm_destroy": [_vp],
     "dcn_allreduce_grads": [_vp, _vp, _vp, _sz],
     "dcn_debug_force_generic": [ctypes.c_int],
+    "dcn_set_math": [_vp, ctypes.c_int],
+    "dcn_get_math": [_vp, _ip],
+    "dcn_debug_gemm": [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                       _vp, ctypes.c_int, ctypes.c_long, _vp, ctypes.c_int, ctypes.c_long, _vp,
+                       ctypes.c_int, ctypes.c_long, ctypes.c_int],
     "dcn_roi_pool_fwd": [_vp, ctypes.POINTER(RoiDesc), _vp, _vp, _vp, _vp],
     "dcn_roi_pool_bwd": [_vp, ctypes.POINTER(RoiDesc), _vp, _vp, _vp, _vp, _vp, _vp],
     "dcn_roi_pool_fwd_host": [_vp, ctypes.POINTER(RoiDesc), _vp, _vp, _vp, _vp],
@@ -204,6 +210,16 @@ class Handle:
     def d2h(self, arr, src: int):
         check(self.lib.dcn_memcpy_d2h(self.h, arr.ctypes.data_as(_vp), ctypes.c_void_p(src),
                                       arr.nbytes), "dcn_memcpy_d2h")
+
+    # --- GEMM arithmetic (include/dcn.h dcn_math) ---------------------------------
+    def set_math(self, math: int):
+        """0 native f32 MFMA; 3 / 6 / 9 split-bf16 products (DCN_MATH_F32_BF16X*)."""
+        check(self.lib.dcn_set_math(self.h, int(math)), "dcn_set_math")
+
+    def get_math(self) -> int:
+        m = ctypes.c_int()
+        check(self.lib.dcn_get_math(self.h, ctypes.byref(m)), "dcn_get_math")
+        return m.value
 
     # --- profiling -------------------------------------------------------------
     def prof_enable(self, capacity: int):
