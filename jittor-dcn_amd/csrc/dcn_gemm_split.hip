@@ -29,7 +29,8 @@
 //          across them and three workgroups per CU fit (≤ 168 VGPRs); the other
 //          workgroups hide the load latency. fwd / ∂W / ∂col 1.21 / 1.32 / 1.54 ms;
 //   EARLY: next tile's loads issued before the MFMAs, two workgroups per CU:
-//          1.30 / 1.38 / 1.74 ms.
+//          1.30 / 1.38 / 1.74 ms (with two register sets, loads two k-steps ahead:
+//          1.26 / 1.37 / 1.77 — load latency is not what limits it).
 // LDS images per plane:
 //   k-contiguous operand   → [idx][32 k] bf16, 64-B rows, 16-B chunks XOR-swizzled by
 //                            bit 3 of idx, fragments by ds_read_b128;
@@ -204,8 +205,10 @@ struct Args {
   int n_fast;  // consecutive tiles walk n (share the A panel)
 };
 
-template <int NPROD, bool A_KC, bool B_KC, bool LATE>
-__global__ __launch_bounds__(NT, LATE ? 3 : 2) void gemm_split_kernel(Args s) {
+// FORM 0 (EARLY): next step's loads before the MFMAs, 2 workgroups/CU; 1 (LATE): after
+// the MFMAs, 3 workgroups/CU.
+template <int NPROD, bool A_KC, bool B_KC, int FORM>
+__global__ __launch_bounds__(NT, FORM == 1 ? 3 : 2) void gemm_split_kernel(Args s) {
   constexpr int P = NPROD == 3 ? 2 : 3;
   using TA = Tile<A_KC, P>;
   using TB = Tile<B_KC, P>;
@@ -238,20 +241,13 @@ __global__ __launch_bounds__(NT, LATE ? 3 : 2) void gemm_split_kernel(Args s) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
-  TA ta;
-  TB tb;
   const int nk = (s.k + BK - 1) / BK;
-  ta.load(s.A, b, m0, 0, s.k, tid);
-  tb.load(s.B, b, n0, 0, s.k, tid);
-  for (int kt = 0; kt < nk; ++kt) {
-    ta.store(lds, tid);
-    tb.store(lds + TA::BYTES, tid);
-    __syncthreads();
-    const int k1 = (kt + 1 < nk ? kt + 1 : kt) * BK;  // clamped: no branch around loads
-    if constexpr (!LATE) {
-      ta.load(s.A, b, m0, k1, s.k, tid);
-      tb.load(s.B, b, n0, k1, s.k, tid);
-    }
+  auto load = [&](TA& ta, TB& tb, int kt) {
+    const int k0 = (kt < nk ? kt : nk - 1) * BK;  // clamped: no branch around the loads
+    ta.load(s.A, b, m0, k0, s.k, tid);
+    tb.load(s.B, b, n0, k0, s.k, tid);
+  };
+  auto mfmas = [&]() {
     // m fragments of every plane (MFMA B operand), then n fragments one at a time
     bf16x8 fm[4][P];
 #pragma unroll
@@ -267,12 +263,21 @@ __global__ __launch_bounds__(NT, LATE ? 3 : 2) void gemm_split_kernel(Args s) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = mfma_planes<NPROD, P>(fn, fm[j], acc[i][j]);
     }
-    if constexpr (LATE) {
-      ta.load(s.A, b, m0, k1, s.k, tid);
-      tb.load(s.B, b, n0, k1, s.k, tid);
-    }
+  };
+  // one k-step from register set (ta, tb), which is then refilled with step kt + ahead
+  auto step = [&](TA& ta, TB& tb, int kt, int ahead) {
+    ta.store(lds, tid);
+    tb.store(lds + TA::BYTES, tid);
     __syncthreads();
-  }
+    if constexpr (FORM != 1) load(ta, tb, kt + ahead);
+    mfmas();
+    if constexpr (FORM == 1) load(ta, tb, kt + ahead);
+    __syncthreads();
+  };
+  TA ta;
+  TB tb;
+  load(ta, tb, 0);
+  for (int kt = 0; kt < nk; ++kt) step(ta, tb, kt, 1);
 
   // epilogue: acc[i][j][r] = C(m = m0 + 64wm + 16j + (lane&15), n = n0 + 64wn + 16i +
   // 4(lane>>4) + r); the 16 lanes of one register store 64 contiguous bytes of a column
@@ -292,21 +297,21 @@ __global__ __launch_bounds__(NT, LATE ? 3 : 2) void gemm_split_kernel(Args s) {
 }
 
 template <int NPROD, bool A_KC, bool B_KC>
-hipError_t launch_t(const Args& a, bool late, hipStream_t st) {
+hipError_t launch_t(const Args& a, int form, hipStream_t st) {
   const int T = a.tiles_m * a.tiles_n * a.batch;
-  if (late)
-    hipLaunchKernelGGL((gemm_split_kernel<NPROD, A_KC, B_KC, true>), dim3(T), dim3(NT), 0, st, a);
+  if (form == 1)
+    hipLaunchKernelGGL((gemm_split_kernel<NPROD, A_KC, B_KC, 1>), dim3(T), dim3(NT), 0, st, a);
   else
-    hipLaunchKernelGGL((gemm_split_kernel<NPROD, A_KC, B_KC, false>), dim3(T), dim3(NT), 0, st, a);
+    hipLaunchKernelGGL((gemm_split_kernel<NPROD, A_KC, B_KC, 0>), dim3(T), dim3(NT), 0, st, a);
   return hipGetLastError();
 }
 
 template <int NPROD>
-hipError_t launch_p(const Args& a, bool a_kc, bool b_kc, bool late, hipStream_t st) {
-  if (a_kc && b_kc) return launch_t<NPROD, true, true>(a, late, st);
-  if (a_kc) return launch_t<NPROD, true, false>(a, late, st);
-  if (b_kc) return launch_t<NPROD, false, true>(a, late, st);
-  return launch_t<NPROD, false, false>(a, late, st);
+hipError_t launch_p(const Args& a, bool a_kc, bool b_kc, int form, hipStream_t st) {
+  if (a_kc && b_kc) return launch_t<NPROD, true, true>(a, form, st);
+  if (a_kc) return launch_t<NPROD, true, false>(a, form, st);
+  if (b_kc) return launch_t<NPROD, false, true>(a, form, st);
+  return launch_t<NPROD, false, false>(a, form, st);
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -345,14 +350,14 @@ hipError_t launch_gemm_split(int math, const GemmSpec& s, const float* A, const 
   const double a_el = (double)s.m * s.k * (s.sa ? s.batch : 1);
   const double b_el = (double)s.n * s.k * (s.sb ? s.batch : 1);
   a.n_fast = a_el >= b_el;
-  // form: 0 EARLY, 1 LATE (A/B knob DCN_EXP slot 4: 1 forces EARLY, 2 forces LATE)
+  // form: 0 EARLY, 1 LATE (A/B knob DCN_EXP slot 4 = form + 1)
   const int knob = exp_flag(4);
-  const bool late = knob ? knob == 2 : form == 1;
+  if (knob == 1 || knob == 2) form = knob - 1;
   const bool a_kc = s.ta, b_kc = !s.tb;
   switch (math) {
-    case 3: return launch_p<3>(a, a_kc, b_kc, late, st);
-    case 9: return launch_p<9>(a, a_kc, b_kc, late, st);
-    default: return launch_p<6>(a, a_kc, b_kc, late, st);
+    case 3: return launch_p<3>(a, a_kc, b_kc, form, st);
+    case 9: return launch_p<9>(a, a_kc, b_kc, form, st);
+    default: return launch_p<6>(a, a_kc, b_kc, form, st);
   }
 }
 

@@ -1,0 +1,15 @@
+#!/bin/bash
+# SQ counter passes over a short split-GEMM bench (MATH, default 6); each pass its own run.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -s KILL 60 rocprofv3 --list-avail > gpurun_out/pmc_avail.txt 2>&1 || true
+i=0
+for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
+           "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_BUSY_CYCLES SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_SCA SQ_INSTS_VMEM" \
+           ${EXTRA_SETS}; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $set --kernel-trace -d gpurun_out/pmcg_$i -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --math ${MATH:-6} > gpurun_out/pmcg_$i.log 2>&1 || { echo "pass $i failed"; tail -3 gpurun_out/pmcg_$i.log; }
+done
+echo done
