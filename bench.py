@@ -110,6 +110,10 @@ def load_traffic(path, bf16=False):
     return None, None
 
 
+MATH_NAMES = {0: "f32 MFMA (rocBLAS/hipBLASLt)", 3: "f32 via split-bf16 X3 (2 planes, opt-in)",
+              6: "f32 via exact-split bf16 X6", 9: "f32 via exact-split bf16 X9"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -123,6 +127,9 @@ def main():
     ap.add_argument("--math", type=int, default=0, choices=(0, 3, 6, 9),
                     help="GEMM arithmetic (include/dcn.h dcn_math): 0 native f32 MFMA, "
                          "6/9 split-bf16 fp32 (X6/X9), 3 two-plane opt-in")
+    ap.add_argument("--alt-math", type=int, default=6, choices=(0, 3, 6, 9),
+                    help="also time this GEMM arithmetic after the headline run (N=1, fp32 "
+                         "configs; 0 = skip) and report it under 'alt'")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (default: newest profiles/r*_pmc_hbm.json)")
@@ -236,6 +243,35 @@ def main():
         tot, cnt = h.prof_read(name)
         if cnt:
             kernel_ms[name] = round(tot / cnt, 4)
+    # the same step under another GEMM arithmetic (split-bf16 X6 by default), reported
+    # beside the headline, never as `value`
+    alt = None
+    if world == 1 and not bf16 and args.alt_math and args.alt_math != args.math:
+        h.prof_enable(0)  # profiling off for the timed region
+        h.set_math(args.alt_math)
+        for _ in range(max(2, args.warmup)):
+            step()
+        torch.cuda.synchronize(dev)
+        ta = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        el_alt = time.perf_counter() - ta
+        h.prof_enable(args.steps)
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        alt_k = {}
+        for name in ("gemm_fwd", "gemm_dw", "gemm_dcol"):
+            tot, cnt = h.prof_read(name)
+            if cnt:
+                alt_k[name] = round(tot / cnt, 4)
+        h.set_math(args.math)
+        alt = {"gemm_math": MATH_NAMES[args.alt_math],
+               "value": round(B * Ho * Wo * N * args.steps / el_alt / 1e9, 5),
+               "ms_per_step": round(el_alt / args.steps * 1e3, 4), "kernel_ms": alt_k,
+               "note": "same synthetic step, GEMMs in exact-split bf16 MFMA arithmetic "
+                       "(DESIGN.md §4.6); reported beside the headline, not as value"}
     k1_ms = kernel_ms.get("im2col")
     k1_b = k1_bytes(B, C, H, W, N, Ho, Wo, elem=2 if bf16 else 4, J=J)
     k1_name = K1_KERNEL if (G == 1 and C % 4 == 0) else "dcn::im2col_cl"
@@ -261,8 +297,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": cfg["dtype"],
-            "gemm_math": {0: "f32 MFMA (vendor)", 3: "f32 split-bf16 X3", 6: "f32 split-bf16 X6",
-                          9: "f32 split-bf16 X9"}[args.math] if not bf16 else "bf16 MFMA",
+            "gemm_math": MATH_NAMES[args.math] if not bf16 else "bf16 MFMA (fp32 accumulate)",
             "data": "synthetic",
             "config": {"workload": f"config{args.config}: B={B}/GPU C={C}->O={O_} {H}x{W} k{k} s{s} "
                                    f"p{p} dil{dil} G{G} {cfg['dtype']} DeformConv2d "
@@ -285,6 +320,7 @@ def main():
                 "avg_launch_ms": k1_ms,
             },
             "kernel_ms": kernel_ms,
+            "alt": alt,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
