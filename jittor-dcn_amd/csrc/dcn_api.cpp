@@ -244,8 +244,6 @@ int join_aux(dcn_handle* h) {
   return DCN_OK;
 }
 
-// Split-bf16 GEMM arithmetic (dcn_math X3/X6/X9) applies to this call: fp32 tensors and
-// operand strides the split kernel can stage (else the vendor f32 GEMMs run).
 // Split-bf16 GEMM arithmetic (dcn_math X3/X6/X9) for the forward GEMM with its bias fused
 // (the two backward GEMMs reach the split kernels through dcn::gemm_run).
 bool use_split(dcn_handle* h, const Geo& g) {
@@ -342,7 +340,10 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
       sp.ldc = g.K; sp.sc = (long)g.K * g.O;
       sp.batch = g.B;
       GEMM_TRY(h, sp, colT, gout, parts);
-      HIP_TRY(dcn::launch_sum_partials(parts, g.B, (size_t)g.K * g.O, gw, h->stream));
+      // the fixed-order Σ_b (151 MB read at config 3) on the side stream, beside the ∂col
+      // GEMM (which only reads the weight and ∂out and overwrites the columns)
+      DCN_TRY(fork_aux(h));
+      HIP_TRY(dcn::launch_sum_partials(parts, g.B, (size_t)g.K * g.O, gw, h->aux));
     }
   }
   {
@@ -824,9 +825,14 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
                         (flags & DCN_BWD_COL_IN_WS) != 0, &ob, &ob_done));
   if (ob_done) return DCN_OK;
   ProfScope ps(h, DCN_K_OFFSET_BWD);
+  // ∂b_off = Σ ∂offset (18 channels: a latency-bound reduction) on the side stream, beside
+  // the offset-conv ∂W / ∂x kernels
+  DCN_TRY(fork_aux(h));
+  dcn::launch_channel_sum(goff, g.B, g.J, g.HW, grad_b_off, h->aux);
   HIP_TRY(dcn::launch_offset_conv_bwd(g, x, F(L.xT), w_off, goff, F(L.goffT), F(L.wt), grad_x,
-                                      grad_w_off, grad_b_off,
+                                      grad_w_off, nullptr,
                                       dcn::get_force_generic() ? nullptr : F(L.gxT), h->stream));
+  DCN_TRY(join_aux(h));
   return DCN_OK;
 }
 

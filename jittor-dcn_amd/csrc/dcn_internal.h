@@ -73,6 +73,7 @@ hipError_t launch_offset_conv_fwd(const Geo& g, const float* x, const float* w_o
 // xT: channels-last x; goffT: scratch of offset_conv_goffT_floats(g). gxT_in == NULL:
 // grad_x is accumulated; else grad_x = transpose(gxT_in) + the offset-conv route, written
 // once (gxT_in: the sampling-route ∂x left channels-last by launch_col2im_*).
+// gb_off == NULL: the caller computes ∂b_off (launch_channel_sum) itself.
 hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
                                   const float* w_off, const float* goff, float* goffT, float* wt2,
                                   float* gx, float* gw_off, float* gb_off, const float* gxT_in,

@@ -573,9 +573,11 @@ __global__ __launch_bounds__(256) void offset_wgrad_mfma(Geo g, const float* __r
         const float ay = __uint_as_float(__float_as_uint(ring[d].y) & keep);
         const float az = __uint_as_float(__float_as_uint(ring[d].z) & keep);
         const float aw = __uint_as_float(__float_as_uint(ring[d].w) & keep);
+        // the padding steps past nsteps read LDS beyond the staged rows: mask B as well as
+        // A (0 x a stale NaN/Inf bit pattern would poison the accumulator)
         float bv[NTW];
 #pragma unroll
-        for (int u = 0; u < NTW; ++u) bv[u] = S[sb + bv0[u]];
+        for (int u = 0; u < NTW; ++u) bv[u] = __uint_as_float(__float_as_uint(S[sb + bv0[u]]) & keep);
         sb += 4 * g.J;
         if (++sx == nq) sx = 0, sb += row_skip;
 #pragma unroll
@@ -916,7 +918,7 @@ hipError_t launch_offset_bwd_finish(const Geo& g, const float* goff, const float
   const long E = (long)g.C * g.J * g.kh * g.kw;
   hipLaunchKernelGGL(wgrad_mfma_reduce, dim3((unsigned)((E + 63) / 64)), dim3(1024), 0, s, g,
                      goffT, g.B * ms.cpi, gw_off);
-  launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
+  if (gb_off) launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
   return hipGetLastError();
 }
 
@@ -935,7 +937,7 @@ hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
     if (e == hipSuccess) e = launch_offset_bwd_finish(g, goff, goffT, gw_off, gb_off, s);
     return e;
   }
-  launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
+  if (gb_off) launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
   if (generic) {
     hipError_t e = hipMemsetAsync(gw_off, 0, (size_t)g.J * g.C * KK * sizeof(float), s);
     if (e != hipSuccess) return e;
