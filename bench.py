@@ -130,6 +130,9 @@ def main():
     ap.add_argument("--alt-math", type=int, default=6, choices=(0, 3, 6, 9),
                     help="also time this GEMM arithmetic after the headline run (N=1, fp32 "
                          "configs; 0 = skip) and report it under 'alt'")
+    ap.add_argument("--fwd-path", type=int, default=0, choices=(0, 1, 2),
+                    help="forward schedule (include/dcn.h dcn_fwd_path): 0 auto, 1 K1 + vendor "
+                         "GEMM + bias, 2 fused im2col+GEMM where it applies")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (default: newest profiles/r*_pmc_hbm.json)")
@@ -190,6 +193,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     h.set_stream(stream.cuda_stream)
     h.set_math(args.math)
+    h.set_fwd_path(args.fwd_path)
     L = h.lib
     P = lambda t: t.data_ptr()
     comm = None

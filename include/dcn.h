@@ -247,6 +247,17 @@ typedef enum {
 int dcn_set_math(dcn_handle* h, int math);
 int dcn_get_math(dcn_handle* h, int* math);
 
+/* ---- forward schedule ----------------------------------------------------------- */
+/* How the fp32 forward (deform_conv.py:41-80) runs after the offset conv.
+ * DCN_FWD_FUSED: the fused kernel (bilinear im2col gathered straight into the f32 MFMA
+ * GEMM's LDS tiles, bias in the epilogue; the columns are still written for the backward)
+ * wherever it applies: DCN_F32, deform_groups 1, kh*kw <= 9, C % 32 == 0, O % 128 == 0,
+ * native math; otherwise the unfused schedule. DCN_FWD_UNFUSED: K1 im2col, then the
+ * vendor GEMM, then the bias. DCN_FWD_AUTO (default): the schedule measured faster for the
+ * geometry. Same results to fp32 rounding (the columns bit for bit). */
+typedef enum { DCN_FWD_AUTO = 0, DCN_FWD_UNFUSED = 1, DCN_FWD_FUSED = 2 } dcn_fwd_path;
+int dcn_set_fwd_path(dcn_handle* h, int path);
+
 /* ---- testing ------------------------------------------------------------------ */
 /* One fp32 GEMM through the handle's engine under its current math mode, BLAS
  * column-major convention: C(m×n) = op(A)·op(B), batched by element strides. */

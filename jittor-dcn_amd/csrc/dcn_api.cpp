@@ -175,6 +175,7 @@ struct dcn_handle {
   static constexpr int kChunkEvents = 8;
   hipEvent_t chunk_ev[kChunkEvents] = {};
   dcn::GemmEngine* gemm = nullptr;
+  int fwd_path = DCN_FWD_AUTO;  // dcn_set_fwd_path
   // handle-owned workspace (host-pointer API) and scratch (standalone kernel API)
   void* ws = nullptr;
   size_t ws_bytes = 0;
@@ -256,6 +257,15 @@ int core_forward(dcn_handle* h, const Geo& g, const float* x, const float* off, 
   if (!xT_ready) {
     ProfScope ps(h, DCN_K_XPOSE);
     HIP_TRY(dcn::launch_nchw_to_nhwc(x, xT, g.B, g.C, g.HWi, h->stream));
+  }
+  const bool want_fused =
+      h->fwd_path == DCN_FWD_FUSED || (h->fwd_path == DCN_FWD_AUTO && dcn::fused_fwd_pays(g));
+  if (want_fused && dcn::fused_fwd_ok(g) && !use_split(h, g) && !dcn::get_force_generic()) {
+    // f2: im2col gathered into the GEMM's LDS tiles, bias in the epilogue; the columns are
+    // still written for the ∂W GEMM of the backward (DCN_BWD_COL_IN_WS)
+    ProfScope ps(h, DCN_K_GEMM_FWD);
+    HIP_TRY(dcn::launch_fused_fwd(g, xT, off, w, has_bias ? b : nullptr, out, colT, h->stream));
+    return DCN_OK;
   }
   {
     ProfScope ps(h, DCN_K_IM2COL);
@@ -1110,6 +1120,14 @@ int dcn_set_math(dcn_handle* h, int math) {
       math != DCN_MATH_F32_BF16X9)
     return fail(DCN_ERR_INVALID, "dcn_set_math: unknown mode " + std::to_string(math));
   dcn::gemm_set_math(h->gemm, math);
+  return DCN_OK;
+}
+
+int dcn_set_fwd_path(dcn_handle* h, int path) {
+  if (!h) return fail(DCN_ERR_INVALID, "dcn_set_fwd_path: null handle");
+  if (path != DCN_FWD_AUTO && path != DCN_FWD_UNFUSED && path != DCN_FWD_FUSED)
+    return fail(DCN_ERR_INVALID, "dcn_set_fwd_path: unknown path " + std::to_string(path));
+  h->fwd_path = path;
   return DCN_OK;
 }
 

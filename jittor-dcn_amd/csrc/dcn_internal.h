@@ -61,6 +61,12 @@ hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, co
                                void* bins_ws, int b0, int nb, bool bins_ready, hipStream_t s,
                                int bins_nb = 0);
 bool col2im_chunkable(const Geo& g);
+// dcn_fused.hip (f2): im2col gathered into the forward GEMM's LDS tiles, bias in the
+// epilogue; still writes colT (for the ∂W GEMM) when colT != NULL.
+bool fused_fwd_ok(const Geo& g);
+bool fused_fwd_pays(const Geo& g);  // DCN_FWD_AUTO picks the fused kernel
+hipError_t launch_fused_fwd(const Geo& g, const float* xT, const float* off, const float* Wf,
+                            const float* bias, float* out, float* colT, hipStream_t s);
 // dcn_offset_conv.hip:
 // wt / wt2: scratch of offset_conv_wt_floats(g) floats (transposed w_off copies).
 size_t offset_conv_wt_floats(const Geo& g);

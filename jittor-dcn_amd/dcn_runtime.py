@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("DCN_LIB", os.path.join(HERE, "lib", "libdcn.so"))
 
 DCN_F32, DCN_BF16 = 0, 1
 DCN_BWD_COL_IN_WS = 1
+DCN_FWD_AUTO, DCN_FWD_UNFUSED, DCN_FWD_FUSED = 0, 1, 2
 DCN_MATH_F32, DCN_MATH_F32_BF16X3, DCN_MATH_F32_BF16X6, DCN_MATH_F32_BF16X9 = 0, 3, 6, 9
 KERNEL_IDS = {
     "offset_fwd": 0, "im2col": 1, "gemm_fwd": 2, "bias_fwd": 3, "bwd_bias": 4,
@@ -80,6 +81,7 @@ SIGNATURES = {
     "dcn_debug_force_generic": [ctypes.c_int],
     "dcn_set_math": [_vp, ctypes.c_int],
     "dcn_get_math": [_vp, _ip],
+    "dcn_set_fwd_path": [_vp, ctypes.c_int],
     "dcn_debug_gemm": [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                        _vp, ctypes.c_int, ctypes.c_long, _vp, ctypes.c_int, ctypes.c_long, _vp,
                        ctypes.c_int, ctypes.c_long, ctypes.c_int],
@@ -215,6 +217,10 @@ class Handle:
     def set_math(self, math: int):
         """0 native f32 MFMA; 3 / 6 / 9 split-bf16 products (DCN_MATH_F32_BF16X*)."""
         check(self.lib.dcn_set_math(self.h, int(math)), "dcn_set_math")
+
+    def set_fwd_path(self, path: int):
+        """0 DCN_FWD_AUTO (measured-faster schedule), 1 DCN_FWD_UNFUSED, 2 DCN_FWD_FUSED."""
+        check(self.lib.dcn_set_fwd_path(self.h, int(path)), "dcn_set_fwd_path")
 
     def get_math(self) -> int:
         m = ctypes.c_int()
