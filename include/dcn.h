@@ -267,6 +267,9 @@ int dcn_debug_gemm(dcn_handle* h, int ta, int tb, int m, int n, int k, const flo
 /* 1 = route K1/K5 through the generic global-gather kernels (independent
  * implementation used by the parity tests to cross-check the LDS-window ones). */
 int dcn_debug_force_generic(int on);
+/* Workgroup count of the fused forward's persistent grid (DCN_FWD_FUSED); 0 = one per CU.
+ * Lets the parity tests walk many tiles (straddling images) through one workgroup. */
+int dcn_debug_fused_workgroups(int n);
 
 #ifdef __cplusplus
 }

@@ -189,19 +189,19 @@ struct dcn_handle {
 
 namespace dcn {
 int exp_flag(int i) {
-  static int v[8] = {0};
+  static int v[16] = {0};
   static bool init = false;
   if (!init) {
     init = true;
     if (const char* e = std::getenv("DCN_EXP")) {
-      for (int k = 0; k < 8 && *e; ++k) {
+      for (int k = 0; k < 16 && *e; ++k) {
         v[k] = std::atoi(e);
         while (*e && *e != ',') ++e;
         if (*e == ',') ++e;
       }
     }
   }
-  return (i >= 0 && i < 8) ? v[i] : 0;
+  return (i >= 0 && i < 16) ? v[i] : 0;
 }
 }  // namespace dcn
 
@@ -1111,6 +1111,12 @@ __attribute__((visibility("hidden"))) int dcn_internal_bind(dcn_handle* h, void*
 // Test hook: force the generic global-memory im2col/col2im kernels.
 int dcn_debug_force_generic(int on) {
   dcn::set_force_generic(on);
+  return DCN_OK;
+}
+
+int dcn_debug_fused_workgroups(int n) {
+  if (n < 0) return fail(DCN_ERR_INVALID, "dcn_debug_fused_workgroups: negative count");
+  dcn::set_fused_workgroups(n);
   return DCN_OK;
 }
 

@@ -65,6 +65,7 @@ bool col2im_chunkable(const Geo& g);
 // epilogue; still writes colT (for the ∂W GEMM) when colT != NULL.
 bool fused_fwd_ok(const Geo& g);
 bool fused_fwd_pays(const Geo& g);  // DCN_FWD_AUTO picks the fused kernel
+void set_fused_workgroups(int n);    // test hook (dcn_debug_fused_workgroups)
 hipError_t launch_fused_fwd(const Geo& g, const float* xT, const float* off, const float* Wf,
                             const float* bias, float* out, float* colT, hipStream_t s);
 // dcn_offset_conv.hip:
@@ -163,7 +164,7 @@ hipError_t launch_gemm_split(int math, const GemmSpec& s, const float* A, const 
 // Selection of the im2col / col2im implementation (tests force the generic
 // global-memory kernels to cross-check the channels-last ones).
 void set_force_generic(int on);
-// Development A/B knobs for speed experiments: DCN_EXP="a,b,..." -> exp_flag(i), 0 when
+// Development A/B knobs for speed experiments: DCN_EXP="a,b,..." (16 slots) -> exp_flag(i), 0 when
 // unset. Never changes results, only which of several equivalent kernels runs.
 int exp_flag(int i);
 int get_force_generic();

@@ -82,6 +82,7 @@ SIGNATURES = {
     "dcn_set_math": [_vp, ctypes.c_int],
     "dcn_get_math": [_vp, _ip],
     "dcn_set_fwd_path": [_vp, ctypes.c_int],
+    "dcn_debug_fused_workgroups": [ctypes.c_int],
     "dcn_debug_gemm": [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                        _vp, ctypes.c_int, ctypes.c_long, _vp, ctypes.c_int, ctypes.c_long, _vp,
                        ctypes.c_int, ctypes.c_long, ctypes.c_int],

@@ -56,9 +56,30 @@ def test_fused_forward_vs_unfused(gpu_handle, case):
         np.testing.assert_array_equal(g_f[k], g_u[k], err_msg=f"∂{k} (columns differ)")
 
 
+@pytest.mark.parametrize("nwg", [1, 3, 7])
+def test_fused_few_workgroups_walk_tiles(gpu_handle, nwg):
+    """A persistent workgroup walks many 128-px tiles, some straddling two images, and a
+    ragged last block (B·Ho·Wo = 3·13·15 = 585 pixels = 18.3 blocks)."""
+    c = _rand_case(88 + nwg, B=3, C=64, O_=256, H=13, W=15, off_scale=2.0)
+    rt.check(gpu_handle.lib.dcn_debug_fused_workgroups(nwg))
+    try:
+        out_f, off_f, g_f = _run(gpu_handle, c, rt.DCN_FWD_FUSED)
+    finally:
+        rt.check(gpu_handle.lib.dcn_debug_fused_workgroups(0))
+    out_u, off_u, g_u = _run(gpu_handle, c, rt.DCN_FWD_UNFUSED)
+    scale = np.abs(out_u).max()
+    assert np.abs(out_f - out_u).max() <= 1e-5 * scale, f"fused nwg={nwg} vs unfused out"
+    for k in g_u:
+        np.testing.assert_array_equal(g_f[k], g_u[k], err_msg=f"nwg={nwg} ∂{k}")
+    ro, roff, rg = _oracle(c, off_f)
+    _check(out_f, off_f, g_f, ro, roff, rg, True, f"fused nwg={nwg}")
+
+
 def test_fused_path_rejects_unknown_mode(gpu_handle):
     with pytest.raises(RuntimeError):
         gpu_handle.set_fwd_path(7)
+    with pytest.raises(RuntimeError):
+        rt.check(gpu_handle.lib.dcn_debug_fused_workgroups(-1))
 
 
 def test_fused_config3_tile_vs_oracle(gpu_handle):
