@@ -21,7 +21,7 @@ def per_kernel(path, counter):
             name = r["Kernel_Name"]
             if not name.startswith(("dcn::", "void dcn::", "Cijk", "void ")):
                 continue
-            short = name.replace("void ", "").split("(")[0]
+            short = name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
             acc[short].append(float(r["Counter_Value"]) * 1024.0)
     return {k: sum(v) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}
 

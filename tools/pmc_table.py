@@ -14,7 +14,7 @@ acc = defaultdict(lambda: defaultdict(list))
 for d in args:
     with open(d + "/run_counter_collection.csv") as f:
         for r in csv.DictReader(f):
-            k = r["Kernel_Name"].replace("void ", "").split("(")[0]
+            k = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
             if match in k:
                 acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, cs in acc.items():
