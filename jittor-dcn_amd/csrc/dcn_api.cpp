@@ -298,6 +298,17 @@ int core_forward(dcn_handle* h, const Geo& g, const float* x, const float* off, 
 }
 
 // The offset-conv backward, when core_backward runs it interleaved with col2im.
+// ∂W as dwg grouped NT GEMMs over B/dwg images each, or one NN GEMM per image (0). r01
+// (tools/dw_ab.sh): bf16 config 4 ∂W 0.178 ms per image -> 0.130 ms in 16 groups (step 1.10 ->
+// 1.02 ms); fp32 config 3 unchanged at 1.65 ms, so fp32 stays per image. DCN_EXP slot 9
+// overrides: n > 0 groups, n < 0 per image.
+int dw_groups(const Geo& g) {
+  const int n = dcn::exp_flag(9);
+  if (n < 0) return 0;
+  if (n > 0) return (n < g.B && g.B % n == 0) ? n : 0;
+  return (g.dt == DCN_BF16 && g.B > 16 && g.B % 16 == 0) ? 16 : 0;
+}
+
 struct OffsetBwd {
   const float* w_off;
   float *gw_off, *gb_off, *goffT, *wt2;
@@ -338,7 +349,21 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
     // (config 5: HW = 49) the flat NT GEMM over k = B·HW against ∂outT wins instead.
     ProfScope ps(h, DCN_K_GEMM_DW);
     dcn::GemmSpec sp;
-    if (flat_dw) {
+    const int dwg = dw_groups(g);
+    if (flat && dwg > 0) {
+      // grouped NT: P_g(K×O) = colT_g · ∂outT_g over the pixels of B/dwg images, then the
+      // fixed-order Σ_g (dwg partials instead of B)
+      const int pg = (g.B / dwg) * g.HW;
+      sp.tb = true;
+      sp.m = g.K; sp.n = g.O; sp.k = pg;
+      sp.lda = g.K; sp.sa = (long)g.K * pg;
+      sp.ldb = g.O; sp.sb = (long)g.O * pg;
+      sp.ldc = g.K; sp.sc = (long)g.K * g.O;
+      sp.batch = dwg;
+      GEMM_TRY(h, sp, colT, goutT, parts);
+      DCN_TRY(fork_aux(h));
+      HIP_TRY(dcn::launch_sum_partials(parts, dwg, (size_t)g.K * g.O, gw, h->aux));
+    } else if (flat_dw) {
       sp.tb = true;
       sp.m = g.K; sp.n = g.O; sp.k = g.B * g.HW;
       sp.lda = g.K; sp.ldb = g.O; sp.ldc = g.K;
@@ -501,23 +526,39 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
     HIP_TRY(dcn::launch_bias_grad(g, gout32, F32(L.gb32), st));
     HIP_TRY(dcn::launch_f32_to_bf16(F32(L.gb32), gb, (size_t)g.O, st));
   }
+  bf16_t* goutT = BF(L.goutT);
+  const int dwg = dw_groups(g);
   {
-    ProfScope ps(h, DCN_K_GEMM_DW);  // P_b(K×O) = colT_b · ∂out_b (NN), bf16 in, fp32 out
+    ProfScope ps(h, DCN_K_GEMM_DW);
     dcn::GemmSpec sp;
-    sp.m = g.K; sp.n = g.O; sp.k = g.HW;
-    sp.lda = g.K; sp.sa = (long)g.K * g.HW;
-    sp.ldb = g.HW; sp.sb = (long)g.O * g.HW;
-    sp.ldc = g.K; sp.sc = (long)g.K * g.O;
-    sp.batch = g.B;
     sp.bf16_ab = true;
-    GEMM_TRY(h, sp, col, gout, F32(L.parts));
-    HIP_TRY(dcn::launch_sum_partials(F32(L.parts), g.B, (size_t)g.K * g.O, F32(L.gw32), st));
+    int nparts = g.B;
+    if (dwg > 0) {
+      // grouped NT over the pixels of B/dwg images (∂outT first, shared with ∂col)
+      HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(gout, goutT, g.B, g.O, g.HW, st));
+      const int pg = (g.B / dwg) * g.HW;
+      sp.tb = true;
+      sp.m = g.K; sp.n = g.O; sp.k = pg;
+      sp.lda = g.K; sp.sa = (long)g.K * pg;
+      sp.ldb = g.O; sp.sb = (long)g.O * pg;
+      sp.ldc = g.K; sp.sc = (long)g.K * g.O;
+      sp.batch = dwg;
+      GEMM_TRY(h, sp, col, goutT, F32(L.parts));
+      nparts = dwg;
+    } else {  // P_b(K×O) = colT_b · ∂out_b (NN), bf16 in, fp32 out
+      sp.m = g.K; sp.n = g.O; sp.k = g.HW;
+      sp.lda = g.K; sp.sa = (long)g.K * g.HW;
+      sp.ldb = g.HW; sp.sb = (long)g.O * g.HW;
+      sp.ldc = g.K; sp.sc = (long)g.K * g.O;
+      sp.batch = g.B;
+      GEMM_TRY(h, sp, col, gout, F32(L.parts));
+    }
+    HIP_TRY(dcn::launch_sum_partials(F32(L.parts), nparts, (size_t)g.K * g.O, F32(L.gw32), st));
     HIP_TRY(dcn::launch_f32_to_bf16(F32(L.gw32), gw, (size_t)g.O * g.K, st));
   }
   {
     ProfScope ps(h, DCN_K_GEMM_DCOL);  // ∂colT = ∂outT · Wf, one flat GEMM, bf16 out
-    bf16_t* goutT = BF(L.goutT);
-    HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(gout, goutT, g.B, g.O, g.HW, st));
+    if (dwg <= 0) HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(gout, goutT, g.B, g.O, g.HW, st));
     dcn::GemmSpec sp;
     sp.m = g.K; sp.n = g.B * g.HW; sp.k = g.O;
     sp.lda = g.K; sp.ldb = g.O; sp.ldc = g.K;
