@@ -123,6 +123,9 @@ def test_bf16_forward_backward_vs_oracle(gpu_handle, case):
     out, off, g = _device(gpu_handle, bits, s)
     _, roff, _ = O.forward(v["x"], v["w_off"], v["b_off"], v["w"], v["b"], s, (1, 1))
     assert rel_err(off, roff) <= BF16_TOL, "offsets"
+    # the offset conv's products are exact (bf16 inputs) and summed in fp32, so the only
+    # visible error is the final rounding of the offsets to bf16 (half an ulp, 2^-9)
+    assert np.all(np.abs(off - roff) <= 2.0 ** -8 * np.abs(roff) + 1e-6), "offsets past 1 ulp"
     ro, _, cache = O.forward(v["x"], v["w_off"], v["b_off"], v["w"], v["b"], s, (1, 1),
                              offsets=off)  # condition on the device's bf16 offsets
     rg = O.backward(cache, v["grad_out"])
