@@ -324,6 +324,8 @@ def main():
                 "avg_launch_ms": k1_ms,
             },
             "kernel_ms": kernel_ms,
+            "rooflines_other": other_rooflines(kernel_ms, B, C, O_, H, W, N, Ho, Wo, J, bf16,
+                                               fwd_only),
             "alt": alt,
             "cpu_baseline": None,
         }
@@ -335,6 +337,33 @@ def main():
     h.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def other_rooflines(kernel_ms, B, C, O_, H, W, N, Ho, Wo, J, bf16, fwd_only):
+    """The other hot kernels against their bound (SURVEY §8(d) algorithmic work / the
+    HIP-event scope time of the same profiled pass): the three GEMMs on the MFMA peak of
+    their operand type, K5 (col2im, fp32) on HBM. Scope times include each GEMM's small
+    companion launches (Σ_b partials, transposes), so these fractions are lower bounds."""
+    M, K = B * Ho * Wo, N * C
+    gemm_flop = 2.0 * M * K * O_
+    peak_tf = 2500.0 if bf16 else 157.3  # dense bf16 / f32 MFMA (MI355X_MICROARCH.md)
+    out = []
+    for name in ("gemm_fwd",) + (() if fwd_only else ("gemm_dw", "gemm_dcol")):
+        ms = kernel_ms.get(name)
+        if ms:
+            tf = gemm_flop / (ms * 1e-3) / 1e12
+            out.append({"kernel": name, "bound": "mfma", "achieved": round(tf, 1),
+                        "peak": peak_tf, "unit": "TFLOP/s", "frac": round(tf / peak_tf, 4),
+                        "algorithmic_flop": gemm_flop, "avg_launch_ms": ms})
+    ms = kernel_ms.get("col2im")
+    if ms and not bf16 and not fwd_only:
+        k5_b = 4 * (M * K + 2 * B * C * H * W + 2 * B * J * Ho * Wo)
+        gbs = k5_b / (ms * 1e-3) / 1e9
+        out.append({"kernel": "col2im (K5: ∂x and ∂offset from ∂col)", "bound": "hbm",
+                    "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes": k5_b,
+                    "avg_launch_ms": ms})
+    return out
 
 
 if __name__ == "__main__":
