@@ -61,6 +61,10 @@ def dcn_forward_numpy(x, w_off, b_off, w, b, stride, padding, handle=None):
     O, Cw, kh, kw = w.shape
     if Cw != C:
         raise ValueError(f"input has {C} channels, weight expects {Cw}")
+    if B == 0:  # empty batch: empty outputs, as the reference's ops give (no launch)
+        Ho, Wo = rt.out_shape(rt.make_desc(1, C, H, W, O, (kh, kw), stride, padding))
+        return (np.empty((0, O, Ho, Wo), np.float32),
+                np.empty((0, w_off.shape[0], Ho, Wo), np.float32))
     desc = rt.make_desc(B, C, H, W, O, (kh, kw), stride, padding, bias=b is not None)
     Ho, Wo = rt.out_shape(desc)
     out = np.empty((B, O, Ho, Wo), np.float32)
@@ -76,6 +80,14 @@ def dcn_backward_numpy(x, off, w_off, w, has_bias, grad_out, stride, padding, ha
     x, off, w_off, w, grad_out = map(_f32, (x, off, w_off, w, grad_out))
     B, C, H, W = x.shape
     O, _, kh, kw = w.shape
+    if B == 0:  # empty batch: nothing sampled, every parameter gradient is zero
+        g = {"x": np.empty_like(x), "weight": np.zeros_like(w),
+             "offset_conv.weight": np.zeros_like(w_off),
+             "offset_conv.bias": np.zeros(w_off.shape[0], np.float32),
+             "offset": np.empty_like(off)}
+        if has_bias:
+            g["bias"] = np.zeros(O, np.float32)
+        return g
     desc = rt.make_desc(B, C, H, W, O, (kh, kw), stride, padding, bias=has_bias)
     g = {"x": np.empty_like(x), "weight": np.empty_like(w),
          "offset_conv.weight": np.empty_like(w_off),

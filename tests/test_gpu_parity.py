@@ -289,6 +289,24 @@ def test_module_numpy_backend_on_gpu():
     np.testing.assert_array_equal(out, out2)
 
 
+def test_empty_batch_host_api(gpu_handle):
+    """An empty batch gives empty outputs / ∂x / ∂offset and zero parameter gradients, as
+    the reference's ops do, without a launch (the handle is still required)."""
+    rng = np.random.default_rng(7)
+    x = np.zeros((0, 8, 9, 11), np.float32)
+    wo = rng.standard_normal((18, 8, 3, 3)).astype(np.float32)
+    bo = np.zeros(18, np.float32)
+    w = rng.standard_normal((16, 8, 3, 3)).astype(np.float32)
+    b = np.zeros(16, np.float32)
+    out, off = dcn_forward_numpy(x, wo, bo, w, b, (2, 2), (1, 1), handle=gpu_handle)
+    assert out.shape == (0, 16, 5, 6) and off.shape == (0, 18, 5, 6)
+    g = dcn_backward_numpy(x, off, wo, w, True, np.zeros((0, 16, 5, 6), np.float32), (2, 2),
+                           (1, 1), handle=gpu_handle)
+    assert g["x"].shape == x.shape and g["offset"].shape == off.shape
+    for k in ("weight", "bias", "offset_conv.weight", "offset_conv.bias"):
+        assert not np.any(g[k]), k
+
+
 def test_config3_full_size_properties(gpu_handle):
     """BASELINE config 3 (B=64, C=O=256, 56², k3 s1 p1) at full size: spot-check two
     images' per-image outputs/grads against the C oracle (fp32) and ∂W by linearity
