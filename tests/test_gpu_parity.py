@@ -186,6 +186,7 @@ def test_all_samples_out_of_image(gpu_handle):
     (100, 21, 19, (1, 1), 2.5),   # partial 64-channel LDS slice, ragged 8x8 tiles
     (68, 23, 25, (2, 2), 1.5),    # stride 2: window scale (H-1)/(Wo-1) ~ 2
     (8, 17, 17, (1, 1), 6.0),     # most samples leave the staged window (global path)
+    (256, 15, 13, (1, 1), 3.0),   # whole 1-KiB rows (config-3 channel count), ragged tiles
 ])
 def test_channels_last_kernels_match_generic_kernels(gpu_handle, C, H, W, s, off_scale):
     """The channels-last K1/K5 (LDS-staged window + global fallback, lane maps, sample
