@@ -112,12 +112,22 @@ def _device(h, bits, s):
         D.free()
 
 
+def _bf16_sweep(i):
+    """Seeded random bf16 geometries (3x3, pad 1, stride 1-2): every channel instantiation."""
+    rng = np.random.default_rng(500 + i)
+    C = (4, 20, 48, 96, 160, 256)[i]
+    return dict(seed=600 + i, B=int(rng.integers(1, 4)), C=C, O_=int(rng.choice([8, 64, 256])),
+                H=int(rng.integers(6, 22)), W=int(rng.integers(6, 22)),
+                s=(int(rng.integers(1, 3)), int(rng.integers(1, 3))),
+                off_scale=float(rng.choice([1.0, 2.5])))
+
+
 @pytest.mark.parametrize("case", [
     dict(seed=1, B=2, C=64, O_=32, H=20, W=20),
     dict(seed=2, B=3, C=32, O_=16, H=17, W=15, s=(2, 2)),
     dict(seed=3, B=1, C=256, O_=64, H=14, W=14, off_scale=2.0),
     dict(seed=4, B=2, C=12, O_=8, H=11, W=13),
-])
+] + [_bf16_sweep(i) for i in range(6)])
 def test_bf16_forward_backward_vs_oracle(gpu_handle, case):
     bits, v, s = _case(**case)
     out, off, g = _device(gpu_handle, bits, s)
