@@ -88,6 +88,53 @@ def cpu_baseline(cfg, budget_s=10.0, threads=None, name="config3"):
                       f"oracle/dcn_ref.c fp32 OpenMP, {el:.1f} s on {threads} of {ncpu} host threads"}
 
 
+def cpu_baseline_framework(cfg, budget_s=10.0, threads=None, name="config3"):
+    """The reference-style CPU path beside the C port: oracle/torch_ref.literal_dcn, the
+    reference's own op sequence (conv, grid, x.repeat + grid_sample, permutes, matmul) on
+    torch-CPU in fp32, autograd for the backward; whole images until ~budget_s. Jittor
+    itself is not installable here. None where the restatement does not
+    apply (dilation / deform groups)."""
+    if cfg.get("dil", 1) != 1 or cfg.get("G", 1) != 1:
+        return None
+    import torch
+    from torch_ref import literal_dcn
+    ncpu = os.cpu_count() or 1
+    threads = threads or min(16, ncpu)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        g = torch.Generator().manual_seed(0)
+        C, O_, H, W, k = cfg["C"], cfg["O"], cfg["H"], cfg["W"], cfg["k"]
+        N, st, pd = k * k, (cfg["s"],) * 2, (cfg["p"],) * 2
+        fwd_only = cfg.get("fwd_only", False)
+        x = torch.randn(1, C, H, W, generator=g, requires_grad=not fwd_only)
+        wo = (torch.randn(2 * N, C, k, k, generator=g) / float(np.sqrt(C * N))).requires_grad_()
+        bo = (torch.rand(2 * N, generator=g) - 0.5).requires_grad_()
+        w = (torch.randn(O_, C, k, k, generator=g) * float(np.sqrt(2 / (C * N)))).requires_grad_()
+        b = (torch.randn(O_, generator=g) * 0.1).requires_grad_()
+        n_img, t0 = 0, time.perf_counter()
+        while True:
+            if fwd_only:
+                with torch.no_grad():
+                    out, _ = literal_dcn(x, wo, bo, w, b, st, pd)
+            else:
+                out, _ = literal_dcn(x, wo, bo, w, b, st, pd)
+                out.backward(torch.ones_like(out))
+            n_img += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s or n_img >= 1024:
+                break
+        Ho, Wo = out.shape[2], out.shape[3]
+    finally:
+        torch.set_num_threads(prev)
+    return {"value": n_img * Ho * Wo * N / el / 1e9, "unit": "Gsamples/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{n_img} {name} image(s) (1x{C}x{H}x{W} -> {O_}, k{k}) "
+                      f"{'fwd' if fwd_only else 'fwd+bwd'}, oracle/torch_ref.py (the reference's "
+                      f"op sequence, torch-CPU fp32 + autograd), {el:.1f} s on {threads} of "
+                      f"{ncpu} host threads"}
+
+
 K1_KERNEL = "dcn::im2col_lds"  # K1 on the channels-last path (deform_groups 1, C % 4 == 0)
 
 
@@ -328,9 +375,15 @@ def main():
                                                fwd_only),
             "alt": alt,
             "cpu_baseline": None,
+            "cpu_baseline_other": None,
         }
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_budget, name=f"config{args.config}")
+            # the stronger of the two CPU restatements is the reported baseline: the
+            # reference's own op sequence on torch-CPU; the C/OpenMP port rides beside it
+            fw = cpu_baseline_framework(cfg, args.cpu_budget, name=f"config{args.config}")
+            cport = cpu_baseline(cfg, args.cpu_budget, name=f"config{args.config}")
+            res["cpu_baseline"] = fw if fw and fw["value"] >= cport["value"] else cport
+            res["cpu_baseline_other"] = cport if res["cpu_baseline"] is fw else fw
         print(json.dumps(res), flush=True)
     if comm is not None:
         comm.close()
