@@ -37,6 +37,8 @@ CONFIGS = {
     3: dict(B=64, C=256, O=256, H=56, W=56, k=3, s=1, p=1, dtype="f32"),
     # configs[3] (config 4): N=512 batch-sharded over 8 GPUs = 64 images per GPU, bf16
     4: dict(B=64, C=256, O=256, H=28, W=28, k=3, s=1, p=1, dtype="bf16"),
+    # configs[0] (config 1): the reference's own CPU-runnable plumbing case, fwd+bwd
+    1: dict(B=1, C=1, O=4, H=28, W=28, k=3, s=1, p=1, dtype="f32"),
     # configs[1] (config 2): forward only, vs the CPU path
     2: dict(B=8, C=64, O=128, H=56, W=56, k=3, s=1, p=1, dtype="f32", fwd_only=True),
     # configs[4] (config 5): the DCNv1 option set (extension: dilation 2, 4 deform groups;
