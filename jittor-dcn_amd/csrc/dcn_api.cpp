@@ -335,7 +335,13 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
   {
     // ∂outT (for the flat GEMMs) and ∂b from one pass over ∂out
     ProfScope ps(h, DCN_K_BWD_BIAS);
-    if (flat && has_bias)
+    if (flat && has_bias &&
+        dcn::xpose_chsum_floats(g.B, g.O, g.HW) <= (size_t)g.B * g.HWi * g.C)
+      // tile sums in gxT (written only by K5, after the join), the fold on the side stream
+      // beside the ∂W GEMM (it only feeds ∂b)
+      HIP_TRY(dcn::launch_xpose_chsum(gout, goutT, gxT, gb, g.B, g.O, g.HW, h->stream, h->aux,
+                                      h->fork_ev));
+    else if (flat && has_bias)
       HIP_TRY(dcn::launch_xpose_chsum(gout, goutT, parts, gb, g.B, g.O, g.HW, h->stream));
     else if (flat)
       HIP_TRY(dcn::launch_nchw_to_nhwc(gout, goutT, g.B, g.O, g.HW, h->stream));

@@ -108,8 +108,11 @@ void launch_channel_sum(const float* in, int B, int Cn, int HW, float* out, hipS
 // in[b][c][p] -> out[b][p][c] and chsum[c] = Σ_{b,p} in[b][c][p] (deterministic); tsum is
 // scratch of xpose_chsum_floats(B, C, P) floats.
 size_t xpose_chsum_floats(int B, int C, int P);
+// ∂out -> ∂outT with ∂b; the per-channel fold of the tile sums runs on s_sum (after event ev)
+// when given, so tsum must then stay untouched until s_sum is joined.
 hipError_t launch_xpose_chsum(const float* in, float* out, float* tsum, float* chsum, int B,
-                              int C, int P, hipStream_t s);
+                              int C, int P, hipStream_t s, hipStream_t s_sum = nullptr,
+                              hipEvent_t ev = nullptr);
 hipError_t launch_bias_add(const Geo& g, float* out, const float* bias, int b0, int nb,
                            hipStream_t s);
 hipError_t launch_bias_grad(const Geo& g, const float* gout, float* gb, hipStream_t s);

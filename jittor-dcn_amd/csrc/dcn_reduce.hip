@@ -246,9 +246,16 @@ static int xpose_blocks_x(int P) { return (P + 64 * kXpSub - 1) / (64 * kXpSub);
 size_t xpose_chsum_floats(int B, int C, int P) { return (size_t)B * xpose_blocks_x(P) * C; }
 
 hipError_t launch_xpose_chsum(const float* in, float* out, float* tsum, float* chsum, int B,
-                              int C, int P, hipStream_t s) {
+                              int C, int P, hipStream_t s, hipStream_t s_sum,
+                              hipEvent_t ev) {
   dim3 grid(xpose_blocks_x(P), (C + 63) / 64, B);
   hipLaunchKernelGGL(xpose_chsum, grid, dim3(256), 0, s, in, out, tsum, C, P);
+  if (s_sum && s_sum != s) {  // the fold only feeds ∂b: off the main stream's critical path
+    hipError_t e = hipEventRecord(ev, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s_sum, ev, 0);
+    if (e != hipSuccess) return e;
+    s = s_sum;
+  }
   hipLaunchKernelGGL(tile_sum_to_channels, dim3(C), dim3(64), 0, s, tsum, B * xpose_blocks_x(P), C,
                      chsum);
   return hipGetLastError();
