@@ -1,0 +1,54 @@
+"""CPU: bench.py's measurement arithmetic (no GPU). The algorithmic bytes and FLOPs the
+roofline fractions divide by must be SURVEY §8(d)'s figures, and every BASELINE config must
+be a bench workload."""
+import importlib.util
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def bench():
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_k1_algorithmic_bytes_match_survey(bench):
+    # config 3 K1 = 2,069,659,648 B (1,145.8 B/sample); config 4 bf16 with
+    # bf16 offsets = 258,707,456 B
+    assert bench.k1_bytes(64, 256, 56, 56, 9, 56, 56) == 2_069_659_648
+    assert bench.k1_bytes(64, 256, 28, 28, 9, 28, 28, elem=2) == 258_707_456
+    assert round(bench.k1_bytes(64, 256, 56, 56, 9, 56, 56) / (64 * 56 * 56 * 9), 1) == 1145.8
+
+
+def test_other_rooflines_use_survey_work(bench):
+    km = {"gemm_fwd": 1.5, "gemm_dw": 1.5, "gemm_dcol": 1.5, "col2im": 0.5}
+    r = {e["kernel"].split(" ")[0]: e for e in
+         bench.other_rooflines(km, 64, 256, 256, 56, 56, 9, 56, 56, 18, False, False)}
+    # 2·M·K·O = 236,760,072,192 FLOP per GEMM at config 3
+    assert r["gemm_fwd"]["algorithmic_flop"] == 236_760_072_192
+    assert r["gemm_fwd"]["peak"] == 157.3 and r["gemm_fwd"]["unit"] == "TFLOP/s"
+    assert abs(r["gemm_fwd"]["achieved"] - 236.76 / 1.5) < 0.1
+    # K5 = 4·(M·K + 2·B·C·Hi·Wi + 2·B·2N·Ho·Wo) = 2,289,631,232 B
+    assert r["col2im"]["algorithmic_bytes"] == 2_289_631_232
+    assert r["col2im"]["bound"] == "hbm"
+    # forward-only configs report the forward GEMM alone; bf16 prices against the bf16 peak
+    fo = bench.other_rooflines(km, 8, 64, 128, 56, 56, 9, 56, 56, 18, False, True)
+    assert [e["kernel"] for e in fo] == ["gemm_fwd"]
+    b16 = bench.other_rooflines(km, 64, 256, 256, 28, 28, 9, 28, 28, 18, True, False)
+    assert all(e["peak"] == 2500.0 for e in b16 if e["bound"] == "mfma")
+
+
+def test_every_baseline_config_is_a_workload(bench):
+    # BASELINE.json configs[0..4] = configs 1..5
+    assert sorted(bench.CONFIGS) == [1, 2, 3, 4, 5]
+    c3 = bench.CONFIGS[3]
+    assert (c3["B"], c3["C"], c3["O"], c3["H"], c3["W"], c3["k"], c3["dtype"]) == \
+        (64, 256, 256, 56, 56, 3, "f32")
+    assert bench.CONFIGS[4]["dtype"] == "bf16" and bench.CONFIGS[2].get("fwd_only")
+    c5 = bench.CONFIGS[5]
+    assert (c5["s"], c5["dil"], c5["G"]) == (2, 2, 4)
