@@ -86,3 +86,20 @@ def test_roi_pool_rejects_bad_batch_index(gpu_handle):
     rois[1, 0] = 2.0
     with pytest.raises(RuntimeError, match="batch index"):
         roi_pool_forward_numpy(feat, rois, offsets, (1, 1), handle=gpu_handle)
+
+
+@pytest.mark.parametrize("B,C,H,W,R", [(1, 3, 7, 5, 9), (3, 70, 16, 13, 17), (2, 300, 10, 12, 6),
+                                       (4, 64, 21, 9, 33), (1, 129, 5, 30, 8)])
+@pytest.mark.parametrize("kind,out_size", [("roi", (1, 1)), ("ps", (2, 2))])
+def test_roi_pool_shapes_vs_oracle(gpu_handle, B, C, H, W, R, kind, out_size):
+    """Feature-map and channel shapes beside the fixed cases: C below, between and above the
+    64-lane block (3, 70, 129, 300), tall/wide maps, more RoIs than the batch."""
+    P = out_size[0] * out_size[1]
+    if kind == "ps" and C < P:
+        pytest.skip("PS pooling needs C >= ph·pw channels (C // (ph·pw) output channels)")
+    feat, rois, offsets = roi_case(40 + C, B=B, C=C, H=H, W=W, R=R, P=P)
+    case = dict(kind=kind, output_size=out_size, spatial_scale=0.75)
+    out, ref, gf, rgf, go, rgo = _run(case, feat, rois, offsets, gpu_handle)
+    assert_close(out, ref, what="pooled")
+    assert_close(gf, rgf, what="∂features")
+    assert_close_reduction(go, rgo, what="∂offsets")
