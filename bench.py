@@ -182,6 +182,9 @@ def main():
     ap.add_argument("--fwd-path", type=int, default=0, choices=(0, 1, 2),
                     help="forward schedule (include/dcn.h dcn_fwd_path): 0 auto, 1 K1 + vendor "
                          "GEMM + bias, 2 fused im2col+GEMM where it applies")
+    ap.add_argument("--graph", type=int, default=0, choices=(0, 1),
+                    help="1: capture one step (libdcn launches on both of its streams, and the "
+                         "all-reduce) into a HIP graph after the warmup and time its replays")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (default: newest profiles/r*_pmc_hbm.json)")
@@ -271,11 +274,32 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    run = step
+    graph_note = None
+    if args.graph:
+        # one step captured on a side stream (libdcn bound to it, its own side stream joins
+        # through events); each replay is one full step of the same kernels
+        try:
+            gs = torch.cuda.Stream(dev)
+            gs.wait_stream(stream)
+            graph = torch.cuda.CUDAGraph()
+            h.set_stream(gs.cuda_stream)
+            with torch.cuda.graph(graph, stream=gs):
+                step()
+            h.set_stream(stream.cuda_stream)
+            run = graph.replay
+            run()
+            torch.cuda.synchronize(dev)
+            graph_note = "HIP graph replay of one captured step"
+        except Exception as e:  # capture unsupported: time the eager step instead
+            h.set_stream(stream.cuda_stream)
+            graph_note = f"graph capture failed ({type(e).__name__}: {e}); eager step timed"
+            torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        run()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -373,6 +397,7 @@ def main():
                 "avg_launch_ms": k1_ms,
             },
             "kernel_ms": kernel_ms,
+            "launch": graph_note or "eager (one launch per kernel)",
             "rooflines_other": other_rooflines(kernel_ms, B, C, O_, H, W, N, Ho, Wo, J, bf16,
                                                fwd_only),
             "alt": alt,
