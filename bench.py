@@ -54,13 +54,49 @@ def k1_bytes(B, C, H, W, N, Ho, Wo, elem=4, J=None):
     return elem * (B * C * H * W + B * J * Ho * Wo + B * Ho * Wo * N * C)
 
 
+def host_cpus():
+    """The host cores this process may run on: the scheduler affinity mask, capped by the
+    cgroup CPU quota when one is set (a GPU box shares its host; os.cpu_count() reports
+    the whole machine). Returns (threads to use, description dict)."""
+    ncpu = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = ncpu
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            txt = open(path).read().split()
+        except OSError:
+            continue
+        if path.endswith("cpu.max") and txt and txt[0] != "max":
+            quota = int(txt[0]) / int(txt[1])
+        elif path.endswith("cfs_quota_us") and txt and int(txt[0]) > 0:
+            period = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            quota = int(txt[0]) / period
+        break
+    threads = aff if quota is None else max(1, min(aff, int(quota + 0.999)))
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return threads, {"host_threads": ncpu, "affinity_threads": aff, "cgroup_cpu_quota": quota,
+                     "cpu_model": model}
+
+
 def cpu_baseline(cfg, budget_s=10.0, threads=None, name="config3"):
     """Time the fp32 C restatement (oracle/dcn_ref.c, 'port') on a bounded sample:
-    whole images of the configuration, fwd(+bwd), one at a time until ~budget_s."""
+    whole images of the configuration, fwd(+bwd), one at a time until ~budget_s, on every
+    host core this process may use (host_cpus)."""
     import ref_lib as R
     R.build()
     ncpu = os.cpu_count() or 1
-    threads = threads or min(16, ncpu)
+    auto, info = host_cpus()
+    threads = threads or auto
     R.set_threads(threads)
     rng = np.random.default_rng(0)
     C, O_, H, W, k = cfg["C"], cfg["O"], cfg["H"], cfg["W"], cfg["k"]
@@ -85,9 +121,13 @@ def cpu_baseline(cfg, budget_s=10.0, threads=None, name="config3"):
             break
     samples = n_img * Ho * Wo * N
     return {"value": samples / el / 1e9, "unit": "Gsamples/s", "cores": threads, "kind": "port",
+            **info,
             "sample": f"{n_img} {name} image(s) (1x{C}x{H}x{W} -> {O_}, k{k}) "
                       f"{'fwd' if fwd_only else 'fwd+bwd'}, "
-                      f"oracle/dcn_ref.c fp32 OpenMP, {el:.1f} s on {threads} of {ncpu} host threads"}
+                      f"oracle/dcn_ref.c fp32 OpenMP, {el:.1f} s on {threads} threads "
+                      f"({info['cpu_model']}; {ncpu} host threads, "
+                      f"{info['affinity_threads']} in this process's affinity mask, "
+                      f"cgroup quota {info['cgroup_cpu_quota']} CPUs)"}
 
 
 def cpu_baseline_framework(cfg, budget_s=10.0, threads=None, name="config3"):
@@ -101,7 +141,8 @@ def cpu_baseline_framework(cfg, budget_s=10.0, threads=None, name="config3"):
     import torch
     from torch_ref import literal_dcn
     ncpu = os.cpu_count() or 1
-    threads = threads or min(16, ncpu)
+    auto, info = host_cpus()
+    threads = threads or auto
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     try:
@@ -130,11 +171,13 @@ def cpu_baseline_framework(cfg, budget_s=10.0, threads=None, name="config3"):
     finally:
         torch.set_num_threads(prev)
     return {"value": n_img * Ho * Wo * N / el / 1e9, "unit": "Gsamples/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", **info,
             "sample": f"{n_img} {name} image(s) (1x{C}x{H}x{W} -> {O_}, k{k}) "
                       f"{'fwd' if fwd_only else 'fwd+bwd'}, oracle/torch_ref.py (the reference's "
-                      f"op sequence, torch-CPU fp32 + autograd), {el:.1f} s on {threads} of "
-                      f"{ncpu} host threads"}
+                      f"op sequence, torch-CPU fp32 + autograd), {el:.1f} s on {threads} threads "
+                      f"({info['cpu_model']}; {ncpu} host threads, "
+                      f"{info['affinity_threads']} in this process's affinity mask, "
+                      f"cgroup quota {info['cgroup_cpu_quota']} CPUs)"}
 
 
 K1_KERNEL = "dcn::im2col_lds"  # K1 on the channels-last path (deform_groups 1, C % 4 == 0)
@@ -188,7 +231,30 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (default: newest profiles/r*_pmc_hbm.json)")
+    ap.add_argument("--dry", action="store_true",
+                    help="launcher check without a GPU: ranks join a gloo group, sum their "
+                         "rank ids and rank 0 prints the world it saw (CPU tests)")
+    ap.add_argument("--exchange", action="store_true",
+                    help="run the gradient exchange even at N=1 (a 1-rank RCCL group), to "
+                         "exercise the overlapped all-reduce path on one GPU")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `bench.py --gpus N` with no external launcher: start the N ranks here, from a
+        # parent that never touches the GPU (no torch import), one process per GPU
+        sys.exit(spawn_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry:
+        return dry_run(world, rank)
+
+    # stdout carries exactly one JSON line: whatever the libraries print there (RCCL's
+    # version banner at communicator init, ...) goes to stderr instead
+    out_stream = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
 
     import torch  # plumbing: HBM buffers, stream handle, torch.distributed (RCCL)
     import torch.distributed as dist
@@ -196,14 +262,14 @@ def main():
     import dcn_dp
     import dcn_runtime as rt
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
+    exch = world > 1 or args.exchange  # gradient exchange in the step
+    if exch:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=dev)
 
     cfg = CONFIGS[args.config]
@@ -249,16 +315,29 @@ def main():
     L = h.lib
     P = lambda t: t.data_ptr()
     comm = None
-    if world > 1 and args.comm == "libdcn":
+    gs = None
+    n_dw = gw.numel() + gb.numel()  # ∂W and ∂b lead the packed buffer (dcn_dp.PARAM_ORDER)
+    if exch and args.comm == "libdcn":
+        # libdcn's own communicator attached to the handle: dcn_backward returns summed
+        # gradients, the ∂W/∂b part overlapped with ∂col/col2im/offset-conv backward, the
+        # sums in fp32 (bf16: over the fp32 working copies)
         uid = [dcn_dp.RcclComm.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         comm = dcn_dp.RcclComm(h, world, rank, uid[0])
+        h.set_comm(comm)
+    elif exch:
+        # torch.distributed (RCCL over xGMI): libdcn releases `gs` as soon as ∂W and ∂b are
+        # final, so their all-reduce runs beside the rest of the backward
+        gs = torch.cuda.Stream(dev)
+        h.set_grad_stream(gs.cuda_stream)
 
-    def allreduce():
-        if comm is not None:
-            comm.allreduce(gflat.data_ptr(), gflat.numel())  # on the handle's stream
-        else:
-            dcn_dp.allreduce_torch(gflat)  # RCCL over xGMI: 2.53 MB of fp32 grads
+    def reduce_fp32(t):
+        if t.dtype == torch.float32:
+            dcn_dp.allreduce_torch(t)
+        else:  # bf16 gradients are summed in fp32 (one bf16 rounding of the sum)
+            t32 = t.float()
+            dcn_dp.allreduce_torch(t32)
+            t.copy_(t32)
 
     def step():
         rt.check(L.dcn_forward(h.h, desc, P(x), P(w_off), P(b_off), P(w), P(b), P(out), P(off),
@@ -268,8 +347,11 @@ def main():
         rt.check(L.dcn_backward(h.h, desc, P(x), P(off), P(w_off), P(w), P(gout), P(gx), P(gw),
                                 P(gb), P(gwo), P(gbo), P(goff), P(ws), wsb, rt.DCN_BWD_COL_IN_WS),
                  "dcn_backward")
-        if world > 1:
-            allreduce()
+        if gs is not None:
+            with torch.cuda.stream(gs):
+                reduce_fp32(gflat[:n_dw])  # starts once ∂W/∂b are final (dcn_set_grad_stream)
+            reduce_fp32(gflat[n_dw:])      # ∂W_off/∂b_off after the whole backward
+            stream.wait_stream(gs)
 
     for _ in range(args.warmup):
         step()
@@ -383,7 +465,8 @@ def main():
                        "global_batch": B * world, "B_per_gpu": B, "C": C, "O": O_, "H": H, "W": W,
                        "kernel": k, "stride": s, "padding": p,
                        "parallelism": f"dp{world} (batch-sharded, replicated params)",
-                       "grad_allreduce": (args.comm if world > 1 else None)},
+                       "grad_allreduce": (f"{args.comm} (overlapped with the backward, fp32 sums)"
+                                          if exch else None)},
             "roofline": {
                 "kernel": f"{k1_name} (K1, deformable bilinear im2col)",
                 "bound": "hbm",
@@ -411,12 +494,60 @@ def main():
             cport = cpu_baseline(cfg, args.cpu_budget, name=f"config{args.config}")
             res["cpu_baseline"] = fw if fw and fw["value"] >= cport["value"] else cport
             res["cpu_baseline_other"] = cport if res["cpu_baseline"] is fw else fw
-        print(json.dumps(res), flush=True)
+        print(json.dumps(res), file=out_stream, flush=True)
     if comm is not None:
+        h.set_comm(None)
         comm.close()
     h.close()
-    if world > 1:
+    if exch:
         dist.destroy_process_group()
+
+
+def spawn_ranks(n):
+    """Run this script once per GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in the env)
+    and return the worst exit status. The parent imports nothing that touches the GPU."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rcs = [None] * n
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+                if rcs[i] not in (None, 0):  # one rank failed: the others would hang
+                    for q in procs:
+                        if q.poll() is None:
+                            q.kill()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return max((abs(rc) for rc in rcs), default=0)
+
+
+def dry_run(world, rank):
+    """--dry: the launch contract without a GPU (gloo on CPU)."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        t = torch.tensor([float(rank)])
+        dist.all_reduce(t)
+        seen = int(t.item())
+        dist.barrier()
+        dist.destroy_process_group()
+    else:
+        seen = 0
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "dry": True,
+                          "rank_id_sum": seen, "pid": os.getpid()}), flush=True)
 
 
 def other_rooflines(kernel_ms, B, C, O_, H, W, N, Ho, Wo, J, bf16, fwd_only):

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define DCN_ABI_VERSION 1
+#define DCN_ABI_VERSION 2 /* 2: dcn_allreduce_grads takes a dtype; dcn_set_comm, dcn_set_grad_stream */
 
 typedef enum {
   DCN_OK = 0,
@@ -226,8 +226,23 @@ typedef struct dcn_comm dcn_comm;
 int dcn_comm_get_unique_id(void* id /* DCN_COMM_ID_BYTES */);
 int dcn_comm_init(dcn_handle* h, int nranks, int rank, const void* id, dcn_comm** out);
 int dcn_comm_destroy(dcn_comm* c);
-/* In-place sum over ranks of `count` fp32 device values, on the handle's stream. */
-int dcn_allreduce_grads(dcn_handle* h, dcn_comm* c, float* grads, size_t count);
+/* In-place sum over ranks of `count` device values of `dtype` (DCN_F32 or DCN_BF16), on
+ * the handle's stream. DCN_ERR_INVALID when count elements of dtype do not fit inside the
+ * device allocation holding `grads`. */
+int dcn_allreduce_grads(dcn_handle* h, dcn_comm* c, void* grads, size_t count, int dtype);
+/* Attach a communicator to the handle (NULL detaches). dcn_backward (and
+ * dcn_backward_host) then returns gradients already summed over the communicator's ranks:
+ * grad_w and grad_b are all-reduced on an internal stream as soon as they are final,
+ * overlapped with the ∂columns GEMM, col2im and the offset-conv backward; grad_w_off and
+ * grad_b_off are all-reduced at the end; the handle's stream waits for both before any
+ * later work. For DCN_BF16 the sums run over the fp32 working copies (one bf16 rounding
+ * of the summed value). Every rank must run the same sequence of dcn_backward calls. */
+int dcn_set_comm(dcn_handle* h, dcn_comm* c);
+/* For callers with their own collectives (e.g. torch.distributed): when `hip_stream` is not
+ * NULL, each later dcn_backward makes that stream wait (hipStreamWaitEvent) until grad_w
+ * and grad_b are final, before the ∂columns GEMM even starts, so a collective enqueued on
+ * it right after dcn_backward returns overlaps the rest of the backward. NULL disables. */
+int dcn_set_grad_stream(dcn_handle* h, void* hip_stream);
 
 /* ---- GEMM arithmetic ------------------------------------------------------------ */
 /* How the three fp32 GEMMs of the op (deform_conv.py:76 and its two autodiff GEMMs)

@@ -129,6 +129,18 @@ WsLayout ws_layout(const Geo& g, bool bwd) {
   L.wt = take(dcn::offset_conv_wt_floats(g) * sizeof(float));
   L.part = take(dcn::offset_conv_fpart_floats(g) * sizeof(float));
   L.col = take((size_t)g.B * g.HW * g.K * sizeof(float));
+  const size_t f = sizeof(float);
+  if (g.dt == DCN_BF16) {
+    // DCN_BF16 forward copies, at the same offsets in the forward-only and the
+    // forward+backward layouts: a backward with DCN_BWD_COL_IN_WS reads what the forward
+    // (which always uses the forward-only layout) wrote
+    L.x32 = take((size_t)g.B * g.C * g.HWi * f);
+    L.woff32 = take((size_t)g.J * g.C * g.N * f);
+    L.boff32 = take((size_t)g.J * f);
+    L.b32 = take((size_t)g.O * f);
+    L.off32 = take((size_t)g.B * g.J * g.HW * f);
+    L.out32 = take((size_t)g.B * g.O * g.HW * f);
+  }
   if (bwd) {
     // ∂W partials; first also the ∂b tile sums of the fused ∂out transpose
     L.parts = take(std::max((size_t)g.B * g.O * g.K, dcn::xpose_chsum_floats(g.B, g.O, g.HW)) *
@@ -139,23 +151,14 @@ WsLayout ws_layout(const Geo& g, bool bwd) {
     L.goutT = take((size_t)g.B * g.HW * g.O * sizeof(float));
     L.bins = take(dcn::bins_ws_bytes(g, g.B));
   }
-  if (g.dt == DCN_BF16) {
-    const size_t f = sizeof(float);
-    L.x32 = take((size_t)g.B * g.C * g.HWi * f);
-    L.woff32 = take((size_t)g.J * g.C * g.N * f);
-    L.boff32 = take((size_t)g.J * f);
-    L.b32 = take((size_t)g.O * f);
-    L.off32 = take((size_t)g.B * g.J * g.HW * f);
-    L.out32 = take((size_t)g.B * g.O * g.HW * f);
-    if (bwd) {
-      L.gout32 = take((size_t)g.B * g.O * g.HW * f);
-      L.gx32 = take((size_t)g.B * g.C * g.HWi * f);
-      L.gw32 = take((size_t)g.O * g.K * f);
-      L.gb32 = take((size_t)g.O * f);
-      L.gwo32 = take((size_t)g.J * g.C * g.N * f);
-      L.gbo32 = take((size_t)g.J * f);
-      L.goff32 = take((size_t)g.B * g.J * g.HW * f);
-    }
+  if (g.dt == DCN_BF16 && bwd) {
+    L.gout32 = take((size_t)g.B * g.O * g.HW * f);
+    L.gx32 = take((size_t)g.B * g.C * g.HWi * f);
+    L.gw32 = take((size_t)g.O * g.K * f);
+    L.gb32 = take((size_t)g.O * f);
+    L.gwo32 = take((size_t)g.J * g.C * g.N * f);
+    L.gbo32 = take((size_t)g.J * f);
+    L.goff32 = take((size_t)g.B * g.J * g.HW * f);
   }
   L.total = off;
   return L;
@@ -171,11 +174,15 @@ struct dcn_handle {
   // sample bins beside the GEMMs); forked from / joined back into `stream` with events
   hipStream_t aux = nullptr;
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
-  // backward pipeline: chunk k's ∂offset is ready (main -> aux)
-  static constexpr int kChunkEvents = 8;
-  hipEvent_t chunk_ev[kChunkEvents] = {};
   dcn::GemmEngine* gemm = nullptr;
   int fwd_path = DCN_FWD_AUTO;  // dcn_set_fwd_path
+  // data-parallel gradient exchange (dcn_set_comm / dcn_set_grad_stream): the ∂W/∂b
+  // all-reduce runs on comm_stream as soon as they are final (dw_main / dw_aux), beside the
+  // rest of the backward; the stream waits for comm_done before anything later
+  dcn_comm* comm = nullptr;
+  hipStream_t comm_stream = nullptr;
+  hipStream_t grad_stream = nullptr;  // caller's stream to release at ∂W/∂b-final
+  hipEvent_t dw_main = nullptr, dw_aux = nullptr, end_ev = nullptr, comm_done = nullptr;
   // handle-owned workspace (host-pointer API) and scratch (standalone kernel API)
   void* ws = nullptr;
   size_t ws_bytes = 0;
@@ -245,6 +252,50 @@ int join_aux(dcn_handle* h) {
   return DCN_OK;
 }
 
+extern "C" __attribute__((visibility("hidden"))) int dcn_internal_allreduce_n(
+    dcn_comm* c, int n, void* const* bufs, const size_t* counts, int dtype, void* st);
+
+// ∂W / ∂b are final once everything issued so far on the main and the side stream is done:
+// release the caller's grad stream (dcn_set_grad_stream) and, with a communicator attached,
+// start their all-reduce on comm_stream (fp32 values: DCN_F32 tensors, or the fp32 working
+// copies of DCN_BF16, converted to bf16 by `post` on comm_stream after the sum).
+int dw_final(dcn_handle* h, float* gw, float* gb, const Geo& g,
+             dcn::bf16_t* gw_bf = nullptr, dcn::bf16_t* gb_bf = nullptr) {
+  if (!h->comm && !h->grad_stream) return DCN_OK;
+  HIP_TRY(hipEventRecord(h->dw_main, h->stream));
+  HIP_TRY(hipEventRecord(h->dw_aux, h->aux));
+  if (h->grad_stream) {
+    HIP_TRY(hipStreamWaitEvent(h->grad_stream, h->dw_main, 0));
+    HIP_TRY(hipStreamWaitEvent(h->grad_stream, h->dw_aux, 0));
+  }
+  if (!h->comm) return DCN_OK;
+  HIP_TRY(hipStreamWaitEvent(h->comm_stream, h->dw_main, 0));
+  HIP_TRY(hipStreamWaitEvent(h->comm_stream, h->dw_aux, 0));
+  void* bufs[2] = {gw, gb};
+  const size_t counts[2] = {(size_t)g.O * g.K, gb ? (size_t)g.O : 0};
+  DCN_TRY(dcn_internal_allreduce_n(h->comm, 2, bufs, counts, DCN_F32, h->comm_stream));
+  if (gw_bf) HIP_TRY(dcn::launch_f32_to_bf16(gw, gw_bf, counts[0], h->comm_stream));
+  if (gb_bf && gb) HIP_TRY(dcn::launch_f32_to_bf16(gb, gb_bf, counts[1], h->comm_stream));
+  return DCN_OK;
+}
+
+// End of dcn_backward with a communicator: ∂W_off / ∂b_off summed after everything on the
+// main stream, then the main stream waits for the whole exchange.
+int grads_final(dcn_handle* h, float* gwo, float* gbo, const Geo& g,
+                dcn::bf16_t* gwo_bf = nullptr, dcn::bf16_t* gbo_bf = nullptr) {
+  if (!h->comm) return DCN_OK;
+  HIP_TRY(hipEventRecord(h->end_ev, h->stream));
+  HIP_TRY(hipStreamWaitEvent(h->comm_stream, h->end_ev, 0));
+  void* bufs[2] = {gwo, gbo};
+  const size_t counts[2] = {(size_t)g.J * g.C * g.N, (size_t)g.J};
+  DCN_TRY(dcn_internal_allreduce_n(h->comm, 2, bufs, counts, DCN_F32, h->comm_stream));
+  if (gwo_bf) HIP_TRY(dcn::launch_f32_to_bf16(gwo, gwo_bf, counts[0], h->comm_stream));
+  if (gbo_bf) HIP_TRY(dcn::launch_f32_to_bf16(gbo, gbo_bf, counts[1], h->comm_stream));
+  HIP_TRY(hipEventRecord(h->comm_done, h->comm_stream));
+  HIP_TRY(hipStreamWaitEvent(h->stream, h->comm_done, 0));
+  return DCN_OK;
+}
+
 // Split-bf16 GEMM arithmetic (dcn_math X3/X6/X9) for the forward GEMM with its bias fused
 // (the two backward GEMMs reach the split kernels through dcn::gemm_run).
 bool use_split(dcn_handle* h, const Geo& g) {
@@ -309,15 +360,10 @@ int dw_groups(const Geo& g) {
   return (g.dt == DCN_BF16 && g.B > 16 && g.B % 16 == 0) ? 16 : 0;
 }
 
-struct OffsetBwd {
-  const float* w_off;
-  float *gw_off, *gb_off, *goffT, *wt2;
-};
-
 int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off, const float* w,
                   const float* gout, float* gx, float* gw, float* gb, bool has_bias, float* goff,
                   float* xT, float* colT, float* parts, float* gxT, float* goutT, void* bins,
-                  bool col_valid, const OffsetBwd* ob = nullptr, bool* ob_done = nullptr) {
+                  bool col_valid) {
   // the sample bins depend only on the offsets: build them on the side stream while the
   // main stream runs the ∂W / ∂col GEMMs
   DCN_TRY(fork_aux(h));
@@ -387,6 +433,8 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
       HIP_TRY(dcn::launch_sum_partials(parts, g.B, (size_t)g.K * g.O, gw, h->aux));
     }
   }
+  // ∂W and ∂b are final once the work issued so far on both streams is done
+  DCN_TRY(dw_final(h, gw, has_bias ? gb : nullptr, g));
   {
     // ∂colT[B·HW][K] = ∂outT · Wf as ONE GEMM over the whole batch (r01 probe: 1.68 ms
     // flat vs 1.92 ms as 64 per-image NT GEMMs), after transposing ∂out to
@@ -410,37 +458,6 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
     }
   }
   DCN_TRY(join_aux(h));  // bins ready
-  if (ob && ob_done && dcn::col2im_chunkable(g) && dcn::offset_bwd_chunkable(g) && g.B >= 2 &&
-      dcn::exp_flag(3) >= 2) {
-    // Batch-chunk pipeline (A/B knob DCN_EXP slot 3 = chunk count, off by default): K5
-    // (col2im, HBM-latency bound) of chunk k+1 on the main stream beside K7 (offset-conv
-    // ∂W_off / ∂x on MFMA) of chunk k on the side stream, which waits for chunk k's
-    // ∂offset. Same kernels and per-image results as the serial order. r01 at config 3:
-    // serial 0.668 + 0.470 ms; 2 / 4 / 8 chunks 1.18 / 1.23 / 1.32 ms (the two contend for
-    // the CUs instead of overlapping).
-    // (profile scopes: "col2im" = the whole interleaved region, "offset_bwd" = the fold)
-    {
-      ProfScope ps(h, DCN_K_COL2IM);
-      static_assert(dcn_handle::kChunkEvents >= 8, "one event per chunk");
-      const int nc = std::min(g.B, std::min(dcn::exp_flag(3), 8));
-      const int cb = (g.B + nc - 1) / nc;
-      HIP_TRY(dcn::launch_offset_bwd_prep(g, ob->w_off, ob->wt2, h->aux));
-      for (int k = 0; k * cb < g.B; ++k) {
-        const int b0 = k * cb, nb = std::min(cb, g.B - b0);
-        HIP_TRY(dcn::launch_col2im_coord(g, x, xT, off, colT + (size_t)b0 * g.HW * g.K, nullptr,
-                                         gxT, goff, bins, b0, nb, true, h->stream, g.B));
-        HIP_TRY(hipEventRecord(h->chunk_ev[k], h->stream));
-        HIP_TRY(hipStreamWaitEvent(h->aux, h->chunk_ev[k], 0));
-        HIP_TRY(dcn::launch_offset_bwd_chunk(g, xT, goff, ob->goffT, ob->wt2, gx, gxT, b0, nb,
-                                             h->aux));
-      }
-      DCN_TRY(join_aux(h));
-    }
-    ProfScope ps2(h, DCN_K_OFFSET_BWD);
-    HIP_TRY(dcn::launch_offset_bwd_finish(g, goff, ob->goffT, ob->gw_off, ob->gb_off, h->stream));
-    *ob_done = true;
-    return DCN_OK;
-  }
   {
     // K5 overwrites grad_x (sampling route) and grad_off
     ProfScope ps(h, DCN_K_COL2IM);
@@ -526,11 +543,12 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
     ProfScope ps(h, DCN_K_IM2COL);
     HIP_TRY(dcn::launch_im2col_bf16(g, xT, off32, col, 0, g.B, st));
   }
+  const bool exch = h->comm != nullptr;  // sum the fp32 copies over ranks, then round
   if (has_bias) {
     ProfScope ps(h, DCN_K_BWD_BIAS);
     HIP_TRY(dcn::launch_bf16_to_f32(gout, gout32, nout, st));
     HIP_TRY(dcn::launch_bias_grad(g, gout32, F32(L.gb32), st));
-    HIP_TRY(dcn::launch_f32_to_bf16(F32(L.gb32), gb, (size_t)g.O, st));
+    if (!exch) HIP_TRY(dcn::launch_f32_to_bf16(F32(L.gb32), gb, (size_t)g.O, st));
   }
   bf16_t* goutT = BF(L.goutT);
   const int dwg = dw_groups(g);
@@ -560,8 +578,10 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
       GEMM_TRY(h, sp, col, gout, F32(L.parts));
     }
     HIP_TRY(dcn::launch_sum_partials(F32(L.parts), nparts, (size_t)g.K * g.O, F32(L.gw32), st));
-    HIP_TRY(dcn::launch_f32_to_bf16(F32(L.gw32), gw, (size_t)g.O * g.K, st));
+    if (!exch) HIP_TRY(dcn::launch_f32_to_bf16(F32(L.gw32), gw, (size_t)g.O * g.K, st));
   }
+  DCN_TRY(dw_final(h, F32(L.gw32), has_bias ? F32(L.gb32) : nullptr, g, exch ? gw : nullptr,
+                   exch && has_bias ? gb : nullptr));
   {
     ProfScope ps(h, DCN_K_GEMM_DCOL);  // ∂colT = ∂outT · Wf, one flat GEMM, bf16 out
     if (dwg <= 0) HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(gout, goutT, g.B, g.O, g.HW, st));
@@ -581,9 +601,10 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
   HIP_TRY(dcn::launch_offset_conv_bwd(g, x32, xT, F32(L.woff32), goff32, F32(L.goffT), F32(L.wt),
                                       gx32, F32(L.gwo32), F32(L.gbo32), F32(L.gxT), st));
   HIP_TRY(dcn::launch_f32_to_bf16(gx32, gx, nx, st));
+  if (goff_out) HIP_TRY(dcn::launch_f32_to_bf16(goff32, goff_out, noff, st));
+  if (exch) return grads_final(h, F32(L.gwo32), F32(L.gbo32), g, gw_off, gb_off);
   HIP_TRY(dcn::launch_f32_to_bf16(F32(L.gwo32), gw_off, nwo, st));
   HIP_TRY(dcn::launch_f32_to_bf16(F32(L.gbo32), gb_off, (size_t)g.J, st));
-  if (goff_out) HIP_TRY(dcn::launch_f32_to_bf16(goff32, goff_out, noff, st));
   return DCN_OK;
 }
 #undef BF
@@ -640,8 +661,9 @@ int dcn_create(int device, dcn_handle** out) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming);
-  for (auto& ce : h->chunk_ev)
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ce, hipEventDisableTiming);
+  for (hipEvent_t* ev : {&h->dw_main, &h->dw_aux, &h->end_ev, &h->comm_done})
+    if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     dcn_destroy(h);
     return fail(DCN_ERR_HIP, std::string("dcn_create: ") + hipGetErrorString(e));
@@ -668,8 +690,12 @@ int dcn_destroy(dcn_handle* h) {
   dcn::gemm_engine_destroy(h->gemm);
   if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
   if (h->join_ev) (void)hipEventDestroy(h->join_ev);
-  for (hipEvent_t ce : h->chunk_ev)
-    if (ce) (void)hipEventDestroy(ce);
+  for (hipEvent_t ev : {h->dw_main, h->dw_aux, h->end_ev, h->comm_done})
+    if (ev) (void)hipEventDestroy(ev);
+  if (h->comm_stream) {
+    (void)hipStreamSynchronize(h->comm_stream);
+    (void)hipStreamDestroy(h->comm_stream);
+  }
   if (h->aux) (void)hipStreamDestroy(h->aux);
   if (h->own) (void)hipStreamDestroy(h->own);
   delete h;
@@ -875,22 +901,21 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
   }
   auto F = [&](size_t o) { return reinterpret_cast<float*>(base + o); };
   float* goff = grad_off_out ? grad_off_out : F(L.goff);
-  const OffsetBwd ob{w_off, grad_w_off, grad_b_off, F(L.goffT), F(L.wt)};
-  bool ob_done = false;
   DCN_TRY(core_backward(h, g, x, off, w, grad_out, grad_x, grad_w, grad_b, d->has_bias != 0, goff,
                         F(L.xT), F(L.col), F(L.parts), F(L.gxT), F(L.goutT), base + L.bins,
-                        (flags & DCN_BWD_COL_IN_WS) != 0, &ob, &ob_done));
-  if (ob_done) return DCN_OK;
-  ProfScope ps(h, DCN_K_OFFSET_BWD);
-  // ∂b_off = Σ ∂offset (18 channels: a latency-bound reduction) on the side stream, beside
-  // the offset-conv ∂W / ∂x kernels
-  DCN_TRY(fork_aux(h));
-  dcn::launch_channel_sum(goff, g.B, g.J, g.HW, grad_b_off, h->aux);
-  HIP_TRY(dcn::launch_offset_conv_bwd(g, x, F(L.xT), w_off, goff, F(L.goffT), F(L.wt), grad_x,
-                                      grad_w_off, nullptr,
-                                      dcn::get_force_generic() ? nullptr : F(L.gxT), h->stream));
-  DCN_TRY(join_aux(h));
-  return DCN_OK;
+                        (flags & DCN_BWD_COL_IN_WS) != 0));
+  {
+    ProfScope ps(h, DCN_K_OFFSET_BWD);
+    // ∂b_off = Σ ∂offset (18 channels: a latency-bound reduction) on the side stream, beside
+    // the offset-conv ∂W / ∂x kernels
+    DCN_TRY(fork_aux(h));
+    dcn::launch_channel_sum(goff, g.B, g.J, g.HW, grad_b_off, h->aux);
+    HIP_TRY(dcn::launch_offset_conv_bwd(g, x, F(L.xT), w_off, goff, F(L.goffT), F(L.wt), grad_x,
+                                        grad_w_off, nullptr,
+                                        dcn::get_force_generic() ? nullptr : F(L.gxT), h->stream));
+    DCN_TRY(join_aux(h));
+  }
+  return grads_final(h, grad_w_off, grad_b_off, g);
 }
 
 // ---- host-pointer variants -----------------------------------------------------
@@ -1173,6 +1198,19 @@ int dcn_set_math(dcn_handle* h, int math) {
       math != DCN_MATH_F32_BF16X9)
     return fail(DCN_ERR_INVALID, "dcn_set_math: unknown mode " + std::to_string(math));
   dcn::gemm_set_math(h->gemm, math);
+  return DCN_OK;
+}
+
+int dcn_set_comm(dcn_handle* h, dcn_comm* c) {
+  DCN_TRY(set_device(h));
+  if (h->comm && h->comm != c) HIP_TRY(hipStreamSynchronize(h->comm_stream));
+  h->comm = c;
+  return DCN_OK;
+}
+
+int dcn_set_grad_stream(dcn_handle* h, void* s) {
+  DCN_TRY(set_device(h));
+  h->grad_stream = reinterpret_cast<hipStream_t>(s);
   return DCN_OK;
 }
 

@@ -18,6 +18,8 @@
 extern "C" __attribute__((visibility("hidden"))) int dcn_internal_fail(int code, const char* msg);
 extern "C" __attribute__((visibility("hidden"))) int dcn_internal_bind(dcn_handle* h,
                                                                       void** stream);
+extern "C" __attribute__((visibility("hidden"))) int dcn_internal_allreduce(
+    dcn_comm* c, void* buf, size_t count, int dtype, void* st);
 
 namespace {
 
@@ -31,8 +33,10 @@ typedef int (*CommInitRank_t)(ncclComm_t*, int, ncclUniqueId, int);
 typedef int (*CommDestroy_t)(ncclComm_t);
 typedef int (*AllReduce_t)(const void*, void*, size_t, int, int, ncclComm_t, hipStream_t);
 typedef const char* (*GetErrorString_t)(int);
-constexpr int kNcclFloat32 = 7;  // ncclFloat32
-constexpr int kNcclSum = 0;      // ncclSum
+typedef int (*Group_t)(void);
+constexpr int kNcclFloat32 = 7;   // ncclFloat32
+constexpr int kNcclBfloat16 = 9;  // ncclBfloat16
+constexpr int kNcclSum = 0;       // ncclSum
 
 struct Rccl {
   void* lib = nullptr;
@@ -41,6 +45,7 @@ struct Rccl {
   CommDestroy_t destroy = nullptr;
   AllReduce_t allreduce = nullptr;
   GetErrorString_t errstr = nullptr;
+  Group_t group_start = nullptr, group_end = nullptr;
 };
 
 Rccl* rccl(std::string* err) {
@@ -58,9 +63,12 @@ Rccl* rccl(std::string* err) {
       r.destroy = (CommDestroy_t)dlsym(r.lib, "ncclCommDestroy");
       r.allreduce = (AllReduce_t)dlsym(r.lib, "ncclAllReduce");
       r.errstr = (GetErrorString_t)dlsym(r.lib, "ncclGetErrorString");
+      r.group_start = (Group_t)dlsym(r.lib, "ncclGroupStart");
+      r.group_end = (Group_t)dlsym(r.lib, "ncclGroupEnd");
     }
   }
-  if (!r.lib || !r.get_id || !r.init || !r.destroy || !r.allreduce) {
+  if (!r.lib || !r.get_id || !r.init || !r.destroy || !r.allreduce || !r.group_start ||
+      !r.group_end) {
     *err = "RCCL (librccl.so.1) not loadable";
     return nullptr;
   }
@@ -128,19 +136,57 @@ int dcn_comm_destroy(dcn_comm* c) {
   return DCN_OK;
 }
 
-int dcn_allreduce_grads(dcn_handle* h, dcn_comm* c, float* grads, size_t count) {
+int dcn_allreduce_grads(dcn_handle* h, dcn_comm* c, void* grads, size_t count, int dtype) {
   if (!c || (!grads && count)) return dcn_internal_fail(DCN_ERR_INVALID, "null argument");
+  if (dtype != DCN_F32 && dtype != DCN_BF16)
+    return dcn_internal_fail(DCN_ERR_INVALID, "dcn_allreduce_grads: dtype must be DCN_F32 or DCN_BF16");
   void* st = nullptr;
   int rc = dcn_internal_bind(h, &st);
   if (rc != DCN_OK) return rc;
   if (count == 0) return DCN_OK;
-  std::string err;
-  Rccl* r = rccl(&err);
-  if (!r) return dcn_internal_fail(DCN_ERR_COMM, err.c_str());
-  rc = r->allreduce(grads, grads, count, kNcclFloat32, kNcclSum, c->comm,
-                    static_cast<hipStream_t>(st));
-  if (rc != 0) return rccl_fail(r, "ncclAllReduce", rc);
-  return DCN_OK;
+  // the buffer must hold count elements of dtype inside ONE device allocation (a count in
+  // fp32 elements over a bf16 buffer would run RCCL 2x past its end)
+  const size_t bytes = count * (dtype == DCN_BF16 ? 2 : 4);
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, grads) != hipSuccess || !base)
+    return dcn_internal_fail(DCN_ERR_INVALID, "dcn_allreduce_grads: grads is not device memory");
+  const char* b = static_cast<const char*>(base);
+  const char* p = static_cast<const char*>(grads);
+  if (p + bytes > b + size)
+    return dcn_internal_fail(DCN_ERR_INVALID,
+                             "dcn_allreduce_grads: count x sizeof(dtype) runs past the end of "
+                             "the allocation holding grads");
+  return dcn_internal_allreduce(c, grads, count, dtype, st);
 }
 
 }  // extern "C"
+
+// In-place sums for dcn_backward when a communicator is attached (dcn_set_comm): several
+// buffers in one RCCL group, on stream st. Internal (not in dcn.h).
+extern "C" __attribute__((visibility("hidden"))) int dcn_internal_allreduce_n(
+    dcn_comm* c, int n, void* const* bufs, const size_t* counts, int dtype, void* st) {
+  std::string err;
+  Rccl* r = rccl(&err);
+  if (!r) return dcn_internal_fail(DCN_ERR_COMM, err.c_str());
+  const int ty = dtype == DCN_BF16 ? kNcclBfloat16 : kNcclFloat32;
+  int rc = r->group_start();
+  if (rc != 0) return rccl_fail(r, "ncclGroupStart", rc);
+  for (int i = 0; i < n; ++i) {
+    if (!counts[i]) continue;
+    rc = r->allreduce(bufs[i], bufs[i], counts[i], ty, kNcclSum, c->comm,
+                      static_cast<hipStream_t>(st));
+    if (rc != 0) {
+      (void)r->group_end();
+      return rccl_fail(r, "ncclAllReduce", rc);
+    }
+  }
+  rc = r->group_end();
+  if (rc != 0) return rccl_fail(r, "ncclGroupEnd", rc);
+  return DCN_OK;
+}
+
+extern "C" __attribute__((visibility("hidden"))) int dcn_internal_allreduce(
+    dcn_comm* c, void* buf, size_t count, int dtype, void* st) {
+  return dcn_internal_allreduce_n(c, 1, &buf, &count, dtype, st);
+}

@@ -101,10 +101,13 @@ class RcclComm:
         rt.check(rt.load().dcn_comm_get_unique_id(buf), "dcn_comm_get_unique_id")
         return buf.raw
 
-    def allreduce(self, dev_ptr: int, count: int):
-        """In-place sum of `count` fp32 values at device address `dev_ptr`."""
+    def allreduce(self, dev_ptr: int, count: int, dtype: int = 0):
+        """In-place sum of `count` values of `dtype` (dcn_runtime.DCN_F32 / DCN_BF16) at
+        device address `dev_ptr`, on the handle's stream. libdcn rejects a count/dtype
+        that runs past the allocation holding dev_ptr."""
         self.rt.check(self.handle.lib.dcn_allreduce_grads(self.handle.h, self.c,
-                                                          ctypes.c_void_p(dev_ptr), count),
+                                                          ctypes.c_void_p(dev_ptr), count,
+                                                          int(dtype)),
                       "dcn_allreduce_grads")
 
     def close(self):

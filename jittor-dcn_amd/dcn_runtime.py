@@ -14,6 +14,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DCN_LIB", os.path.join(HERE, "lib", "libdcn.so"))
 
+ABI_VERSION = 2  # include/dcn.h DCN_ABI_VERSION
 DCN_F32, DCN_BF16 = 0, 1
 DCN_BWD_COL_IN_WS = 1
 DCN_FWD_AUTO, DCN_FWD_UNFUSED, DCN_FWD_FUSED = 0, 1, 2
@@ -77,7 +78,9 @@ SIGNATURES = {
     "dcn_comm_get_unique_id": [_vp],
     "dcn_comm_init": [_vp, ctypes.c_int, ctypes.c_int, _vp, ctypes.POINTER(_vp)],
     "dcn_comm_destroy": [_vp],
-    "dcn_allreduce_grads": [_vp, _vp, _vp, _sz],
+    "dcn_allreduce_grads": [_vp, _vp, _vp, _sz, ctypes.c_int],
+    "dcn_set_comm": [_vp, _vp],
+    "dcn_set_grad_stream": [_vp, _vp],
     "dcn_debug_force_generic": [ctypes.c_int],
     "dcn_set_math": [_vp, ctypes.c_int],
     "dcn_get_math": [_vp, _ip],
@@ -113,7 +116,7 @@ def load(path: str | None = None):
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = _RESTYPES.get(name, ctypes.c_int)
-        if L.dcn_abi_version() != 1:
+        if L.dcn_abi_version() != ABI_VERSION:
             raise RuntimeError("libdcn ABI version mismatch")
         if path is None:
             _lib = L
@@ -222,6 +225,18 @@ class Handle:
     def set_fwd_path(self, path: int):
         """0 DCN_FWD_AUTO (measured-faster schedule), 1 DCN_FWD_UNFUSED, 2 DCN_FWD_FUSED."""
         check(self.lib.dcn_set_fwd_path(self.h, int(path)), "dcn_set_fwd_path")
+
+    # --- data-parallel gradient exchange (include/dcn.h) ---------------------------
+    def set_comm(self, comm):
+        """Attach a dcn_dp.RcclComm (None detaches): dcn_backward then returns gradients
+        summed over the ranks, the ∂W/∂b all-reduce overlapped with the rest of it."""
+        check(self.lib.dcn_set_comm(self.h, comm.c if comm is not None else None), "dcn_set_comm")
+
+    def set_grad_stream(self, stream_ptr: int | None):
+        """Each later dcn_backward makes this hipStream_t wait until ∂W and ∂b are final
+        (None / 0 disables), so a collective enqueued on it overlaps the backward's rest."""
+        check(self.lib.dcn_set_grad_stream(self.h, ctypes.c_void_p(stream_ptr or 0)),
+              "dcn_set_grad_stream")
 
     def get_math(self) -> int:
         m = ctypes.c_int()

@@ -201,17 +201,24 @@ int dcnref_backward(const dcnref_desc* d, const float* x, const float* off, cons
   float* col = (float*)malloc((size_t)g.K * g.HW * sizeof(float));
   float* dcol = (float*)malloc((size_t)g.K * g.HW * sizeof(float));
   float* goff = (float*)malloc((size_t)g.J * g.HW * sizeof(float));
-  if (!col || !dcol || !goff) {
+  /* the four parameter reductions (sums over B*Ho*Wo pixels) accumulate in double, so the
+   * checker's own rounding stays far below the 1e-4 reduction tolerance at full size */
+  const size_t nwo = (size_t)g.J * d->C * KK;
+  double* aw = (double*)calloc((size_t)d->O * g.K, sizeof(double));
+  double* ab = (double*)calloc((size_t)d->O, sizeof(double));
+  double* awo = (double*)calloc(nwo, sizeof(double));
+  double* abo = (double*)calloc((size_t)g.J, sizeof(double));
+  if (!col || !dcol || !goff || !aw || !ab || !awo || !abo) {
     free(col);
     free(dcol);
     free(goff);
+    free(aw);
+    free(ab);
+    free(awo);
+    free(abo);
     return -2;
   }
   memset(gx, 0, (size_t)d->B * d->C * g.HWi * sizeof(float));
-  memset(gw, 0, (size_t)d->O * g.K * sizeof(float));
-  if (d->has_bias) memset(gb, 0, (size_t)d->O * sizeof(float));
-  memset(gw_off, 0, (size_t)g.J * d->C * KK * sizeof(float));
-  memset(gb_off, 0, (size_t)g.J * sizeof(float));
   for (int bi = 0; bi < d->B; ++bi) {
     const float* xb = x + (size_t)bi * d->C * g.HWi;
     const float* offb = off + (size_t)bi * g.J * g.HW;
@@ -220,9 +227,9 @@ int dcnref_backward(const dcnref_desc* d, const float* x, const float* off, cons
     im2col_img(d, &g, xb, offb, col);
     if (d->has_bias)
       for (int o = 0; o < d->O; ++o) {
-        float s = 0.f;
+        double s = 0.0;
         for (int m = 0; m < g.HW; ++m) s += gob[(size_t)o * g.HW + m];
-        gb[o] += s;
+        ab[o] += s;
       }
       /* ∂W[o][k] += Σ_m ∂out[o][m] col[k][m] */
 #pragma omp parallel for schedule(static)
@@ -230,9 +237,9 @@ int dcnref_backward(const dcnref_desc* d, const float* x, const float* off, cons
       for (int k = 0; k < g.K; ++k) {
         const float* a = gob + (size_t)o * g.HW;
         const float* c = col + (size_t)k * g.HW;
-        float s = 0.f;
-        for (int m = 0; m < g.HW; ++m) s = fmaf(a[m], c[m], s);
-        gw[(size_t)o * g.K + k] += s;
+        double s = 0.0;
+        for (int m = 0; m < g.HW; ++m) s += (double)a[m] * c[m];
+        aw[(size_t)o * g.K + k] += s;
       }
       /* ∂col[k][m] = Σ_o W[o][k] ∂out[o][m] */
 #pragma omp parallel for schedule(static)
@@ -293,24 +300,24 @@ int dcnref_backward(const dcnref_desc* d, const float* x, const float* off, cons
 #pragma omp parallel for schedule(static)
     for (int j = 0; j < g.J; ++j) {
       const float* gj = goff + (size_t)j * g.HW;
-      float s = 0.f;
+      double s = 0.0;
       for (int m = 0; m < g.HW; ++m) s += gj[m];
-      gb_off[j] += s;
+      abo[j] += s;
       for (int c = 0; c < d->C; ++c)
         for (int i = 0; i < d->kh; ++i)
           for (int k = 0; k < d->kw; ++k) {
             const float* xc = xb + (size_t)c * g.HWi;
-            float acc = 0.f;
+            double acc = 0.0;
             for (int ho = 0; ho < g.Ho; ++ho) {
               int y = ho * d->sh - d->ph + i * d->dh;
               if (y < 0 || y >= d->H) continue;
               for (int wo_ = 0; wo_ < g.Wo; ++wo_) {
                 int xx = wo_ * d->sw - d->pw + k * d->dw;
                 if (xx < 0 || xx >= d->W) continue;
-                acc = fmaf(gj[ho * g.Wo + wo_], xc[y * d->W + xx], acc);
+                acc += (double)gj[ho * g.Wo + wo_] * xc[y * d->W + xx];
               }
             }
-            gw_off[((size_t)j * d->C + c) * KK + i * d->kw + k] += acc;
+            awo[((size_t)j * d->C + c) * KK + i * d->kw + k] += acc;
           }
     }
 #pragma omp parallel for schedule(static)
@@ -334,8 +341,17 @@ int dcnref_backward(const dcnref_desc* d, const float* x, const float* off, cons
     }
     if (goff_out) memcpy(goff_out + (size_t)bi * g.J * g.HW, goff, (size_t)g.J * g.HW * sizeof(float));
   }
+  for (size_t i = 0; i < (size_t)d->O * g.K; ++i) gw[i] = (float)aw[i];
+  if (d->has_bias)
+    for (int o = 0; o < d->O; ++o) gb[o] = (float)ab[o];
+  for (size_t i = 0; i < nwo; ++i) gw_off[i] = (float)awo[i];
+  for (int j = 0; j < g.J; ++j) gb_off[j] = (float)abo[j];
   free(col);
   free(dcol);
   free(goff);
+  free(aw);
+  free(ab);
+  free(awo);
+  free(abo);
   return 0;
 }

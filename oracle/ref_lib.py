@@ -29,6 +29,22 @@ def build():
     subprocess.run(["make", "-s", "-C", HERE], check=True)
 
 
+def usable_cpus():
+    """Host cores this process may use: the affinity mask, capped by a cgroup CPU quota
+    (a shared GPU box reports the whole machine in os.cpu_count())."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = max(1, min(n, -(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -42,6 +58,7 @@ def lib():
         L.dcnref_out_shape.argtypes = [D, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         L.dcnref_num_threads.restype = ctypes.c_int
         L.dcnref_set_threads.argtypes = [ctypes.c_int]
+        L.dcnref_set_threads(usable_cpus())  # no oversubscription under a CPU quota
         _lib = L
     return _lib
 

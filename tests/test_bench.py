@@ -52,3 +52,39 @@ def test_every_baseline_config_is_a_workload(bench):
     assert bench.CONFIGS[4]["dtype"] == "bf16" and bench.CONFIGS[2].get("fwd_only")
     c5 = bench.CONFIGS[5]
     assert (c5["s"], c5["dil"], c5["G"]) == (2, 2, 4)
+
+
+def _run_bench(*argv, env=None, timeout=180):
+    import json
+    import subprocess
+    import sys
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *argv], env=e,
+                       capture_output=True, text=True, timeout=timeout)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r.returncode, (json.loads(lines[-1]) if lines else None), r.stderr
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_gpus_flag_spawns_that_many_ranks(n):
+    """`bench.py --gpus N` with no external launcher starts N ranks itself (the driver may
+    run it that way); --dry joins them in a gloo group without touching a GPU."""
+    rc, line, err = _run_bench("--gpus", str(n), "--dry")
+    assert rc == 0, err
+    assert line["n_gpus"] == n and line["rank_id_sum"] == n * (n - 1) // 2
+
+
+def test_world_size_mismatch_fails():
+    rc, line, _ = _run_bench("--gpus", "2", "--dry",
+                             env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc != 0 and line is None
+
+
+def test_host_cpus_reports_model_and_count(bench):
+    threads, info = bench.host_cpus()
+    assert 1 <= threads <= info["host_threads"]
+    assert threads <= info["affinity_threads"]
+    assert "cpu_model" in info

@@ -65,50 +65,56 @@ class Buf:
             self.h.free(p)
 
 
-def _case(seed, B, C, O_, H, W, s=(1, 1), off_scale=1.0):
+def _case(seed, B, C, O_, H, W, s=(1, 1), off_scale=1.0, k=(3, 3), p=(1, 1)):
     rng = np.random.default_rng(seed)
+    N = k[0] * k[1]
     x = rng.standard_normal((B, C, H, W)).astype(np.float32)
-    wo = (rng.standard_normal((18, C, 3, 3)) * off_scale / np.sqrt(C * 9)).astype(np.float32)
-    bo = rng.uniform(-0.5, 0.5, 18).astype(np.float32)
-    w = (rng.standard_normal((O_, C, 3, 3)) * np.sqrt(2 / (C * 9))).astype(np.float32)
+    wo = (rng.standard_normal((2 * N, C, *k)) * off_scale / np.sqrt(C * N)).astype(np.float32)
+    bo = rng.uniform(-0.5, 0.5, 2 * N).astype(np.float32)
+    w = (rng.standard_normal((O_, C, *k)) * np.sqrt(2 / (C * N))).astype(np.float32)
     b = (rng.standard_normal(O_) * 0.1).astype(np.float32)
-    Ho, Wo = O.out_size(H, W, 3, 3, *s, 1, 1)
+    Ho, Wo = O.out_size(H, W, *k, *s, *p)
     gout = rng.standard_normal((B, O_, Ho, Wo)).astype(np.float32)
     c = dict(x=x, w_off=wo, b_off=bo, w=w, b=b, grad_out=gout)
-    bits = {k: to_bf16(v) for k, v in c.items()}
-    vals = {k: from_bf16(v) for k, v in bits.items()}  # what the device actually sees
+    bits = {k_: to_bf16(v) for k_, v in c.items()}
+    vals = {k_: from_bf16(v) for k_, v in bits.items()}  # what the device actually sees
     return bits, vals, s
 
 
-def _device(h, bits, s):
+def _device(h, bits, s, pad=(1, 1), comm=None):
     B, C, H, W = bits["x"].shape
-    O_ = bits["w"].shape[0]
-    desc = rt.make_desc(B, C, H, W, O_, (3, 3), s, (1, 1), dtype=rt.DCN_BF16)
+    O_, _, kh, kw = bits["w"].shape
+    J = bits["w_off"].shape[0]
+    desc = rt.make_desc(B, C, H, W, O_, (kh, kw), s, pad, dtype=rt.DCN_BF16)
     Ho, Wo = rt.out_shape(desc)
     D = Buf(h)
     vp = ctypes.c_void_p
     try:
         p = {k: D.up(v) for k, v in bits.items()}
-        pout, poff = D.zeros(B * O_ * Ho * Wo * 2), D.zeros(B * 18 * Ho * Wo * 2)
+        pout, poff = D.zeros(B * O_ * Ho * Wo * 2), D.zeros(B * J * Ho * Wo * 2)
         wsb = rt.workspace_bytes(desc, True)
         ws = D.zeros(wsb)
         rt.check(h.lib.dcn_forward(h.h, desc, vp(p["x"]), vp(p["w_off"]), vp(p["b_off"]),
                                    vp(p["w"]), vp(p["b"]), vp(pout), vp(poff), vp(ws), wsb))
         g = {k: D.zeros(v.nbytes) for k, v in bits.items() if k != "grad_out"}
-        pgoff = D.zeros(B * 18 * Ho * Wo * 2)
+        pgoff = D.zeros(B * J * Ho * Wo * 2)
+        if comm is not None:
+            h.set_comm(comm)
         rt.check(h.lib.dcn_backward(h.h, desc, vp(p["x"]), vp(poff), vp(p["w_off"]), vp(p["w"]),
                                     vp(p["grad_out"]), vp(g["x"]), vp(g["w"]), vp(g["b"]),
                                     vp(g["w_off"]), vp(g["b_off"]), vp(pgoff), vp(ws), wsb,
                                     rt.DCN_BWD_COL_IN_WS))
         out = D.down(pout, (B, O_, Ho, Wo))
-        off = D.down(poff, (B, 18, Ho, Wo))
+        off = D.down(poff, (B, J, Ho, Wo))
         grads = {"x": D.down(g["x"], bits["x"].shape), "weight": D.down(g["w"], bits["w"].shape),
                  "bias": D.down(g["b"], bits["b"].shape),
                  "offset_conv.weight": D.down(g["w_off"], bits["w_off"].shape),
                  "offset_conv.bias": D.down(g["b_off"], bits["b_off"].shape),
-                 "offset": D.down(pgoff, (B, 18, Ho, Wo))}
+                 "offset": D.down(pgoff, (B, J, Ho, Wo))}
         return out, off, grads
     finally:
+        if comm is not None:
+            h.set_comm(None)
         D.free()
 
 
@@ -146,18 +152,55 @@ def test_bf16_forward_backward_vs_oracle(gpu_handle, case):
     assert not bad, f"bf16 relative errors {errs}"
 
 
-def test_bf16_config4_shape_spot_check(gpu_handle):
-    """BASELINE config 4 per GPU (B=64, C=O=256, 28x28, bf16): finite everywhere and two
-    images within the bf16 tolerance of the fp32 C oracle on the same bf16 inputs."""
+def test_bf16_config4_full_size_every_tensor(gpu_handle):
+    """BASELINE config 4 per GPU (B=64, C=O=256, 28x28, bf16) at full size: every tensor
+    against the C oracle run on the same bf16 inputs over the whole batch — the outputs
+    from the oracle's own fp32 offsets (sampling is continuous in position, so the bf16
+    rounding of the offsets, ~4e-3 px, stays inside the tolerance), the backward
+    conditioned on the device's bf16 offsets (knife edges), and the four parameter
+    gradients as 50,176-pixel reductions."""
     bits, v, s = _case(11, B=64, C=256, O_=256, H=28, W=28)
     out, off, g = _device(gpu_handle, bits, s)
-    assert np.isfinite(out).all() and np.isfinite(g["x"]).all()
-    for bi in (0, 63):
-        desc = R.make_desc((1, 256, 28, 28), v["w"].shape, (1, 1), (1, 1))
-        # forward from the oracle's own fp32 offsets: sampling is continuous in position,
-        # so the bf16 rounding of the offsets (~4e-3 px) stays inside the tolerance
-        ro, _ = R.forward(desc, v["x"][bi:bi + 1], v["w_off"], v["b_off"], v["w"], v["b"])
-        rg = R.backward(desc, v["x"][bi:bi + 1], off[bi:bi + 1], v["w_off"], v["w"],
-                        v["grad_out"][bi:bi + 1])
-        assert rel_err(out[bi:bi + 1], ro) <= BF16_TOL
-        assert rel_err(g["x"][bi:bi + 1], rg["x"]) <= BF16_TOL
+    assert np.isfinite(out).all() and all(np.isfinite(t).all() for t in g.values())
+    desc = R.make_desc((64, 256, 28, 28), v["w"].shape, (1, 1), (1, 1))
+    ro, roff = R.forward(desc, v["x"], v["w_off"], v["b_off"], v["w"], v["b"])
+    rg = R.backward(desc, v["x"], off, v["w_off"], v["w"], v["grad_out"])
+    errs = {"out": rel_err(out, ro), "offset_values": rel_err(off, roff)}
+    for k in ("x", "offset", "weight", "bias", "offset_conv.weight", "offset_conv.bias"):
+        errs[k] = rel_err(g[k], rg[k])
+    bad = {k: e for k, e in errs.items() if not e <= BF16_TOL}
+    assert not bad, f"bf16 relative errors {errs}"
+
+
+@pytest.mark.parametrize("k,pad", [((1, 3), (0, 1)), ((3, 1), (1, 0)), ((2, 2), (1, 1))])
+def test_bf16_nonsquare_kernels_vs_oracle(gpu_handle, k, pad):
+    """kh*kw outside {1,4,6,9} takes the generic offset-conv backward, which reads the fp32
+    copy of x that the forward left in the workspace (the layouts of dcn_forward and
+    dcn_backward share that region): ∂W_off must match the oracle."""
+    bits, v, s = _case(31, B=2, C=24, O_=16, H=13, W=11, k=k, p=pad)
+    out, off, g = _device(gpu_handle, bits, s, pad=pad)
+    ro, _, cache = O.forward(v["x"], v["w_off"], v["b_off"], v["w"], v["b"], s, pad,
+                             offsets=off)
+    rg = O.backward(cache, v["grad_out"])
+    errs = {"out": rel_err(out, ro)}
+    for name in ("x", "weight", "bias", "offset_conv.weight", "offset_conv.bias", "offset"):
+        errs[name] = rel_err(g[name], rg[name])
+    bad = {n: e for n, e in errs.items() if not e <= BF16_TOL}
+    assert not bad, f"bf16 relative errors {errs}"
+
+
+def test_bf16_backward_with_attached_comm_single_rank(gpu_handle):
+    """dcn_set_comm on a 1-rank world: dcn_backward sums the fp32 working copies of the
+    parameter gradients over the ranks (the identity here) on its comm stream and rounds
+    them to bf16 there; every gradient must equal the run without a communicator."""
+    import dcn_dp
+    bits, v, s = _case(41, B=3, C=32, O_=24, H=15, W=14)
+    ref = _device(gpu_handle, bits, s)
+    comm = dcn_dp.RcclComm(gpu_handle, 1, 0, dcn_dp.RcclComm.unique_id())
+    try:
+        got = _device(gpu_handle, bits, s, comm=comm)
+    finally:
+        comm.close()
+    np.testing.assert_array_equal(got[0], ref[0])
+    for name in ref[2]:
+        np.testing.assert_array_equal(got[2][name], ref[2][name], err_msg=name)

@@ -308,33 +308,6 @@ def test_empty_batch_host_api(gpu_handle):
         assert not np.any(g[k]), k
 
 
-def test_config3_full_size_properties(gpu_handle):
-    """BASELINE config 3 (B=64, C=O=256, 56², k3 s1 p1) at full size: spot-check two
-    images' per-image outputs/grads against the C oracle (fp32) and ∂W by linearity
-    (batch = sum of its two halves computed separately)."""
-    h = gpu_handle
-    c = _rand_case(61, B=64, C=256, O_=256, H=56, W=56)
-    out, off, g = _device_fwd_bwd(h, c)
-    assert np.isfinite(out).all() and np.isfinite(g["x"]).all()
-    for bi in (0, 63):
-        sub = {k: (v[bi:bi + 1] if k in ("x", "grad_out") else v) for k, v in c.items()}
-        desc = R.make_desc(sub["x"].shape, c["w"].shape, (1, 1), (1, 1))
-        ro, roff = R.forward(desc, sub["x"], c["w_off"], c["b_off"], c["w"], c["b"])
-        # backward conditioned on the device offsets (knife edges, see O.forward)
-        rg = R.backward(desc, sub["x"], off[bi:bi + 1], c["w_off"], c["w"], sub["grad_out"])
-        assert_close(out[bi:bi + 1], ro, what=f"img{bi} out")
-        assert_close(off[bi:bi + 1], roff, what=f"img{bi} offset")
-        assert_close(g["x"][bi:bi + 1], rg["x"], what=f"img{bi} ∂x")
-        assert_close(g["offset"][bi:bi + 1], rg["offset"], what=f"img{bi} ∂offset")
-    halves = []
-    for lo, hi in ((0, 32), (32, 64)):
-        sub = dict(c)
-        sub["x"], sub["grad_out"] = c["x"][lo:hi], c["grad_out"][lo:hi]
-        halves.append(_device_fwd_bwd(h, sub)[2])
-    for k in ("weight", "bias", "offset_conv.weight", "offset_conv.bias"):
-        assert_close_reduction(g[k], halves[0][k] + halves[1][k], tol=2e-5, what=f"linearity ∂{k}")
-
-
 def test_rccl_comm_single_rank_allreduce(gpu_handle):
     """libdcn's RCCL communicator (dcn_comm_* / dcn_allreduce_grads) on a 1-rank world:
     the in-place sum is the identity, on the handle's stream."""
