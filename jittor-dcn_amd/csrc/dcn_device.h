@@ -170,6 +170,15 @@ __device__ __forceinline__ float wave_sum(float v) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
+// Workgroup barrier that orders LDS only: __syncthreads()'s fence would also drain every
+// outstanding global load and store (vmcnt(0)), i.e. the prefetch pipelines kept in flight
+// across the barrier (fused forward: the column stores of a k step; K5: the ∂col rows).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }

@@ -60,13 +60,6 @@ __device__ __forceinline__ float4 bilerp4f(float fr, float fc, float4 a, float4 
                      bilerp(fr, fc, a.z, b.z, c.z, d.z), bilerp(fr, fc, a.w, b.w, c.w, d.w));
 }
 
-// Workgroup barrier that orders LDS only: __syncthreads()'s fence would also drain the
-// non-temporal column stores (vmcnt(0)) every k step, ≈ a store round trip per step.
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kAuxNT = 2;  // buffer-op cache policy: non-temporal (the columns are streamed)

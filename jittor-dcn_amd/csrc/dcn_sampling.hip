@@ -15,9 +15,10 @@
 // ∂x without atomics: LDS float atomics (ds_add_f32) measured ~0.3 lanes/clk/CU on
 // MI355X and global float atomics cap at ~1.3 TB/s, both far too slow for the
 // 4·B·HW·N·C scatter. Instead each sample is binned by its top-left corner
-// (counting sort per image: int atomics on 28k samples/image), every bin list is
-// sorted, and each input pixel gathers the ∂col rows of the four bins whose 2x2
-// footprint covers it — a fixed summation order, so ∂x is bitwise reproducible.
+// (counting sort per image: int atomics on 28k samples/image), each sample's place in
+// its bin is its rank by sample index, and each input pixel gathers the ∂col rows of the
+// four bins whose 2x2 footprint covers it — a fixed summation order, so ∂x is bitwise
+// reproducible.
 #include <climits>
 #include <cstdlib>
 
@@ -451,27 +452,6 @@ __global__ __launch_bounds__(256) void bins_fill(Geo g, const float4* __restrict
   list[(size_t)bg * NS + start[(size_t)bg * (NB + 1) + bin] + slot] = (int)(idx % NS);
 }
 
-// Sort every bin list ascending: fixes the gather's summation order.
-__global__ __launch_bounds__(256) void bins_sort(int NB, int NS, long nbins,
-                                                 const int* __restrict__ start,
-                                                 int* __restrict__ list) {
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= nbins) return;
-  const int bg = (int)(idx / NB), bin = (int)(idx % NB);
-  const int* st = start + (size_t)bg * (NB + 1);
-  int* l = list + (size_t)bg * NS;
-  const int lo = st[bin], hi = st[bin + 1];
-  for (int i = lo + 1; i < hi; ++i) {
-    const int v = l[i];
-    int j = i - 1;
-    while (j >= lo && l[j] > v) {
-      l[j + 1] = l[j];
-      --j;
-    }
-    l[j + 1] = v;
-  }
-}
-
 // ---------------------------------------------------------------------------
 // K5 fused (∂x + ∂offset from ONE pass over the binned ∂col rows).
 // One block = a kTR x kTQ tile of INPUT pixels of one image and kTR+1 waves. Bin
@@ -639,21 +619,35 @@ __global__ __launch_bounds__(kC2iThreads) void col2im_tile(Geo g, const float* _
   }
 }
 
-// Binned samples as contiguous records for col2im_tile, in bin order:
-// {∂colT row offset m*K + n*C, fr, fc, ∂offset index n*HW + m}.
-__global__ __launch_bounds__(256) void bins_pack(Geo g, int nbg, const float4* __restrict__ rec,
+// Binned samples as contiguous records for the fused K5 kernels, in bin order:
+// {∂colT row offset m*K + n*C, fr, fc, ∂offset index n*HW + m}. One thread per sample,
+// in sample order: its place in its bin is the number of the bin's samples with a smaller
+// index (the bin lists are filled in atomic order, so this is what fixes the order; the
+// rank needs only independent loads of the bin's ~N entries, no sort).
+__global__ __launch_bounds__(256) void bins_rank(Geo g, int nbg, const float4* __restrict__ rec,
                                                  const int* __restrict__ start,
                                                  const int* __restrict__ list,
-                                                 int4* __restrict__ brec) {
+                                                 int4* __restrict__ brec, int* __restrict__ slist) {
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
   const int NS = g.HW * g.N, NB = (g.H + 1) * (g.W + 1);
   if (idx >= (long)nbg * NS) return;
-  const int bg = (int)(idx / NS), pos = (int)(idx - (long)bg * NS);
-  if (pos >= start[(size_t)bg * (NB + 1) + NB]) return;  // past the binned samples
-  const int sidx = list[idx];
-  const float4 R = rec[(size_t)bg * NS + sidx];
-  const int m = sidx / g.N, n = sidx - m * g.N;
-  brec[idx] = make_int4(m * g.K + n * g.C, __float_as_int(R.y), __float_as_int(R.z), n * g.HW + m);
+  const int bg = (int)(idx / NS), s = (int)(idx - (long)bg * NS);
+  const float4 R = rec[idx];
+  const int bin = __float_as_int(R.x);
+  if (bin < 0) return;
+  const int* stb = start + (size_t)bg * (NB + 1);
+  const int lo = stb[bin], hi = stb[bin + 1];
+  const int* l = list + (size_t)bg * NS;
+  int rank = 0;
+  for (int j = lo; j < hi; ++j) rank += l[j] < s;
+  const size_t pos = (size_t)bg * NS + lo + rank;
+  if (brec) {
+    const int m = s / g.N, n = s - m * g.N;
+    brec[pos] = make_int4(m * g.K + n * g.C, __float_as_int(R.y), __float_as_int(R.z),
+                          n * g.HW + m);
+  } else {
+    slist[pos] = s;
+  }
 }
 
 // ∂xT[b][r][q][gi*Cg + c] = Σ over the samples of bins (r-1,q-1), (r-1,q), (r,q-1),
@@ -951,7 +945,7 @@ static bool k5_fused(const Geo& g) {
 
 // Pointers into the bins workspace (bins_ws_bytes layout).
 struct BinsWs {
-  int *cnt, *start, *cursor, *list;
+  int *cnt, *start, *cursor, *list, *slist;
   float4* rec;
   int4* brec;
 };
@@ -969,6 +963,7 @@ static BinsWs bins_ptrs(const Geo& g, void* bins_ws, int nb) {
   P.list = reinterpret_cast<int*>(P.rec + groups * NS);
   const size_t lend = (size_t)((char*)(P.list + groups * NS) - w);
   P.brec = reinterpret_cast<int4*>(w + (lend + 15) / 16 * 16);
+  P.slist = reinterpret_cast<int*>(P.brec);  // sorted lists (non-fused K5) share that region
   return P;
 }
 
@@ -986,12 +981,12 @@ hipError_t launch_bins(const Geo& g, const float* off, void* bins_ws, float* gof
   hipLaunchKernelGGL(bins_scan, dim3((unsigned)groups), dim3(1024), 0, s, NB, P.cnt, P.start,
                      P.cursor);
   hipLaunchKernelGGL(bins_fill, dim3(gs), dim3(256), 0, s, g, P.rec, P.start, P.cursor, P.list, nb);
-  const long nbins = (long)groups * NB;
-  hipLaunchKernelGGL(bins_sort, dim3((unsigned)((nbins + 255) / 256)), dim3(256), 0, s, NB, NS,
-                     nbins, P.start, P.list);
-  if (k5_fused(g)) {
-    hipLaunchKernelGGL(bins_pack, dim3(gs), dim3(256), 0, s, g, (int)groups, P.rec, P.start,
-                       P.list, P.brec);
+  // bin order fixed by rank (r01: an insertion sort per bin took 0.83 ms beside the GEMMs):
+  // packed records for the fused K5 kernels, else a sorted list for dx_gather_cl
+  const bool fused = k5_fused(g);
+  hipLaunchKernelGGL(bins_rank, dim3(gs), dim3(256), 0, s, g, (int)groups, P.rec, P.start, P.list,
+                     fused ? P.brec : nullptr, P.slist);
+  if (fused) {
     // samples in no bin (every corner outside the image) have ∂offset 0
     e = hipMemsetAsync(goff + (size_t)b0 * g.J * g.HW, 0, (size_t)nb * g.J * g.HW * sizeof(float),
                        s);
@@ -1010,6 +1005,18 @@ static BinsWs bins_view(const Geo& g, void* bins_ws, int b0, int nb, int bins_nb
   P.start += (size_t)b0 * g.G * (NB + 1);
   P.brec += (size_t)b0 * g.G * NS;
   return P;
+}
+
+// The fused ∂x + ∂offset kernel (deform_groups 1, C % 4 == 0, C <= 256) over packed bins.
+// r01 A/B at config 3 (2-deep prefetch pipeline): U=2 0.92 ms col2im, U=4 0.93, U=8 1.50;
+// 4x6 tiles 1.05x slower, 4x8 tiles no longer unroll (2.7 ms). r02: column sweeps and
+// strips without the tile's bin-row re-read measured no faster (DESIGN.md §4 "K5").
+template <typename GT>
+static void launch_k5_fused(const Geo& g, const float* xT, const BinsWs& P, const GT* gcolT,
+                            float* gxT, float* goff, int b0, int nb, hipStream_t s) {
+  const int tr_n = (g.H + kTR - 1) / kTR, tq_n = (g.W + 4 - 1) / 4;
+  hipLaunchKernelGGL((col2im_tile<2, 4, GT>), dim3(tr_n * tq_n, 1, nb), dim3(kC2iThreads), 0, s,
+                     g, xT, P.brec, P.start, gcolT, gxT, goff, b0, tq_n);
 }
 
 hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, const float* off,
@@ -1045,24 +1052,16 @@ hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, co
     if (e != hipSuccess) return e;
   }
   const BinsWs P = bins_view(g, bins_ws, b0, nb, bins_nb);
-  if (fused) {  // one pass over ∂colT: ∂xT tiles + ∂offset of the owned bins
-    const int tr_n = (g.H + kTR - 1) / kTR;
-    auto go = [&](auto kern, int tq) {
-      const int tq_n = (g.W + tq - 1) / tq;
-      hipLaunchKernelGGL(kern, dim3(tr_n * tq_n, 1, nb), dim3(kC2iThreads), 0, s, g, xT, P.brec,
-                         P.start, gcolT, gxT, goff, b0, tq_n);
-    };
-    // r01 A/B at config 3 (2-deep prefetch pipeline): U=2 0.92 ms col2im, U=4 0.93, U=8 1.50;
-    // 4x6 tiles 1.05x slower, 4x8 tiles no longer unroll (2.7 ms)
-    go(col2im_tile<2, 4>, 4);
+  if (fused) {  // one pass over ∂colT: ∂xT + ∂offset of the owned bins
+    launch_k5_fused(g, xT, P, gcolT, gxT, goff, b0, nb, s);
   } else {  // gather ∂xT, then back to NCHW (overwrites gx for these images)
     const int pix_per_block = 4 * L.SP;
     dim3 grid((g.HWi + pix_per_block - 1) / pix_per_block, g.G, nb);
     if (v4)
-      hipLaunchKernelGGL(dx_gather_cl<4>, grid, dim3(256), 0, s, g, L, P.rec, P.start, P.list,
+      hipLaunchKernelGGL(dx_gather_cl<4>, grid, dim3(256), 0, s, g, L, P.rec, P.start, P.slist,
                          gcolT, gxT, b0);
     else
-      hipLaunchKernelGGL(dx_gather_cl<1>, grid, dim3(256), 0, s, g, L, P.rec, P.start, P.list,
+      hipLaunchKernelGGL(dx_gather_cl<1>, grid, dim3(256), 0, s, g, L, P.rec, P.start, P.slist,
                          gcolT, gxT, b0);
   }
   if (!gx) return hipGetLastError();  // caller finalises ∂x from gxT (offset-conv ∂x pass)
@@ -1103,9 +1102,7 @@ hipError_t launch_col2im_bf16(const Geo& g, const float* xT, const float* off,
     if (e != hipSuccess) return e;
   }
   const BinsWs P = bins_view(g, bins_ws, b0, nb, bins_nb);
-  const int tr_n = (g.H + kTR - 1) / kTR, tq_n = (g.W + 4 - 1) / 4;
-  hipLaunchKernelGGL((col2im_tile<2, 4, bf16_t>), dim3(tr_n * tq_n, 1, nb), dim3(kC2iThreads), 0,
-                     s, g, xT, P.brec, P.start, gcolT, gxT, goff, b0, tq_n);
+  launch_k5_fused(g, xT, P, gcolT, gxT, goff, b0, nb, s);
   if (!gx) return hipGetLastError();
   return launch_nhwc_to_nchw(gxT + (size_t)b0 * g.HWi * g.C, gx + (size_t)b0 * g.C * g.HWi, nb,
                              g.C, g.HWi, s);
