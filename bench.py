@@ -229,6 +229,8 @@ def main():
                     help="1: capture one step (libdcn launches on both of its streams, and the "
                          "all-reduce) into a HIP graph after the warmup and time its replays")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="skip the host-pointer API rate (PCIe-inclusive, reported beside value)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (default: newest profiles/r*_pmc_hbm.json)")
     ap.add_argument("--dry", action="store_true",
@@ -487,6 +489,8 @@ def main():
             "cpu_baseline": None,
             "cpu_baseline_other": None,
         }
+        if world == 1 and not bf16 and not args.no_host_path:
+            res["host_path"] = host_path_rate(cfg, args.config)
         if world == 1 and not args.no_cpu_baseline:
             # the stronger of the two CPU restatements is the reported baseline: the
             # reference's own op sequence on torch-CPU; the C/OpenMP port rides beside it
@@ -501,6 +505,52 @@ def main():
     h.close()
     if exch:
         dist.destroy_process_group()
+
+
+def host_path_rate(cfg, config, steps=4):
+    """The reference caller's path through the drop-in: DeformConv2d fwd + bwd on host (NumPy)
+    arrays, i.e. dcn_forward_host + dcn_backward_host_ex (persistent device copies, pinned
+    staging, the backward reusing its forward's columns). PCIe-inclusive, so never `value`."""
+    from deform_conv import dcn_backward_numpy, dcn_forward_numpy
+    import dcn_runtime as rt
+
+    B, C, O_, H, W, k, s, p = (cfg[n] for n in ("B", "C", "O", "H", "W", "k", "s", "p"))
+    if cfg.get("dil", 1) != 1 or cfg.get("G", 1) != 1:
+        return None
+    rng = np.random.default_rng(0)
+    N = k * k
+    x = rng.standard_normal((B, C, H, W), dtype=np.float32)
+    wo = (rng.standard_normal((2 * N, C, k, k)) / np.sqrt(C * N)).astype(np.float32)
+    bo = rng.uniform(-0.5, 0.5, 2 * N).astype(np.float32)
+    w = (rng.standard_normal((O_, C, k, k)) * np.sqrt(2 / (C * N))).astype(np.float32)
+    b = (rng.standard_normal(O_) * 0.1).astype(np.float32)
+    h = rt.Handle(0)
+    Ho, Wo = rt.out_shape(rt.make_desc(B, C, H, W, O_, (k, k), (s, s), (p, p)))
+    gout = rng.standard_normal((B, O_, Ho, Wo), dtype=np.float32)
+    fwd_only = cfg.get("fwd_only", False)
+
+    def step():
+        out, off, ctx = dcn_forward_numpy(x, wo, bo, w, b, (s, s), (p, p), handle=h,
+                                          return_ctx=True)
+        if not fwd_only:
+            dcn_backward_numpy(x, off, wo, w, True, gout, (s, s), (p, p), handle=h, ctx=ctx)
+
+    step()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    el = (time.perf_counter() - t0) / steps
+    h.close()
+    moved = (x.nbytes + gout.nbytes * (0 if fwd_only else 1) + B * O_ * Ho * Wo * 4
+             + B * 2 * N * Ho * Wo * 4 + (0 if fwd_only else x.nbytes))
+    return {"what": "host-pointer API (NumPy arrays in, NumPy arrays out): dcn_forward_host"
+                    + ("" if fwd_only else " + dcn_backward_host_ex(DCN_HOST_REUSE_FWD)"),
+            "config": f"config{config}", "steps": steps, "ms_per_step": round(el * 1e3, 3),
+            "value": round(B * Ho * Wo * N / el / 1e9, 5), "unit": "Gsamples/s",
+            "pcie_bytes_per_step": int(moved),
+            "transfers": "direct from / to the arrays (recycled resident outputs, hostmem.py)"
+                         if os.environ.get("DCN_HOST_STAGING", "0") == "0" else
+                         "pinned staging ring (DCN_HOST_STAGING=1)"}
 
 
 def spawn_ranks(n):

@@ -36,7 +36,8 @@
 extern "C" {
 #endif
 
-#define DCN_ABI_VERSION 2 /* 2: dcn_allreduce_grads takes a dtype; dcn_set_comm, dcn_set_grad_stream */
+#define DCN_ABI_VERSION 3 /* 2: dcn_allreduce_grads takes a dtype; dcn_set_comm, dcn_set_grad_stream;
+                             3: dcn_backward_host_ex */
 
 typedef enum {
   DCN_OK = 0,
@@ -144,7 +145,11 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x,
                  float* grad_b, float* grad_w_off, float* grad_b_off,
                  float* grad_off_out, void* ws, size_t ws_bytes, int flags);
 
-/* Host-pointer variants (NumPy / Jittor-CPU callers). Synchronous. */
+/* Host-pointer variants (NumPy / Jittor-CPU callers, the reference caller's path:
+ * train.py:408-414 through the module). Synchronous. Device copies of the tensors are
+ * kept on the handle between calls (no per-call allocation); transfers run straight from /
+ * to the caller's memory (env DCN_HOST_STAGING=1: through a pinned ring with host copy
+ * threads instead, which pays for destinations whose pages were never touched). */
 int dcn_forward_host(dcn_handle* h, const dcn_desc* d, const float* x,
                      const float* w_off, const float* b_off, const float* w,
                      const float* b, float* out, float* off);
@@ -153,6 +158,18 @@ int dcn_backward_host(dcn_handle* h, const dcn_desc* d, const float* x,
                       const float* grad_out, float* grad_x, float* grad_w,
                       float* grad_b, float* grad_w_off, float* grad_b_off,
                       float* grad_off_out);
+/* dcn_backward_host with flags. DCN_HOST_REUSE_FWD: x, off, w_off and w are the very
+ * arrays (same pointers, unmodified since) of the last dcn_forward_host on this handle,
+ * with the same descriptor; their device copies and the forward's sampled columns are
+ * reused instead of uploaded and recomputed (the autodiff pair of one module call,
+ * train.py:408-414). DCN_ERR_INVALID when they are not. Without the flag: as
+ * dcn_backward_host. */
+#define DCN_HOST_REUSE_FWD 2
+int dcn_backward_host_ex(dcn_handle* h, const dcn_desc* d, const float* x,
+                         const float* off, const float* w_off, const float* w,
+                         const float* grad_out, float* grad_x, float* grad_w,
+                         float* grad_b, float* grad_w_off, float* grad_b_off,
+                         float* grad_off_out, int flags);
 
 /* ---- deformable RoI pooling -------------------------------- *
  * DeformRoIPool (deform_conv.py:85-159) and DeformPSRoIPool (:162-241), fp32.

@@ -14,6 +14,7 @@
 #include <string>
 #include <vector>
 
+#include "dcn_host.h"
 #include "dcn_internal.h"
 
 using dcn::Geo;
@@ -186,6 +187,16 @@ struct dcn_handle {
   // handle-owned workspace (host-pointer API) and scratch (standalone kernel API)
   void* ws = nullptr;
   size_t ws_bytes = 0;
+  // host-pointer API: persistent device copies of the caller's tensors (grow-only, one
+  // per role), the pinned staging ring, and what the last dcn_forward_host left on the
+  // device for a dcn_backward_host_ex(DCN_HOST_REUSE_FWD)
+  void* hbuf[16] = {nullptr};
+  size_t hbuf_bytes[16] = {0};
+  dcn::HostStage* stage = nullptr;
+  int staging = -1;  // DCN_HOST_STAGING, read at the first host transfer
+  bool hfwd_valid = false;
+  dcn_desc hfwd_desc{};
+  const void *hfwd_x = nullptr, *hfwd_wo = nullptr, *hfwd_w = nullptr, *hfwd_off = nullptr;
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
   // profiling: events per kernel class
@@ -686,6 +697,9 @@ int dcn_destroy(dcn_handle* h) {
     for (hipEvent_t e : v) (void)hipEventDestroy(e);
   if (h->ws) (void)hipFree(h->ws);
   if (h->scratch) (void)hipFree(h->scratch);
+  for (void* p : h->hbuf)
+    if (p) (void)hipFree(p);
+  delete h->stage;
   if (h->aux) (void)hipStreamSynchronize(h->aux);
   dcn::gemm_engine_destroy(h->gemm);
   if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
@@ -919,7 +933,12 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
 }
 
 // ---- host-pointer variants -----------------------------------------------------
+// Persistent device copies (grow-only per role, no per-call hipMalloc/hipFree), transfers
+// staged through the handle's pinned ring (dcn_host.h), and a backward that can reuse what
+// its forward left on the device (DCN_HOST_REUSE_FWD: no x / offset / weight upload, no
+// transpose or im2col recompute: the columns stay in the handle's workspace).
 namespace {
+// per-call device buffers (RoI pooling's host variants: small tensors)
 struct DevBufs {
   std::vector<void*> ptrs;
   ~DevBufs() {
@@ -935,9 +954,34 @@ struct DevBufs {
   }
 };
 
+enum HostRole {
+  HB_X, HB_WO, HB_BO, HB_W, HB_B, HB_OUT, HB_OFF,
+  HB_GO, HB_GX, HB_GW, HB_GB, HB_GWO, HB_GBO, HB_GOFF, HB_COUNT
+};
+
+int host_buf(dcn_handle* h, int role, size_t bytes, float** p) {
+  bytes = bytes ? bytes : 4;
+  if (h->hbuf_bytes[role] < bytes) {
+    if (h->hbuf[role]) {
+      HIP_TRY(hipStreamSynchronize(h->stream));
+      HIP_TRY(hipFree(h->hbuf[role]));
+    }
+    h->hbuf[role] = nullptr;
+    h->hbuf_bytes[role] = 0;
+    HIP_TRY(hipMalloc(&h->hbuf[role], bytes));
+    h->hbuf_bytes[role] = bytes;
+  }
+  *p = static_cast<float*>(h->hbuf[role]);
+  return DCN_OK;
+}
+
 int ensure_ws(dcn_handle* h, size_t bytes) {
   if (h->ws_bytes >= bytes) return DCN_OK;
-  if (h->ws) HIP_TRY(hipFree(h->ws));
+  h->hfwd_valid = false;  // the forward's columns go with the old workspace
+  if (h->ws) {
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hipFree(h->ws));
+  }
   h->ws = nullptr;
   h->ws_bytes = 0;
   HIP_TRY(hipMalloc(&h->ws, bytes));
@@ -945,12 +989,109 @@ int ensure_ws(dcn_handle* h, size_t bytes) {
   return DCN_OK;
 }
 
+// Transfers go straight from / to the caller's pageable memory by default: on the MI355X
+// box that runs at 54 GB/s both ways when the host pages are resident (tools/pcie_probe.py;
+// pinned: 57 GB/s), and the Python shim hands out recycled, resident output arrays
+// (hostmem.py). DCN_HOST_STAGING=1 routes them through the pinned ring and copy threads
+// instead (DCN_HOST_THREADS, default 8; DCN_HOST_CHUNK_MB, default 32): that pays only for
+// destinations never touched before (page faults: 8.9 GB/s direct, 16 GB/s with 16
+// threads).
+bool staging_on(dcn_handle* h) {
+  if (h->staging < 0) {  // read once per handle, at its first host transfer
+    const char* e = std::getenv("DCN_HOST_STAGING");
+    h->staging = e && std::atoi(e) != 0 ? 1 : 0;
+  }
+  return h->staging != 0;
+}
+int get_stage(dcn_handle* h, dcn::HostStage** st) {
+  if (!h->stage) {
+    const char* t = std::getenv("DCN_HOST_THREADS");
+    const char* c = std::getenv("DCN_HOST_CHUNK_MB");
+    const int threads = t ? std::max(1, std::atoi(t)) : 8;
+    const size_t chunk = (size_t)(c ? std::max(1, std::atoi(c)) : 32) << 20;
+    auto* s = new dcn::HostStage(chunk, threads);
+    const hipError_t e = s->init();
+    if (e != hipSuccess) {
+      delete s;
+      return fail(DCN_ERR_HIP, std::string("pinned staging: ") + hipGetErrorString(e));
+    }
+    h->stage = s;
+  }
+  *st = h->stage;
+  return DCN_OK;
+}
+
 int h2d(dcn_handle* h, float* dst, const float* src, size_t bytes) {
-  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->stream));
+  if (!staging_on(h)) {
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->stream));
+    return DCN_OK;
+  }
+  dcn::HostStage* st;
+  DCN_TRY(get_stage(h, &st));
+  HIP_TRY(st->h2d(dst, src, bytes, h->stream));
   return DCN_OK;
 }
 int d2h(dcn_handle* h, float* dst, const float* src, size_t bytes) {
-  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
+  if (!staging_on(h)) {
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
+    return DCN_OK;
+  }
+  dcn::HostStage* st;
+  DCN_TRY(get_stage(h, &st));
+  HIP_TRY(st->d2h(dst, src, bytes, h->stream));
+  return DCN_OK;
+}
+
+int backward_host(dcn_handle* h, const dcn_desc* d, const float* x, const float* off,
+                  const float* w_off, const float* w, const float* grad_out, float* grad_x,
+                  float* grad_w, float* grad_b, float* grad_w_off, float* grad_b_off,
+                  float* grad_off_out, int flags) {
+  Geo g;
+  DCN_TRY(make_geo(d, &g));
+  DCN_TRY(set_device(h));
+  const bool reuse = (flags & DCN_HOST_REUSE_FWD) != 0;
+  if (reuse) {
+    if (!h->hfwd_valid || std::memcmp(&h->hfwd_desc, d, sizeof(dcn_desc)) != 0 ||
+        h->hfwd_x != x || h->hfwd_wo != w_off || h->hfwd_w != w || h->hfwd_off != off)
+      return fail(DCN_ERR_INVALID,
+                  "DCN_HOST_REUSE_FWD: not the descriptor and x / off / w_off / w arrays of the "
+                  "last dcn_forward_host on this handle");
+  }
+  const size_t nx = (size_t)g.B * g.C * g.HWi, nwo = (size_t)g.J * g.C * g.N, nw = (size_t)g.O * g.K;
+  const size_t nout = (size_t)g.B * g.O * g.HW, noff = (size_t)g.B * g.J * g.HW;
+  const size_t es = elem_bytes(g);
+  float *dx, *doff, *dwo, *dw, *dgo, *dgx, *dgw, *dgb = nullptr, *dgwo, *dgbo, *dgoff;
+  DCN_TRY(host_buf(h, HB_X, nx * es, &dx));
+  DCN_TRY(host_buf(h, HB_OFF, noff * es, &doff));
+  DCN_TRY(host_buf(h, HB_WO, nwo * es, &dwo));
+  DCN_TRY(host_buf(h, HB_W, nw * es, &dw));
+  DCN_TRY(host_buf(h, HB_GO, nout * es, &dgo));
+  DCN_TRY(host_buf(h, HB_GX, nx * es, &dgx));
+  DCN_TRY(host_buf(h, HB_GW, nw * es, &dgw));
+  if (d->has_bias) DCN_TRY(host_buf(h, HB_GB, (size_t)g.O * es, &dgb));
+  DCN_TRY(host_buf(h, HB_GWO, nwo * es, &dgwo));
+  DCN_TRY(host_buf(h, HB_GBO, (size_t)g.J * es, &dgbo));
+  DCN_TRY(host_buf(h, HB_GOFF, noff * es, &dgoff));
+  DCN_TRY(ensure_ws(h, ws_layout(g, true).total));
+  if (!reuse) {
+    h->hfwd_valid = false;  // the workspace columns are about to be rebuilt from these inputs
+    DCN_TRY(h2d(h, dx, x, nx * es));
+    DCN_TRY(h2d(h, doff, off, noff * es));
+    DCN_TRY(h2d(h, dwo, w_off, nwo * es));
+    DCN_TRY(h2d(h, dw, w, nw * es));
+  }
+  DCN_TRY(h2d(h, dgo, grad_out, nout * es));
+  DCN_TRY(dcn_backward(h, d, dx, doff, dwo, dw, dgo, dgx, dgw, dgb, dgwo, dgbo, dgoff, h->ws,
+                       h->ws_bytes, reuse ? DCN_BWD_COL_IN_WS : 0));
+  // the backward overwrites the columns with ∂columns: a second reuse needs a new forward
+  h->hfwd_valid = false;
+  DCN_TRY(d2h(h, grad_x, dgx, nx * es));
+  DCN_TRY(d2h(h, grad_w, dgw, nw * es));
+  if (d->has_bias) DCN_TRY(d2h(h, grad_b, dgb, g.O * es));
+  DCN_TRY(d2h(h, grad_w_off, dgwo, nwo * es));
+  DCN_TRY(d2h(h, grad_b_off, dgbo, g.J * es));
+  if (grad_off_out) DCN_TRY(d2h(h, grad_off_out, dgoff, noff * es));
+  HIP_TRY(hipStreamSynchronize(h->stream));
   return DCN_OK;
 }
 }  // namespace
@@ -960,29 +1101,36 @@ int dcn_forward_host(dcn_handle* h, const dcn_desc* d, const float* x, const flo
   Geo g;
   DCN_TRY(make_geo(d, &g));
   DCN_TRY(set_device(h));
+  if (!out) return fail(DCN_ERR_INVALID, "dcn_forward_host: out is required");
+  h->hfwd_valid = false;
   const size_t nx = (size_t)g.B * g.C * g.HWi, nwo = (size_t)g.J * g.C * g.N, nw = (size_t)g.O * g.K;
   const size_t nout = (size_t)g.B * g.O * g.HW, noff = (size_t)g.B * g.J * g.HW;
   const size_t es = elem_bytes(g);
-  DevBufs db;
   float *dx, *dwo, *dbo, *dw, *db_ = nullptr, *dout, *doff;
-  DCN_TRY(db.alloc(nx * es, &dx));
-  DCN_TRY(db.alloc(nwo * es, &dwo));
-  DCN_TRY(db.alloc((size_t)g.J * es, &dbo));
-  DCN_TRY(db.alloc(nw * es, &dw));
-  if (d->has_bias) DCN_TRY(db.alloc((size_t)g.O * es, &db_));
-  DCN_TRY(db.alloc(nout * es, &dout));
-  DCN_TRY(db.alloc(noff * es, &doff));
+  DCN_TRY(host_buf(h, HB_X, nx * es, &dx));
+  DCN_TRY(host_buf(h, HB_WO, nwo * es, &dwo));
+  DCN_TRY(host_buf(h, HB_BO, (size_t)g.J * es, &dbo));
+  DCN_TRY(host_buf(h, HB_W, nw * es, &dw));
+  if (d->has_bias) DCN_TRY(host_buf(h, HB_B, (size_t)g.O * es, &db_));
+  DCN_TRY(host_buf(h, HB_OUT, nout * es, &dout));
+  DCN_TRY(host_buf(h, HB_OFF, noff * es, &doff));
+  // sized for the backward too, so a DCN_HOST_REUSE_FWD backward finds the columns in place
+  DCN_TRY(ensure_ws(h, ws_layout(g, true).total));
   DCN_TRY(h2d(h, dx, x, nx * es));
   DCN_TRY(h2d(h, dwo, w_off, nwo * es));
   DCN_TRY(h2d(h, dbo, b_off, g.J * es));
   DCN_TRY(h2d(h, dw, w, nw * es));
   if (d->has_bias) DCN_TRY(h2d(h, db_, b, g.O * es));
-  const size_t wsb = ws_layout(g, false).total;
-  DCN_TRY(ensure_ws(h, wsb));
   DCN_TRY(dcn_forward(h, d, dx, dwo, dbo, dw, db_, dout, doff, h->ws, h->ws_bytes));
   DCN_TRY(d2h(h, out, dout, nout * es));
   if (off) DCN_TRY(d2h(h, off, doff, noff * es));
   HIP_TRY(hipStreamSynchronize(h->stream));
+  h->hfwd_valid = off != nullptr;  // a reusing backward names the offsets it was given
+  h->hfwd_desc = *d;
+  h->hfwd_x = x;
+  h->hfwd_wo = w_off;
+  h->hfwd_w = w;
+  h->hfwd_off = off;
   return DCN_OK;
 }
 
@@ -990,42 +1138,17 @@ int dcn_backward_host(dcn_handle* h, const dcn_desc* d, const float* x, const fl
                       const float* w_off, const float* w, const float* grad_out, float* grad_x,
                       float* grad_w, float* grad_b, float* grad_w_off, float* grad_b_off,
                       float* grad_off_out) {
-  Geo g;
-  DCN_TRY(make_geo(d, &g));
-  DCN_TRY(set_device(h));
-  const size_t nx = (size_t)g.B * g.C * g.HWi, nwo = (size_t)g.J * g.C * g.N, nw = (size_t)g.O * g.K;
-  const size_t nout = (size_t)g.B * g.O * g.HW, noff = (size_t)g.B * g.J * g.HW;
-  const size_t es = elem_bytes(g);
-  DevBufs db;
-  float *dx, *doff, *dwo, *dw, *dgo, *dgx, *dgw, *dgb = nullptr, *dgwo, *dgbo, *dgoff;
-  DCN_TRY(db.alloc(nx * es, &dx));
-  DCN_TRY(db.alloc(noff * es, &doff));
-  DCN_TRY(db.alloc(nwo * es, &dwo));
-  DCN_TRY(db.alloc(nw * es, &dw));
-  DCN_TRY(db.alloc(nout * es, &dgo));
-  DCN_TRY(db.alloc(nx * es, &dgx));
-  DCN_TRY(db.alloc(nw * es, &dgw));
-  if (d->has_bias) DCN_TRY(db.alloc((size_t)g.O * es, &dgb));
-  DCN_TRY(db.alloc(nwo * es, &dgwo));
-  DCN_TRY(db.alloc((size_t)g.J * es, &dgbo));
-  DCN_TRY(db.alloc(noff * es, &dgoff));
-  DCN_TRY(h2d(h, dx, x, nx * es));
-  DCN_TRY(h2d(h, doff, off, noff * es));
-  DCN_TRY(h2d(h, dwo, w_off, nwo * es));
-  DCN_TRY(h2d(h, dw, w, nw * es));
-  DCN_TRY(h2d(h, dgo, grad_out, nout * es));
-  const size_t wsb = ws_layout(g, true).total;
-  DCN_TRY(ensure_ws(h, wsb));
-  DCN_TRY(dcn_backward(h, d, dx, doff, dwo, dw, dgo, dgx, dgw, dgb, dgwo, dgbo, dgoff, h->ws,
-                       h->ws_bytes, 0));
-  DCN_TRY(d2h(h, grad_x, dgx, nx * es));
-  DCN_TRY(d2h(h, grad_w, dgw, nw * es));
-  if (d->has_bias) DCN_TRY(d2h(h, grad_b, dgb, g.O * es));
-  DCN_TRY(d2h(h, grad_w_off, dgwo, nwo * es));
-  DCN_TRY(d2h(h, grad_b_off, dgbo, g.J * es));
-  if (grad_off_out) DCN_TRY(d2h(h, grad_off_out, dgoff, noff * es));
-  HIP_TRY(hipStreamSynchronize(h->stream));
-  return DCN_OK;
+  return backward_host(h, d, x, off, w_off, w, grad_out, grad_x, grad_w, grad_b, grad_w_off,
+                       grad_b_off, grad_off_out, 0);
+}
+
+int dcn_backward_host_ex(dcn_handle* h, const dcn_desc* d, const float* x, const float* off,
+                         const float* w_off, const float* w, const float* grad_out,
+                         float* grad_x, float* grad_w, float* grad_b, float* grad_w_off,
+                         float* grad_b_off, float* grad_off_out, int flags) {
+  if (flags & ~DCN_HOST_REUSE_FWD) return fail(DCN_ERR_INVALID, "unknown dcn_backward_host_ex flag");
+  return backward_host(h, d, x, off, w_off, w, grad_out, grad_x, grad_w, grad_b, grad_w_off,
+                       grad_b_off, grad_off_out, flags);
 }
 
 // ---- profiling ------------------------------------------------------------------

@@ -14,7 +14,8 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DCN_LIB", os.path.join(HERE, "lib", "libdcn.so"))
 
-ABI_VERSION = 2  # include/dcn.h DCN_ABI_VERSION
+ABI_VERSION = 3  # include/dcn.h DCN_ABI_VERSION
+HOST_REUSE_FWD = 2  # include/dcn.h DCN_HOST_REUSE_FWD
 DCN_F32, DCN_BF16 = 0, 1
 DCN_BWD_COL_IN_WS = 1
 DCN_FWD_AUTO, DCN_FWD_UNFUSED, DCN_FWD_FUSED = 0, 1, 2
@@ -72,6 +73,8 @@ SIGNATURES = {
                      ctypes.c_int],
     "dcn_forward_host": [_vp, _dp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "dcn_backward_host": [_vp, _dp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "dcn_backward_host_ex": [_vp, _dp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                             ctypes.c_int],
     "dcn_prof_enable": [_vp, ctypes.c_int],
     "dcn_prof_read": [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), _ip],
     "dcn_prof_reset": [_vp],
@@ -177,6 +180,9 @@ class Handle:
         check(self.lib.dcn_create(int(device), ctypes.byref(h)), "dcn_create")
         self.h = h
         self.device = device
+        # host-pointer API: bumped by every dcn_forward_host / dcn_backward_host call, so a
+        # backward knows whether its forward's device state is still the handle's latest
+        self.host_seq = 0
 
     def close(self):
         if getattr(self, "h", None):

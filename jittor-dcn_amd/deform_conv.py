@@ -34,6 +34,7 @@ import math
 import numpy as np
 
 import dcn_runtime as rt
+import hostmem
 
 try:  # pragma: no cover - Jittor is not installable in the build image
     import jittor as jt
@@ -52,8 +53,27 @@ def _f32(a):
     return np.ascontiguousarray(a, dtype=np.float32)
 
 
-def dcn_forward_numpy(x, w_off, b_off, w, b, stride, padding, handle=None):
-    """out, off = DeformConv2d.execute on host arrays (one libdcn call)."""
+class HostFwdCtx:
+    """What a dcn_backward_numpy needs to reuse its forward's device state (libdcn's
+    DCN_HOST_REUSE_FWD): the exact arrays the forward uploaded and the handle's call
+    sequence number at the time. Reuse happens only when no other host call ran since."""
+
+    __slots__ = ("handle", "seq", "arrays")
+
+    def __init__(self, handle, seq, x, w_off, w, off):
+        # the arrays themselves stay referenced (their memory cannot be recycled meanwhile);
+        # they are matched by data pointer, as the library checks them
+        self.handle, self.seq, self.arrays = handle, seq, (x, w_off, w, off)
+
+    def matches(self, h, x, w_off, w, off):
+        return (self.handle is h and self.seq == h.host_seq
+                and all(a.ctypes.data == b.ctypes.data and a.shape == b.shape
+                        for a, b in zip(self.arrays, (x, w_off, w, off))))
+
+
+def dcn_forward_numpy(x, w_off, b_off, w, b, stride, padding, handle=None, return_ctx=False):
+    """out, off = DeformConv2d.execute on host arrays (one libdcn call). With return_ctx,
+    also a HostFwdCtx for dcn_backward_numpy(ctx=...)."""
     h = handle or rt.default_handle()
     x, w_off, b_off, w = _f32(x), _f32(w_off), _f32(b_off), _f32(w)
     b = None if b is None else _f32(b)
@@ -67,16 +87,22 @@ def dcn_forward_numpy(x, w_off, b_off, w, b, stride, padding, handle=None):
                 np.empty((0, w_off.shape[0], Ho, Wo), np.float32))
     desc = rt.make_desc(B, C, H, W, O, (kh, kw), stride, padding, bias=b is not None)
     Ho, Wo = rt.out_shape(desc)
-    out = np.empty((B, O, Ho, Wo), np.float32)
-    off = np.empty((B, w_off.shape[0], Ho, Wo), np.float32)
+    out = hostmem.empty((B, O, Ho, Wo))
+    off = hostmem.empty((B, w_off.shape[0], Ho, Wo))
+    h.host_seq += 1
     rt.check(h.lib.dcn_forward_host(h.h, desc, rt.ptr(x), rt.ptr(w_off), rt.ptr(b_off), rt.ptr(w),
                                     rt.ptr(b), rt.ptr(out), rt.ptr(off)), "dcn_forward_host")
+    if return_ctx:
+        return out, off, HostFwdCtx(h, h.host_seq, x, w_off, w, off)
     return out, off
 
 
-def dcn_backward_numpy(x, off, w_off, w, has_bias, grad_out, stride, padding, handle=None):
-    """Grads of DeformConv2d.execute (dict keyed like the state dict, plus 'x', 'offset')."""
-    h = handle or rt.default_handle()
+def dcn_backward_numpy(x, off, w_off, w, has_bias, grad_out, stride, padding, handle=None,
+                       ctx=None):
+    """Grads of DeformConv2d.execute (dict keyed like the state dict, plus 'x', 'offset').
+    ctx: the forward's HostFwdCtx; when nothing else ran on the handle since, x / off /
+    weights are not uploaded again and the forward's columns are reused."""
+    h = handle or (ctx.handle if ctx is not None else rt.default_handle())
     x, off, w_off, w, grad_out = map(_f32, (x, off, w_off, w, grad_out))
     B, C, H, W = x.shape
     O, _, kh, kw = w.shape
@@ -89,15 +115,19 @@ def dcn_backward_numpy(x, off, w_off, w, has_bias, grad_out, stride, padding, ha
             g["bias"] = np.zeros(O, np.float32)
         return g
     desc = rt.make_desc(B, C, H, W, O, (kh, kw), stride, padding, bias=has_bias)
-    g = {"x": np.empty_like(x), "weight": np.empty_like(w),
-         "offset_conv.weight": np.empty_like(w_off),
-         "offset_conv.bias": np.empty(w_off.shape[0], np.float32), "offset": np.empty_like(off)}
+    g = {"x": hostmem.empty_like(x), "weight": hostmem.empty_like(w),
+         "offset_conv.weight": hostmem.empty_like(w_off),
+         "offset_conv.bias": np.empty(w_off.shape[0], np.float32),
+         "offset": hostmem.empty_like(off)}
     gb = np.empty(O, np.float32) if has_bias else None
-    rt.check(h.lib.dcn_backward_host(h.h, desc, rt.ptr(x), rt.ptr(off), rt.ptr(w_off), rt.ptr(w),
-                                     rt.ptr(grad_out), rt.ptr(g["x"]), rt.ptr(g["weight"]),
-                                     rt.ptr(gb), rt.ptr(g["offset_conv.weight"]),
-                                     rt.ptr(g["offset_conv.bias"]), rt.ptr(g["offset"])),
-             "dcn_backward_host")
+    flags = rt.HOST_REUSE_FWD if ctx is not None and ctx.matches(h, x, w_off, w, off) else 0
+    h.host_seq += 1
+    rt.check(h.lib.dcn_backward_host_ex(h.h, desc, rt.ptr(x), rt.ptr(off), rt.ptr(w_off),
+                                        rt.ptr(w), rt.ptr(grad_out), rt.ptr(g["x"]),
+                                        rt.ptr(g["weight"]), rt.ptr(gb),
+                                        rt.ptr(g["offset_conv.weight"]),
+                                        rt.ptr(g["offset_conv.bias"]), rt.ptr(g["offset"]),
+                                        flags), "dcn_backward_host_ex")
     if has_bias:
         g["bias"] = gb
     return g
@@ -261,18 +291,19 @@ class DeformConv2dNumpy(Module):
 
     def execute(self, x):
         x = _f32(x)
-        out, off = dcn_forward_numpy(x, self.offset_conv.weight, self.offset_conv.bias,
-                                     self.weight, self.bias, self.stride, self.padding)
-        self._ctx = (x, off) if self.training else None
+        out, off, hctx = dcn_forward_numpy(x, self.offset_conv.weight, self.offset_conv.bias,
+                                           self.weight, self.bias, self.stride, self.padding,
+                                           return_ctx=True)
+        self._ctx = (x, off, hctx) if self.training else None
         return out
 
     def backward(self, grad_out):
         """Accumulate parameter grads (.grad) and return ∂L/∂x."""
         if self._ctx is None:
             raise RuntimeError("backward() needs a preceding execute() in training mode")
-        x, off = self._ctx
+        x, off, hctx = self._ctx
         g = dcn_backward_numpy(x, off, self.offset_conv.weight, self.weight, self.bias is not None,
-                               grad_out, self.stride, self.padding)
+                               grad_out, self.stride, self.padding, ctx=hctx)
         for name, p in self.named_parameters():
             p.grad = g[name] if p.grad is None else p.grad + g[name]
         return g["x"]
@@ -353,15 +384,17 @@ if HAVE_JITTOR:  # pragma: no cover
             self.stride, self.padding = stride, padding
             self.has_bias = b is not None
             xn, won, wn = x.numpy(), w_off.numpy(), w.numpy()
-            out, off = dcn_forward_numpy(xn, won, b_off.numpy(), wn,
-                                         None if b is None else b.numpy(), stride, padding)
-            self.saved = (xn, off, won, wn)
+            xn, won, wn = _f32(xn), _f32(won), _f32(wn)
+            out, off, hctx = dcn_forward_numpy(xn, won, b_off.numpy(), wn,
+                                               None if b is None else b.numpy(), stride, padding,
+                                               return_ctx=True)
+            self.saved = (xn, off, won, wn, hctx)
             return jt.array(out)
 
         def grad(self, grad_out):
-            xn, off, won, wn = self.saved
+            xn, off, won, wn, hctx = self.saved
             g = dcn_backward_numpy(xn, off, won, wn, self.has_bias, grad_out.numpy(),
-                                   self.stride, self.padding)
+                                   self.stride, self.padding, ctx=hctx)
             gb = jt.array(g["bias"]) if self.has_bias else None
             return (jt.array(g["x"]), jt.array(g["offset_conv.weight"]),
                     jt.array(g["offset_conv.bias"]), jt.array(g["weight"]), gb, None, None)
@@ -446,4 +479,5 @@ else:
 
 __all__ = ["DeformConv2d", "DeformConv2dNumpy", "DeformRoIPool", "DeformRoIPoolNumpy",
            "DeformPSRoIPool", "DeformPSRoIPoolNumpy", "dcn_forward_numpy", "dcn_backward_numpy",
+           "HostFwdCtx",
            "roi_pool_forward_numpy", "roi_pool_backward_numpy", "HAVE_JITTOR"]

@@ -1,0 +1,73 @@
+"""Recycled host arrays for the host-pointer path (the NumPy / Jittor-CPU caller).
+
+Every dcn_forward_host / dcn_backward_host call returns new arrays (out, offsets, grads),
+as the reference's ops return new Vars. Fresh NumPy memory is not resident yet: the DMA of
+a device result into it runs at the page-fault rate, 8.9 GB/s on the MI355X box against
+54 GB/s into resident pages (tools/pcie_probe.py). So output arrays come from this pool:
+each is a view of a resident block, and the block returns to the pool once nothing
+references it any more (a weakref finalizer on the block's owner object, which every view
+of the array keeps alive), so the next call of the same shape writes into resident memory.
+The arrays behave as ordinary, independent ndarrays to the caller.
+"""
+from __future__ import annotations
+
+import threading
+import weakref
+
+import numpy as np
+
+_KEEP = 4  # free blocks kept per size
+
+
+class _Block:
+    """Owner object of one pooled array: numpy takes its memory through the array interface
+    (the array's .base), so it lives exactly as long as some view of the memory does."""
+
+    __slots__ = ("__array_interface__", "__weakref__")
+
+
+class HostPool:
+    def __init__(self, keep=_KEEP):
+        self.keep = keep
+        self._free: dict[int, list[np.ndarray]] = {}
+        self._lock = threading.Lock()
+
+    def empty(self, shape, dtype=np.float32) -> np.ndarray:
+        dtype = np.dtype(dtype)
+        shape = tuple(int(s) for s in shape)
+        nbytes = int(np.prod(shape, dtype=np.int64)) * dtype.itemsize
+        if nbytes < (1 << 20):  # small: no pooling
+            return np.empty(shape, dtype)
+        with self._lock:
+            lst = self._free.get(nbytes)
+            store = lst.pop() if lst else None
+        if store is None:
+            store = np.empty(nbytes, np.uint8)
+            store[::4096] = 0  # make every page resident once
+        blk = _Block()
+        blk.__array_interface__ = {"shape": shape, "typestr": dtype.str,
+                                   "data": (store.ctypes.data, False), "version": 3}
+        arr = np.asarray(blk)
+        weakref.finalize(blk, self._release, nbytes, store)
+        return arr
+
+    def _release(self, nbytes, store):
+        with self._lock:
+            lst = self._free.setdefault(nbytes, [])
+            if len(lst) < self.keep:
+                lst.append(store)
+
+    def clear(self):
+        with self._lock:
+            self._free.clear()
+
+
+POOL = HostPool()
+
+
+def empty(shape, dtype=np.float32) -> np.ndarray:
+    return POOL.empty(shape, dtype)
+
+
+def empty_like(a) -> np.ndarray:
+    return POOL.empty(np.shape(a), np.asarray(a).dtype)

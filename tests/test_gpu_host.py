@@ -1,0 +1,135 @@
+"""The host-pointer API (dcn_forward_host / dcn_backward_host[_ex]): the NumPy / Jittor-CPU
+caller's path (train.py:408-414 through the module), on libdcn.
+
+Pinned here:
+  * staged transfers (pinned ring, host copy threads) move every byte: results equal the
+    oracle, also with a chunk size that splits every tensor into ragged pieces;
+  * DCN_HOST_REUSE_FWD (the backward reusing its forward's device copies and columns) gives
+    bitwise the gradients of a backward that uploads and recomputes everything;
+  * reuse is refused (DCN_ERR_INVALID) for arrays that are not the forward's, and the Python
+    shim falls back to a full upload when another host call ran in between (two layers).
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import dcn_oracle as O
+import dcn_runtime as rt
+from conftest import assert_close, assert_close_reduction
+from deform_conv import DeformConv2dNumpy, dcn_backward_numpy, dcn_forward_numpy
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(seed, B=2, C=16, O_=12, H=13, W=11, s=(1, 1)):
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    wo = (rng.standard_normal((18, C, 3, 3)) / np.sqrt(C * 9)).astype(np.float32)
+    bo = rng.uniform(-0.5, 0.5, 18).astype(np.float32)
+    w = (rng.standard_normal((O_, C, 3, 3)) * np.sqrt(2 / (C * 9))).astype(np.float32)
+    b = (rng.standard_normal(O_) * 0.1).astype(np.float32)
+    Ho, Wo = O.out_size(H, W, 3, 3, *s, 1, 1, 1, 1)
+    gout = rng.standard_normal((B, O_, Ho, Wo)).astype(np.float32)
+    return x, wo, bo, w, b, gout, s
+
+
+def _grads_equal(a, b):
+    assert a.keys() == b.keys()
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+def test_host_reuse_bitwise_equals_full_upload():
+    h = rt.Handle(0)
+    x, wo, bo, w, b, gout, s = _case(1)
+    out, off, ctx = dcn_forward_numpy(x, wo, bo, w, b, s, (1, 1), handle=h, return_ctx=True)
+    g_reuse = dcn_backward_numpy(x, off, wo, w, True, gout, s, (1, 1), handle=h, ctx=ctx)
+    g_full = dcn_backward_numpy(x, off, wo, w, True, gout, s, (1, 1), handle=h)
+    _grads_equal(g_reuse, g_full)
+    ro, roff, cache = O.forward(x, wo, bo, w, b, s, (1, 1))
+    assert_close(out, ro, what="out")
+    _, _, cache = O.forward(x, wo, bo, w, b, s, (1, 1), offsets=off)
+    rg = O.backward(cache, gout)
+    assert_close(g_reuse["x"], rg["x"], what="∂x")
+    for k in ("weight", "bias", "offset_conv.weight", "offset_conv.bias"):
+        assert_close_reduction(g_reuse[k], rg[k], what=k)
+    h.close()
+
+
+def test_host_reuse_refused_for_other_arrays():
+    h = rt.Handle(0)
+    x, wo, bo, w, b, gout, s = _case(2)
+    out, off = dcn_forward_numpy(x, wo, bo, w, b, s, (1, 1), handle=h)
+    desc = rt.make_desc(*x.shape, w.shape[0], (3, 3), s, (1, 1), bias=True)
+    x2 = x.copy()  # same values, another array: the library cannot vouch for it
+    bufs = [np.empty_like(x), np.empty_like(w), np.empty(w.shape[0], np.float32),
+            np.empty_like(wo), np.empty(18, np.float32), np.empty_like(off)]
+    r = h.lib.dcn_backward_host_ex(h.h, desc, rt.ptr(x2), rt.ptr(off), rt.ptr(wo), rt.ptr(w),
+                                   rt.ptr(gout), *[rt.ptr(a) for a in bufs], rt.HOST_REUSE_FWD)
+    assert r == -1  # DCN_ERR_INVALID
+    assert b"DCN_HOST_REUSE_FWD" in h.lib.dcn_last_error()
+    # the same call on the forward's own arrays is accepted
+    r = h.lib.dcn_backward_host_ex(h.h, desc, rt.ptr(x), rt.ptr(off), rt.ptr(wo), rt.ptr(w),
+                                   rt.ptr(gout), *[rt.ptr(a) for a in bufs], rt.HOST_REUSE_FWD)
+    assert r == 0
+    # ... once: the backward consumed the forward's columns
+    r = h.lib.dcn_backward_host_ex(h.h, desc, rt.ptr(x), rt.ptr(off), rt.ptr(wo), rt.ptr(w),
+                                   rt.ptr(gout), *[rt.ptr(a) for a in bufs], rt.HOST_REUSE_FWD)
+    assert r == -1
+    h.close()
+
+
+def test_two_layers_share_a_handle():
+    """Layer 1's backward runs after layer 2's forward and backward: its context is stale, so
+    the shim uploads again (no reuse) and the gradients stay right."""
+    h = rt.Handle(0)
+    x, wo, bo, w, b, gout, s = _case(3)
+    x2, wo2, bo2, w2, b2, gout2, _ = _case(4)
+    out1, off1, c1 = dcn_forward_numpy(x, wo, bo, w, b, s, (1, 1), handle=h, return_ctx=True)
+    out2, off2, c2 = dcn_forward_numpy(x2, wo2, bo2, w2, b2, s, (1, 1), handle=h, return_ctx=True)
+    assert not c1.matches(h, x, wo, w, off1) and c2.matches(h, x2, wo2, w2, off2)
+    g2 = dcn_backward_numpy(x2, off2, wo2, w2, True, gout2, s, (1, 1), handle=h, ctx=c2)
+    g1 = dcn_backward_numpy(x, off1, wo, w, True, gout, s, (1, 1), handle=h, ctx=c1)
+    g1_ref = dcn_backward_numpy(x, off1, wo, w, True, gout, s, (1, 1), handle=h)
+    _grads_equal(g1, g1_ref)
+    g2_ref = dcn_backward_numpy(x2, off2, wo2, w2, True, gout2, s, (1, 1), handle=h)
+    _grads_equal(g2, g2_ref)
+    h.close()
+
+
+def test_module_backward_reuses_forward():
+    m = DeformConv2dNumpy(16, 12, 3, 1, 1, seed=5)
+    rng = np.random.default_rng(5)
+    m.offset_conv.weight[...] = rng.standard_normal(m.offset_conv.weight.shape) * 0.05
+    x = rng.standard_normal((2, 16, 10, 12)).astype(np.float32)
+    out = m(x)
+    gout = rng.standard_normal(out.shape).astype(np.float32)
+    gx = m.backward(gout)
+    _, _, cache = O.forward(x, m.offset_conv.weight, m.offset_conv.bias, m.weight, m.bias,
+                            (1, 1), (1, 1), offsets=m._ctx[1])
+    rg = O.backward(cache, gout)
+    assert_close(gx, rg["x"], what="module ∂x")
+    assert_close_reduction(m.weight.grad, rg["weight"], what="module ∂W")
+
+
+@pytest.mark.parametrize("chunk_mb,threads", [(1, 3), (1, 1)])
+def test_staging_ragged_chunks(monkeypatch, chunk_mb, threads):
+    """Pinned staging (DCN_HOST_STAGING=1) with 1-MiB chunks and 1 or 3 copy threads: x
+    (2.4 MiB), out, ∂x all split into ragged pieces; results equal the direct transfers'."""
+    x, wo, bo, w, b, gout, s = _case(6, B=3, C=32, O_=24, H=61, W=109, s=(1, 1))
+    h0 = rt.Handle(0)
+    out0, off0 = dcn_forward_numpy(x, wo, bo, w, b, s, (1, 1), handle=h0)
+    g0 = dcn_backward_numpy(x, off0, wo, w, True, gout, s, (1, 1), handle=h0)
+    h0.close()
+    monkeypatch.setenv("DCN_HOST_STAGING", "1")
+    monkeypatch.setenv("DCN_HOST_CHUNK_MB", str(chunk_mb))
+    monkeypatch.setenv("DCN_HOST_THREADS", str(threads))
+    h = rt.Handle(0)  # staging is created with the handle's first host transfer
+    out, off, ctx = dcn_forward_numpy(x, wo, bo, w, b, s, (1, 1), handle=h, return_ctx=True)
+    g = dcn_backward_numpy(x, off, wo, w, True, gout, s, (1, 1), handle=h, ctx=ctx)
+    np.testing.assert_array_equal(out, out0)
+    np.testing.assert_array_equal(off, off0)
+    _grads_equal(g, g0)
+    h.close()

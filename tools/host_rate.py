@@ -25,16 +25,20 @@ def main(steps=5):
     b = (rng.standard_normal(O_) * 0.1).astype(np.float32)
     gout = rng.standard_normal((B, O_, H, W), dtype=np.float32)
 
+    reuse = os.environ.get("HOST_REUSE", "1") != "0"
+
     def step():
-        out, off = dcn_forward_numpy(x, wo, bo, w, b, (1, 1), (1, 1))
-        dcn_backward_numpy(x, off, wo, w, True, gout, (1, 1), (1, 1))
+        out, off, ctx = dcn_forward_numpy(x, wo, bo, w, b, (1, 1), (1, 1), return_ctx=True)
+        dcn_backward_numpy(x, off, wo, w, True, gout, (1, 1), (1, 1), ctx=ctx if reuse else None)
 
     step()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     el = (time.perf_counter() - t0) / steps
-    print(json.dumps({"what": "host-pointer API fwd+bwd incl. PCIe + host allocation",
+    print(json.dumps({"what": "host-pointer API fwd+bwd incl. PCIe", "reuse_fwd": reuse,
+                      "staging": os.environ.get("DCN_HOST_STAGING", "0"),
+                      "threads": os.environ.get("DCN_HOST_THREADS", "8"),
                       "config": "config3", "ms_per_step": round(el * 1e3, 2),
                       "Gsamples_per_s": round(B * H * W * 9 / el / 1e9, 5)}))
 
