@@ -290,6 +290,20 @@ int dcn_get_math(dcn_handle* h, int* math);
 typedef enum { DCN_FWD_AUTO = 0, DCN_FWD_UNFUSED = 1, DCN_FWD_FUSED = 2 } dcn_fwd_path;
 int dcn_set_fwd_path(dcn_handle* h, int path);
 
+/* ---- development A/B knobs ------------------------------------------------------ *
+ * Env DCN_EXP="v0,v1,..." (read once per process; unset = all 0 = the measured defaults)
+ * switches between implementations of the same math for speed experiments; results agree
+ * to fp32 rounding (only summation orders change). Each alternative is measured in
+ * DESIGN.md §4. Slots:
+ *   2  1: fp32 K5 as two kernels (offgrad_cl + dx_gather_cl) instead of col2im_tile
+ *   4  1: offset conv forward on the per-pixel VALU kernel instead of the 2-px row kernel
+ *   5  1 / 2: split-bf16 GEMM form EARLY / LATE (default: picked per shape)
+ *   6  1: offset conv backward on the VALU kernels instead of the MFMA ones
+ *   7  n > 0: output rows per wave of the VALU ∂w_off kernel (default 4)
+ *   8  1: fused forward workgroup shape 0 (4 waves x 2 per CU) instead of shape 1
+ *   9  n > 0: bf16/fp32 ∂W as n grouped GEMMs; n < 0: one GEMM per image
+ * Slots 0, 1, 3 and 10-15 are unused. */
+
 /* ---- testing ------------------------------------------------------------------ */
 /* One fp32 GEMM through the handle's engine under its current math mode, BLAS
  * column-major convention: C(m×n) = op(A)·op(B), batched by element strides. */

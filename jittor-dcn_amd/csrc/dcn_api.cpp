@@ -113,7 +113,9 @@ struct WsLayout {
   size_t bins = 0;   // sample bins of K5b
   // DCN_BF16 only: fp32 working copies (the offset conv, coordinates and reductions run
   // in fp32; only the columns and the GEMM operands are bf16)
-  size_t x32 = 0, woff32 = 0, boff32 = 0, b32 = 0, off32 = 0, out32 = 0;
+  // (DCN_BF16 keeps its channels-last x in `xT` as bf16; xT32 is the fp32 one that only the
+  // VALU offset-conv fallbacks read, wb16 the bf16 weights of the MFMA offset conv)
+  size_t x32 = 0, xT32 = 0, wb16 = 0, woff32 = 0, boff32 = 0, b32 = 0, off32 = 0, out32 = 0;
   size_t gout32 = 0, gx32 = 0, gw32 = 0, gb32 = 0, gwo32 = 0, gbo32 = 0, goff32 = 0;
   size_t total = 0;
 };
@@ -136,6 +138,8 @@ WsLayout ws_layout(const Geo& g, bool bwd) {
     // forward+backward layouts: a backward with DCN_BWD_COL_IN_WS reads what the forward
     // (which always uses the forward-only layout) wrote
     L.x32 = take((size_t)g.B * g.C * g.HWi * f);
+    L.xT32 = take((size_t)g.B * g.C * g.HWi * f);  // fp32 channels-last x (VALU fallbacks)
+    L.wb16 = take(dcn::offset_fwd_bf16_wb_elems(g) * sizeof(dcn::bf16_t));
     L.woff32 = take((size_t)g.J * g.C * g.N * f);
     L.boff32 = take((size_t)g.J * f);
     L.b32 = take((size_t)g.O * f);
@@ -493,23 +497,30 @@ int forward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x,
                  const bf16_t* w_off, const bf16_t* b_off, const bf16_t* w, const bf16_t* b,
                  bf16_t* out, bf16_t* off, char* base, const WsLayout& L) {
   hipStream_t st = h->stream;
-  float *x32 = F32(L.x32), *xT = F32(L.xT), *off32 = F32(L.off32), *out32 = F32(L.out32);
-  HIP_TRY(dcn::launch_bf16_to_f32(x, x32, (size_t)g.B * g.C * g.HWi, st));
-  HIP_TRY(dcn::launch_bf16_to_f32(w_off, F32(L.woff32), (size_t)g.J * g.C * g.N, st));
+  bf16_t* xT = BF(L.xT);  // channels-last bf16 x: K1, K5 and the offset conv read it
+  float *off32 = F32(L.off32), *out32 = F32(L.out32);
   HIP_TRY(dcn::launch_bf16_to_f32(b_off, F32(L.boff32), (size_t)g.J, st));
   if (has_bias) HIP_TRY(dcn::launch_bf16_to_f32(b, F32(L.b32), (size_t)g.O, st));
-  DCN_TRY(fork_aux(h));
   {
-    ProfScope ps(h, DCN_K_XPOSE, h->aux);
-    HIP_TRY(dcn::launch_nchw_to_nhwc(x32, xT, g.B, g.C, g.HWi, h->aux));
+    ProfScope ps(h, DCN_K_XPOSE);
+    HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(x, xT, g.B, g.C, g.HWi, st));
   }
   {
     ProfScope ps(h, DCN_K_OFFSET_FWD);
-    HIP_TRY(dcn::launch_offset_conv_fwd(g, x32, F32(L.woff32), F32(L.boff32), off32, F32(L.wt),
-                                        F32(L.part), st));
-    HIP_TRY(dcn::launch_round_to_bf16(off32, off, (size_t)g.B * g.J * g.HW, st));
+    if (dcn::offset_fwd_mfma_bf16_ok(g)) {
+      // bf16 MFMA straight from the bf16 xT: the offsets, rounded to bf16 (off) and as
+      // fp32 values (off32, what the sampling uses)
+      HIP_TRY(dcn::launch_offset_conv_fwd_bf16(g, xT, w_off, F32(L.boff32), off32, off,
+                                               BF(L.wb16), st));
+    } else {  // fp32 VALU kernels on an fp32 copy of x
+      float* x32 = F32(L.x32);
+      HIP_TRY(dcn::launch_bf16_to_f32(x, x32, (size_t)g.B * g.C * g.HWi, st));
+      HIP_TRY(dcn::launch_bf16_to_f32(w_off, F32(L.woff32), (size_t)g.J * g.C * g.N, st));
+      HIP_TRY(dcn::launch_offset_conv_fwd(g, x32, F32(L.woff32), F32(L.boff32), off32, F32(L.wt),
+                                          F32(L.part), st));
+      HIP_TRY(dcn::launch_round_to_bf16(off32, off, (size_t)g.B * g.J * g.HW, st));
+    }
   }
-  DCN_TRY(join_aux(h));
   {
     ProfScope ps(h, DCN_K_IM2COL);
     HIP_TRY(dcn::launch_im2col_bf16(g, xT, off32, BF(L.col), 0, g.B, st));
@@ -536,7 +547,8 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
                   bf16_t* gw, bf16_t* gb, bf16_t* gw_off, bf16_t* gb_off, bf16_t* goff_out,
                   char* base, const WsLayout& L, bool col_valid) {
   hipStream_t st = h->stream;
-  float *x32 = F32(L.x32), *xT = F32(L.xT), *off32 = F32(L.off32), *goff32 = F32(L.goff32);
+  bf16_t* xT = BF(L.xT);
+  float *off32 = F32(L.off32), *goff32 = F32(L.goff32);
   float *gx32 = F32(L.gx32), *gout32 = F32(L.gout32);
   bf16_t* col = BF(L.col);
   const size_t nx = (size_t)g.B * g.C * g.HWi, noff = (size_t)g.B * g.J * g.HW;
@@ -546,10 +558,9 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
   DCN_TRY(fork_aux(h));
   HIP_TRY(dcn::launch_bins(g, off32, base + L.bins, goff32, 0, g.B, h->aux));
   if (!col_valid) {
-    HIP_TRY(dcn::launch_bf16_to_f32(x, x32, nx, st));
     {
       ProfScope ps(h, DCN_K_XPOSE);
-      HIP_TRY(dcn::launch_nchw_to_nhwc(x32, xT, g.B, g.C, g.HWi, st));
+      HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(x, xT, g.B, g.C, g.HWi, st));
     }
     ProfScope ps(h, DCN_K_IM2COL);
     HIP_TRY(dcn::launch_im2col_bf16(g, xT, off32, col, 0, g.B, st));
@@ -609,8 +620,20 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
                                     g.B, true, st));
   }
   ProfScope ps(h, DCN_K_OFFSET_BWD);
-  HIP_TRY(dcn::launch_offset_conv_bwd(g, x32, xT, F32(L.woff32), goff32, F32(L.goffT), F32(L.wt),
-                                      gx32, F32(L.gwo32), F32(L.gbo32), F32(L.gxT), st));
+  if (dcn::offset_bwd_chunkable(g)) {
+    // f32 MFMA on the bf16 xT (exact products of the bf16 values) and the fp32 ∂offset
+    HIP_TRY(dcn::launch_offset_bwd_prep(g, F32(L.woff32), F32(L.wt), st));
+    HIP_TRY(dcn::launch_offset_bwd_chunk(g, xT, true, goff32, F32(L.goffT), F32(L.wt), gx32,
+                                         F32(L.gxT), 0, g.B, st));
+    HIP_TRY(dcn::launch_offset_bwd_finish(g, goff32, F32(L.goffT), F32(L.gwo32), F32(L.gbo32), st));
+  } else {  // VALU / generic kernels on fp32 copies of x (NCHW and channels-last)
+    float *x32 = F32(L.x32), *xT32 = F32(L.xT32);
+    HIP_TRY(dcn::launch_bf16_to_f32(x, x32, nx, st));
+    HIP_TRY(dcn::launch_nchw_to_nhwc(x32, xT32, g.B, g.C, g.HWi, st));
+    HIP_TRY(dcn::launch_offset_conv_bwd(g, x32, xT32, F32(L.woff32), goff32, F32(L.goffT),
+                                        F32(L.wt), gx32, F32(L.gwo32), F32(L.gbo32), F32(L.gxT),
+                                        st));
+  }
   HIP_TRY(dcn::launch_f32_to_bf16(gx32, gx, nx, st));
   if (goff_out) HIP_TRY(dcn::launch_f32_to_bf16(goff32, goff_out, noff, st));
   if (exch) return grads_final(h, F32(L.gwo32), F32(L.gbo32), g, gw_off, gb_off);

@@ -35,9 +35,9 @@ hipError_t launch_nchw_to_nhwc_bf16(const bf16_t* in, bf16_t* out, int B, int C,
                                     hipStream_t s);
 // bf16 columns / ∂columns (DCN_BF16; needs bf16_path_ok(g)): same kernels, bf16 rows.
 bool bf16_path_ok(const Geo& g);
-hipError_t launch_im2col_bf16(const Geo& g, const float* xT, const float* off, bf16_t* colT,
+hipError_t launch_im2col_bf16(const Geo& g, const bf16_t* xT, const float* off, bf16_t* colT,
                               int b0, int nb, hipStream_t s);
-hipError_t launch_col2im_bf16(const Geo& g, const float* xT, const float* off,
+hipError_t launch_col2im_bf16(const Geo& g, const bf16_t* xT, const float* off,
                               const bf16_t* gcolT, float* gx, float* gxT, float* goff,
                               void* bins_ws, int b0, int nb, bool bins_ready, hipStream_t s,
                               int bins_nb = 0);
@@ -77,6 +77,13 @@ size_t offset_conv_fpart_floats(const Geo& g);  // forward channel-slice partial
 hipError_t launch_offset_conv_fwd(const Geo& g, const float* x, const float* w_off,
                                   const float* b_off, float* off, float* wt, float* part,
                                   hipStream_t s);
+// DCN_BF16 forward offset conv on bf16 MFMA from the channels-last bf16 x: writes the
+// bf16-rounded offsets (off) and their fp32 values (off32). Needs offset_fwd_mfma_bf16_ok.
+bool offset_fwd_mfma_bf16_ok(const Geo& g);
+size_t offset_fwd_bf16_wb_elems(const Geo& g);
+hipError_t launch_offset_conv_fwd_bf16(const Geo& g, const bf16_t* xT, const bf16_t* w_off,
+                                       const float* b_off, float* off32, bf16_t* off, bf16_t* wb,
+                                       hipStream_t s);
 // xT: channels-last x; goffT: scratch of offset_conv_goffT_floats(g). gxT_in == NULL:
 // grad_x is accumulated; else grad_x = transpose(gxT_in) + the offset-conv route, written
 // once (gxT_in: the sampling-route ∂x left channels-last by launch_col2im_*).
@@ -91,7 +98,8 @@ hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
 // partial fold and ∂b_off). Same results as launch_offset_conv_bwd with gxT_in.
 bool offset_bwd_chunkable(const Geo& g);
 hipError_t launch_offset_bwd_prep(const Geo& g, const float* w_off, float* wt2, hipStream_t s);
-hipError_t launch_offset_bwd_chunk(const Geo& g, const float* xT, const float* goff,
+// xT: the fp32 channels-last x, or (xT_bf16) the bf16 one of DCN_BF16.
+hipError_t launch_offset_bwd_chunk(const Geo& g, const void* xT, bool xT_bf16, const float* goff,
                                    float* goffT, const float* wt2, float* gx,
                                    const float* gxT_in, int b0, int nb, hipStream_t s);
 hipError_t launch_offset_bwd_finish(const Geo& g, const float* goff, const float* goffT,

@@ -510,8 +510,23 @@ __device__ __forceinline__ int g_toff(const Geo& g, int tj, int SW) {
 // owns N-tiles w, w+4, w+8 (all 4 channel tiles), so no cross-wave reduction. Lane
 // (n = l&15, q = l>>4) loads channels c0+4n..+3 of pixel x0+q as one float4: element e
 // is row n of M-tile e (tile e = channels c0+4r+e). part[chunk][c][tj].
-template <int NTW, bool W4>
-__global__ __launch_bounds__(256) void offset_wgrad_mfma(Geo g, const float* __restrict__ xT,
+// 4 channels of xT through a buffer resource: fp32 (16 B) or bf16 (8 B, widened; DCN_BF16
+// passes its channels-last bf16 copy, whose products are then exact f32 MFMA products too)
+template <typename XT>
+__device__ __forceinline__ float4 buf_ld4(__amdgpu_buffer_rsrc_t rsrc, unsigned voff, int soff) {
+  if constexpr (sizeof(XT) == 4) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, soff, 0);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+                       __uint_as_float(v[3]));
+  } else {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, voff, soff, 0);
+    return make_float4(__uint_as_float(v[0] << 16), __uint_as_float(v[0] & 0xffff0000u),
+                       __uint_as_float(v[1] << 16), __uint_as_float(v[1] & 0xffff0000u));
+  }
+}
+
+template <int NTW, bool W4, typename XT = float>
+__global__ __launch_bounds__(256) void offset_wgrad_mfma(Geo g, const XT* __restrict__ xT,
                                                         const float* __restrict__ goff,
                                                         float* __restrict__ part, int rowsB,
                                                         int cpi, int chunk0) {
@@ -541,25 +556,21 @@ __global__ __launch_bounds__(256) void offset_wgrad_mfma(Geo g, const float* __r
   // multiple of kPf with zero-operand steps, so the unrolled body has no early exit.
   constexpr int kPf = 4;
   const int nq = (g.W + 3) / 4, nsteps = nrows * nq;
+  constexpr int XB = (int)sizeof(XT);
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(xT + ((size_t)b * g.H + y0) * g.W * g.C), 0,
-      (int)((size_t)max(nrows, 1) * g.W * g.C * sizeof(float)), 0x00020000);
+      const_cast<XT*>(xT + ((size_t)b * g.H + y0) * g.W * g.C), 0,
+      (int)((size_t)max(nrows, 1) * g.W * g.C * XB), 0x00020000);
   const int cl = cok ? cb + 4 * n : 0;
   float4 ring[kPf];
-  auto f4 = [](decltype(__builtin_amdgcn_raw_buffer_load_b128(rsrc, 0, 0, 0)) v) {
-    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
-                       __uint_as_float(v[3]));
-  };
   if (W4) {
     // W % 4 == 0: step ks covers pixels 4ks..4ks+3 of the chunk, so the xT offset is
     // linear in ks and a row change is wave-uniform: all per-step addressing is one
     // scalar add (no per-lane divides, clamps or multiplies in the loop)
-    const unsigned lane_x = (unsigned)((q * g.C + cl) * 4);
-    const int step_x = 16 * g.C, last = (nsteps - 1) * step_x;
+    const unsigned lane_x = (unsigned)((q * g.C + cl) * XB);
+    const int step_x = 4 * XB * g.C, last = (nsteps - 1) * step_x;
     int lo = 0;  // scalar byte offset of the step being loaded
 #pragma unroll
-    for (int d = 0; d < kPf; ++d, lo += step_x)
-      ring[d] = f4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, lane_x, min(lo, last), 0));
+    for (int d = 0; d < kPf; ++d, lo += step_x) ring[d] = buf_ld4<XT>(rsrc, lane_x, min(lo, last));
     int bv0[NTW];  // lane part of the B addresses
 #pragma unroll
     for (int u = 0; u < NTW; ++u) bv0[u] = q * g.J + toff[u];
@@ -583,7 +594,7 @@ __global__ __launch_bounds__(256) void offset_wgrad_mfma(Geo g, const float* __r
 #pragma unroll
         for (int u = 0; u < NTW; ++u)
           mfma16x4_acc(acc[0][u], acc[1][u], acc[2][u], acc[3][u], ax, ay, az, aw, bv[u]);
-        ring[d] = f4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, lane_x, min(lo, last), 0));
+        ring[d] = buf_ld4<XT>(rsrc, lane_x, min(lo, last));
         lo += step_x;
       }
     }
@@ -592,10 +603,10 @@ __global__ __launch_bounds__(256) void offset_wgrad_mfma(Geo g, const float* __r
     int ly = 0, lx = q;
     auto load_next = [&]() {
       const unsigned off =
-          (unsigned)(((min(ly, nrows - 1) * g.W + min(lx, g.W - 1)) * g.C + cl) * 4);
+          (unsigned)(((min(ly, nrows - 1) * g.W + min(lx, g.W - 1)) * g.C + cl) * XB);
       lx += 4;
       if (lx >= nq * 4) lx = q, ++ly;
-      return f4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
+      return buf_ld4<XT>(rsrc, off, 0);
     };
 #pragma unroll
     for (int d = 0; d < kPf; ++d) ring[d] = load_next();
@@ -766,6 +777,126 @@ __global__ __launch_bounds__(256, 4) void offset_dgrad_mfma(Geo g, const float* 
 }
 
 // ---------------------------------------------------------------------------
+// K3 on the bf16 matrix cores (DCN_BF16). The inputs are bf16, so every product w·x is
+// exact in fp32 and the MFMA sums are fp32: the arithmetic of the fp32 kernels on the
+// same values, in another summation order.
+//   off[b][j][p] = b_off[j] + Σ_{tap, c} w_off[j][c][tap] · xT[b][shift_tap(p)][c]
+// One block = 32 output pixels of one image x all J <= 32 offset channels: one 32x32 f32
+// tile of v_mfma_f32_32x32x16_bf16 (pixels on the rows, offset channels on the columns).
+// Its 4 waves split the input channels; A = the channels-last bf16 x (lane: 8 channels of
+// one pixel, one 16-B load), B = the weights as wb[tap][j][c] (lane: 8 channels of one j),
+// so no LDS staging and no transpose. The 4 channel partials fold through LDS in wave
+// order, then + bias, then the bf16 rounding the sampling uses (off32 = that value).
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+// wb[(tap*32 + j)*Cp + c] = w_off[j][c][tap] (bf16), 0 for j >= J or c >= C
+__global__ __launch_bounds__(256) void woff_to_tjc_bf16(const bf16_t* __restrict__ w,
+                                                       bf16_t* __restrict__ wb, int J, int C,
+                                                       int Cp, int KK) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= KK * 32 * Cp) return;
+  const int c = i % Cp, tj = i / Cp;
+  const int j = tj % 32, t = tj / 32;
+  wb[i] = (j < J && c < C) ? w[((size_t)j * C + c) * KK + t] : (bf16_t)0;
+}
+
+__device__ __forceinline__ bf16x8_t ld_bf16x8(const bf16_t* p) {
+  return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(p));
+}
+
+template <int SPT>  // 16-channel k-steps per tap and wave, loads issued together
+__global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16(
+    Geo g, const bf16_t* __restrict__ xT, const bf16_t* __restrict__ wb, int Cp,
+    const float* __restrict__ b_off, float* __restrict__ off32, bf16_t* __restrict__ off,
+    int tiles) {
+  __shared__ f32x16 red[3][64];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const Block3 blk = xcd_block();
+  const int tile = blk.x, b = blk.z;
+  const int r = lane & 31, hh = lane >> 5;
+  const int p = tile * 32 + r;
+  const bool pok = p < g.HW;
+  const int ho = pok ? p / g.Wo : 0, wo = pok ? p - (p / g.Wo) * g.Wo : 0;
+  const int c0 = w * SPT * 16 + 8 * hh;  // this lane's first channel in each tap
+  const bf16_t* xb = xT + (size_t)b * g.HWi * g.C;
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  const int KK = g.kh * g.kw;
+  for (int t = 0; t < KK; ++t) {
+    const int i = t / g.kw, k = t - i * g.kw;
+    const int y = ho * g.sh - g.ph + i * g.dh, x = wo * g.sw - g.pw + k * g.dw;
+    const bool ok = pok && y >= 0 && y < g.H && x >= 0 && x < g.W;
+    const bf16_t* xp = xb + (size_t)(ok ? y * g.W + x : 0) * g.C;
+    const bf16_t* wp = wb + ((size_t)t * 32 + r) * Cp;
+    bf16x8_t a[SPT], bv[SPT];
+#pragma unroll
+    for (int u = 0; u < SPT; ++u) {
+      const int c = c0 + 16 * u;
+      const bool cin = c < g.C;  // the launcher takes C % 16 == 0: whole 8-channel runs
+      a[u] = ld_bf16x8(xp + (cin ? c : 0));
+      if (!(ok && cin)) a[u] = bf16x8_t{};
+      bv[u] = ld_bf16x8(wp + (c < Cp ? c : 0));  // zero-padded to Cp (multiple of 64)
+    }
+#pragma unroll
+    for (int u = 0; u < SPT; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[u], bv[u], acc, 0, 0, 0);
+  }
+  if (w > 0) red[w - 1][lane] = acc;
+  __syncthreads();
+  if (w != 0) return;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const f32x16 o = red[q][lane];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] += o[i];
+  }
+  const int j = r;
+  if (j >= g.J) return;
+  const float bj = b_off[j];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int pp = tile * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+    if (pp < g.HW) {
+      const bf16_t v = f2bf(acc[i] + bj);
+      const size_t o = ((size_t)b * g.J + j) * g.HW + pp;
+      off[o] = v;
+      off32[o] = bf2f(v);
+    }
+  }
+}
+
+bool offset_fwd_mfma_bf16_ok(const Geo& g) {
+  return g.dt == DCN_BF16 && g.G == 1 && g.J <= 32 && g.C % 16 == 0;
+}
+size_t offset_fwd_bf16_wb_elems(const Geo& g) {
+  const int Cp = (g.C + 63) / 64 * 64;
+  return (size_t)g.kh * g.kw * 32 * Cp;
+}
+
+// xT: channels-last bf16 x; wb: scratch of offset_fwd_bf16_wb_elems(g) bf16 values.
+hipError_t launch_offset_conv_fwd_bf16(const Geo& g, const bf16_t* xT, const bf16_t* w_off,
+                                       const float* b_off, float* off32, bf16_t* off, bf16_t* wb,
+                                       hipStream_t s) {
+  if (!offset_fwd_mfma_bf16_ok(g)) return hipErrorInvalidValue;
+  const int KK = g.kh * g.kw, Cp = (g.C + 63) / 64 * 64;
+  const int n = KK * 32 * Cp;
+  hipLaunchKernelGGL(woff_to_tjc_bf16, dim3((n + 255) / 256), dim3(256), 0, s, w_off, wb, g.J,
+                     g.C, Cp, KK);
+  const int tiles = (g.HW + 31) / 32, spt = Cp / 64;  // 16-channel steps per tap and wave
+  dim3 grid(tiles, 1, g.B);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, g, xT, wb, Cp, b_off, off32, off, tiles);
+  };
+  if (spt == 1) go(offset_conv_fwd_mfma_bf16<1>);
+  else if (spt == 2) go(offset_conv_fwd_mfma_bf16<2>);
+  else if (spt == 3) go(offset_conv_fwd_mfma_bf16<3>);
+  else go(offset_conv_fwd_mfma_bf16<4>);  // C <= 256 on the bf16 path
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Generic fallbacks (kernel sizes without an instantiation): plain per-thread loops.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void offset_conv_fwd_generic(Geo g, const float* __restrict__ x,
@@ -888,8 +1019,9 @@ hipError_t launch_offset_bwd_prep(const Geo& g, const float* w_off, float* wt2, 
   return hipGetLastError();
 }
 
-// images [b0, b0+nb): their ∂W_off chunk partials (goffT region) and their ∂x
-hipError_t launch_offset_bwd_chunk(const Geo& g, const float* xT, const float* goff,
+// images [b0, b0+nb): their ∂W_off chunk partials (goffT region) and their ∂x.
+// xT: fp32 channels-last x, or (xT_bf16) the bf16 one.
+hipError_t launch_offset_bwd_chunk(const Geo& g, const void* xT, bool xT_bf16, const float* goff,
                                    float* goffT, const float* wt2, float* gx,
                                    const float* gxT_in, int b0, int nb, hipStream_t s) {
   MfmaStage ms;
@@ -897,15 +1029,23 @@ hipError_t launch_offset_bwd_chunk(const Geo& g, const float* xT, const float* g
   if (nb <= 0) return hipSuccess;
   const int TJ = g.J * g.kh * g.kw, NT = (TJ + 15) / 16;
   dim3 grid(nb * ms.cpi, (g.C + 63) / 64);
-  auto wg = [&](auto kern) {
-    hipLaunchKernelGGL(kern, grid, dim3(256), ms.lds_w, s, g, xT, goff, goffT, ms.rowsB, ms.cpi,
+  auto wg = [&](auto kern, auto* xp) {
+    hipLaunchKernelGGL(kern, grid, dim3(256), ms.lds_w, s, g, xp, goff, goffT, ms.rowsB, ms.cpi,
                        b0 * ms.cpi);
   };
   // W % 4 == 0 and C % 64 == 0: linear K-step addressing (see the kernel)
   const bool w4 = g.W % 4 == 0 && g.C % 64 == 0;
-  if (NT <= 4) w4 ? wg(offset_wgrad_mfma<1, true>) : wg(offset_wgrad_mfma<1, false>);
-  else if (NT <= 8) w4 ? wg(offset_wgrad_mfma<2, true>) : wg(offset_wgrad_mfma<2, false>);
-  else w4 ? wg(offset_wgrad_mfma<3, true>) : wg(offset_wgrad_mfma<3, false>);
+  if (xT_bf16) {
+    const bf16_t* xb = static_cast<const bf16_t*>(xT);
+    if (NT <= 4) w4 ? wg(offset_wgrad_mfma<1, true, bf16_t>, xb) : wg(offset_wgrad_mfma<1, false, bf16_t>, xb);
+    else if (NT <= 8) w4 ? wg(offset_wgrad_mfma<2, true, bf16_t>, xb) : wg(offset_wgrad_mfma<2, false, bf16_t>, xb);
+    else w4 ? wg(offset_wgrad_mfma<3, true, bf16_t>, xb) : wg(offset_wgrad_mfma<3, false, bf16_t>, xb);
+  } else {
+    const float* xf = static_cast<const float*>(xT);
+    if (NT <= 4) w4 ? wg(offset_wgrad_mfma<1, true>, xf) : wg(offset_wgrad_mfma<1, false>, xf);
+    else if (NT <= 8) w4 ? wg(offset_wgrad_mfma<2, true>, xf) : wg(offset_wgrad_mfma<2, false>, xf);
+    else w4 ? wg(offset_wgrad_mfma<3, true>, xf) : wg(offset_wgrad_mfma<3, false>, xf);
+  }
   hipLaunchKernelGGL(offset_dgrad_mfma, dim3(nb * ms.spi), dim3(256), ms.lds_x, s, g, wt2,
                      pad_c(g.C), goff, gx, gxT_in, ms.spi, b0 * ms.spi);
   return hipGetLastError();
@@ -933,7 +1073,8 @@ hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
   DCN_KK_DISPATCH(KK, (void)KKc);
   if (!generic && offset_bwd_chunkable(g)) {
     hipError_t e = launch_offset_bwd_prep(g, w_off, wt2, s);
-    if (e == hipSuccess) e = launch_offset_bwd_chunk(g, xT, goff, goffT, wt2, gx, gxT_in, 0, g.B, s);
+    if (e == hipSuccess)
+      e = launch_offset_bwd_chunk(g, xT, false, goff, goffT, wt2, gx, gxT_in, 0, g.B, s);
     if (e == hipSuccess) e = launch_offset_bwd_finish(g, goff, goffT, gw_off, gb_off, s);
     return e;
   }

@@ -74,6 +74,11 @@ __device__ __forceinline__ void stv(float* p, typename Vec<VEC>::T v) {
   *reinterpret_cast<typename Vec<VEC>::T*>(p) = v;
 }
 
+template <typename T>
+__device__ __forceinline__ float4 ld4_if(const T* p, bool ok) {
+  return ok ? ld4(p) : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 __device__ __forceinline__ float4 bilerp4(float fr, float fc, float4 a, float4 b, float4 c,
                                           float4 d) {
   return make_float4(bilerp(fr, fc, a.x, b.x, c.x, d.x), bilerp(fr, fc, a.y, b.y, c.y, d.y),
@@ -208,8 +213,10 @@ struct Win {
   static constexpr int PIX = R * Q;
 };
 
-template <int TH, int TW, int MAR, int CS, bool NT, typename OT = float>
-__global__ __launch_bounds__(256) void im2col_lds(Geo g, const float* __restrict__ xT,
+// xT element type XT: float, or bf16 (DCN_BF16: the channels-last copy of the bf16 input,
+// half the window bytes; staged into LDS as fp32, so the arithmetic is unchanged)
+template <int TH, int TW, int MAR, int CS, bool NT, typename OT = float, typename XT = float>
+__global__ __launch_bounds__(256) void im2col_lds(Geo g, const XT* __restrict__ xT,
                                                   const float* __restrict__ off,
                                                   OT* __restrict__ colT, int b0, int tw_n) {
   typedef Win<TH, TW, MAR> Wn;
@@ -237,7 +244,7 @@ __global__ __launch_bounds__(256) void im2col_lds(Geo g, const float* __restrict
     }
     rec[sidx] = r;
   }
-  const float* xb = xT + (size_t)b * g.HWi * g.C;
+  const XT* xb = xT + (size_t)b * g.HWi * g.C;
   OT* cb = colT + (size_t)bl * g.HW * g.K;
   const int grp = tid / LPS, cl = tid % LPS;  // GS sample groups of LPS lanes
   for (int cs = 0; cs < g.C; cs += CS) {
@@ -254,8 +261,7 @@ __global__ __launch_bounds__(256) void im2col_lds(Geo g, const float* __restrict
         const int rr = pix / Wn::Q, qq = pix - rr * Wn::Q;
         const int r = rlo + rr, q = qlo + qq, cc = cs + l * 4;
         const bool ok = idx < TOT && r >= 0 && r < g.H && q >= 0 && q < g.W && cc < g.C;
-        v[k] = ok ? *reinterpret_cast<const float4*>(xb + ((size_t)r * g.W + q) * g.C + cc)
-                  : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[k] = ok ? ld4(xb + ((size_t)r * g.W + q) * g.C + cc) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
       for (int k = 0; k < IT; ++k)
@@ -280,12 +286,12 @@ __global__ __launch_bounds__(256) void im2col_lds(Geo g, const float* __restrict
           d = w4[(Wn::Q + 1) * LPS];
         } else {  // outside the staged window: global corner reads
           const bool r0ok = r.x >= 0, r1ok = r.x + 1 < g.H, c0ok = r.y >= 0, c1ok = r.y + 1 < g.W;
-          const float* p00 = xb + ((long)r.x * g.W + r.y) * (long)g.C + c;
+          const XT* p00 = xb + ((long)r.x * g.W + r.y) * (long)g.C + c;
           const long rs = (long)g.W * g.C;
-          a = ldv<4>(p00, cok && r0ok && c0ok);
-          bq = ldv<4>(p00 + g.C, cok && r0ok && c1ok);
-          cq = ldv<4>(p00 + rs, cok && r1ok && c0ok);
-          d = ldv<4>(p00 + rs + g.C, cok && r1ok && c1ok);
+          a = ld4_if(p00, cok && r0ok && c0ok);
+          bq = ld4_if(p00 + g.C, cok && r0ok && c1ok);
+          cq = ld4_if(p00 + rs, cok && r1ok && c0ok);
+          d = ld4_if(p00 + rs + g.C, cok && r1ok && c1ok);
         }
         o = bilerp4(fr, fc, a, bq, cq, d);
       }
@@ -477,8 +483,8 @@ __device__ __forceinline__ float4 add4(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
 
-template <int U, int kTQ, typename GT = float>
-__global__ __launch_bounds__(kC2iThreads) void col2im_tile(Geo g, const float* __restrict__ xT,
+template <int U, int kTQ, typename GT = float, typename XT = float>
+__global__ __launch_bounds__(kC2iThreads) void col2im_tile(Geo g, const XT* __restrict__ xT,
                                                            const int4* __restrict__ brec,
                                                            const int* __restrict__ start,
                                                            const GT* __restrict__ gcolT,
@@ -496,14 +502,13 @@ __global__ __launch_bounds__(kC2iThreads) void col2im_tile(Geo g, const float* _
   const int R0 = tr_i * kTR, Q0 = tq_i * kTQ;
   const int c = lane * 4;
   const bool cok = c < g.C;
-  const float* xb = xT + (size_t)b * g.HWi * g.C;
+  const XT* xb = xT + (size_t)b * g.HWi * g.C;
   // stage xT rows R0..R0+kTR, cols Q0..Q0+kTQ (zero outside the image)
   for (int idx = tid; idx < WIN; idx += kC2iThreads) {
     const int pix = idx >> 6, l = idx & 63;
     const int r = R0 + pix / WQ, q = Q0 + pix % WQ, cc = l * 4;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (r < g.H && q < g.W && cc < g.C)
-      v = *reinterpret_cast<const float4*>(xb + ((size_t)r * g.W + q) * g.C + cc);
+    if (r < g.H && q < g.W && cc < g.C) v = ld4(xb + ((size_t)r * g.W + q) * g.C + cc);
     lds[idx] = v;
   }
   __syncthreads();
@@ -1011,12 +1016,12 @@ static BinsWs bins_view(const Geo& g, void* bins_ws, int b0, int nb, int bins_nb
 // r01 A/B at config 3 (2-deep prefetch pipeline): U=2 0.92 ms col2im, U=4 0.93, U=8 1.50;
 // 4x6 tiles 1.05x slower, 4x8 tiles no longer unroll (2.7 ms). r02: column sweeps and
 // strips without the tile's bin-row re-read measured no faster (DESIGN.md §4 "K5").
-template <typename GT>
-static void launch_k5_fused(const Geo& g, const float* xT, const BinsWs& P, const GT* gcolT,
+template <typename GT, typename XT>
+static void launch_k5_fused(const Geo& g, const XT* xT, const BinsWs& P, const GT* gcolT,
                             float* gxT, float* goff, int b0, int nb, hipStream_t s) {
   const int tr_n = (g.H + kTR - 1) / kTR, tq_n = (g.W + 4 - 1) / 4;
-  hipLaunchKernelGGL((col2im_tile<2, 4, GT>), dim3(tr_n * tq_n, 1, nb), dim3(kC2iThreads), 0, s,
-                     g, xT, P.brec, P.start, gcolT, gxT, goff, b0, tq_n);
+  hipLaunchKernelGGL((col2im_tile<2, 4, GT, XT>), dim3(tr_n * tq_n, 1, nb), dim3(kC2iThreads), 0,
+                     s, g, xT, P.brec, P.start, gcolT, gxT, goff, b0, tq_n);
 }
 
 hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, const float* off,
@@ -1072,7 +1077,7 @@ hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, co
 // ---- DCN_BF16: bf16 column rows through the same LDS-window / fused kernels ----------
 bool bf16_path_ok(const Geo& g) { return g.G == 1 && g.N <= kMaxTaps && g.C % 4 == 0 && g.C <= 256; }
 
-hipError_t launch_im2col_bf16(const Geo& g, const float* xT, const float* off, bf16_t* colT,
+hipError_t launch_im2col_bf16(const Geo& g, const bf16_t* xT, const float* off, bf16_t* colT,
                               int b0, int nb, hipStream_t s) {
   if (nb <= 0) return hipSuccess;
   auto go = [&](auto kern, int TH, int TW) {
@@ -1081,17 +1086,17 @@ hipError_t launch_im2col_bf16(const Geo& g, const float* xT, const float* off, b
                        tw_n);
   };
   if (g.C <= 32)
-    go(im2col_lds<8, 8, 2, 32, true, bf16_t>, 8, 8);
+    go(im2col_lds<8, 8, 2, 32, true, bf16_t, bf16_t>, 8, 8);
   else if (g.C <= 64)
-    go(im2col_lds<8, 8, 2, 64, true, bf16_t>, 8, 8);
+    go(im2col_lds<8, 8, 2, 64, true, bf16_t, bf16_t>, 8, 8);
   else if (g.C <= 128)
-    go(im2col_lds<4, 4, 1, 128, true, bf16_t>, 4, 4);
+    go(im2col_lds<4, 4, 1, 128, true, bf16_t, bf16_t>, 4, 4);
   else
-    go(im2col_lds<4, 4, 1, 256, true, bf16_t>, 4, 4);
+    go(im2col_lds<4, 4, 1, 256, true, bf16_t, bf16_t>, 4, 4);
   return hipGetLastError();
 }
 
-hipError_t launch_col2im_bf16(const Geo& g, const float* xT, const float* off,
+hipError_t launch_col2im_bf16(const Geo& g, const bf16_t* xT, const float* off,
                               const bf16_t* gcolT, float* gx, float* gxT, float* goff,
                               void* bins_ws, int b0, int nb, bool bins_ready, hipStream_t s,
                               int bins_nb) {

@@ -129,7 +129,13 @@ def test_staging_ragged_chunks(monkeypatch, chunk_mb, threads):
     h = rt.Handle(0)  # staging is created with the handle's first host transfer
     out, off, ctx = dcn_forward_numpy(x, wo, bo, w, b, s, (1, 1), handle=h, return_ctx=True)
     g = dcn_backward_numpy(x, off, wo, w, True, gout, s, (1, 1), handle=h, ctx=ctx)
-    np.testing.assert_array_equal(out, out0)
-    np.testing.assert_array_equal(off, off0)
-    _grads_equal(g, g0)
+    g_full = dcn_backward_numpy(x, off, wo, w, True, gout, s, (1, 1), handle=h)
+    _grads_equal(g, g_full)  # same handle: bitwise
+    # across handles each GEMM engine autotunes on its own (timing-based), so the GEMM
+    # summation orders may differ: fp32 rounding, not bits
+    assert_close(out, out0, what="out")
+    np.testing.assert_array_equal(off, off0)  # the offset conv has no autotuned GEMM
+    assert_close(g["x"], g0["x"], what="∂x")
+    for k in ("weight", "bias", "offset_conv.weight", "offset_conv.bias"):
+        assert_close_reduction(g[k], g0[k], what=k)
     h.close()
