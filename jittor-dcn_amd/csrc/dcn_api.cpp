@@ -116,7 +116,7 @@ struct WsLayout {
   // (DCN_BF16 keeps its channels-last x in `xT` as bf16; xT32 is the fp32 one that only the
   // VALU offset-conv fallbacks read, wb16 the bf16 weights of the MFMA offset conv)
   size_t x32 = 0, xT32 = 0, wb16 = 0, woff32 = 0, boff32 = 0, b32 = 0, off32 = 0, out32 = 0;
-  size_t gout32 = 0, gx32 = 0, gw32 = 0, gb32 = 0, gwo32 = 0, gbo32 = 0, goff32 = 0;
+  size_t gx32 = 0, gw32 = 0, gb32 = 0, gwo32 = 0, gbo32 = 0, goff32 = 0;
   size_t total = 0;
 };
 
@@ -157,7 +157,6 @@ WsLayout ws_layout(const Geo& g, bool bwd) {
     L.bins = take(dcn::bins_ws_bytes(g, g.B));
   }
   if (g.dt == DCN_BF16 && bwd) {
-    L.gout32 = take((size_t)g.B * g.O * g.HW * f);
     L.gx32 = take((size_t)g.B * g.C * g.HWi * f);
     L.gw32 = take((size_t)g.O * g.K * f);
     L.gb32 = take((size_t)g.O * f);
@@ -549,10 +548,10 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
   hipStream_t st = h->stream;
   bf16_t* xT = BF(L.xT);
   float *off32 = F32(L.off32), *goff32 = F32(L.goff32);
-  float *gx32 = F32(L.gx32), *gout32 = F32(L.gout32);
+  float* gx32 = F32(L.gx32);
   bf16_t* col = BF(L.col);
   const size_t nx = (size_t)g.B * g.C * g.HWi, noff = (size_t)g.B * g.J * g.HW;
-  const size_t nout = (size_t)g.B * g.O * g.HW, nwo = (size_t)g.J * g.C * g.N;
+  const size_t nwo = (size_t)g.J * g.C * g.N;
   HIP_TRY(dcn::launch_bf16_to_f32(off, off32, noff, st));  // == the forward's rounded offsets
   HIP_TRY(dcn::launch_bf16_to_f32(w_off, F32(L.woff32), nwo, st));
   DCN_TRY(fork_aux(h));
@@ -567,9 +566,8 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
   }
   const bool exch = h->comm != nullptr;  // sum the fp32 copies over ranks, then round
   if (has_bias) {
-    ProfScope ps(h, DCN_K_BWD_BIAS);
-    HIP_TRY(dcn::launch_bf16_to_f32(gout, gout32, nout, st));
-    HIP_TRY(dcn::launch_bias_grad(g, gout32, F32(L.gb32), st));
+    ProfScope ps(h, DCN_K_BWD_BIAS);  // Σ over images and pixels of the bf16 ∂out, in fp32
+    dcn::launch_channel_sum_bf16(gout, g.B, g.O, g.HW, F32(L.gb32), st);
     if (!exch) HIP_TRY(dcn::launch_f32_to_bf16(F32(L.gb32), gb, (size_t)g.O, st));
   }
   bf16_t* goutT = BF(L.goutT);

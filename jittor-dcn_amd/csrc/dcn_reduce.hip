@@ -4,24 +4,32 @@
 
 namespace dcn {
 
-// out[ch] = Σ_{b,m} in[b][ch][m]: one 1024-thread block per channel streams its
-// B·HW values with 16-byte loads; fixed reduction order (deterministic).
-template <bool VEC>
-__global__ __launch_bounds__(1024) void channel_sum(const float* __restrict__ in, int B, int Cn,
+// out[ch] = Σ_{b,m} in[b][ch][m]: one 1024-thread block per channel; thread t sums the
+// 4-element runs t, t+1024, ... of the channel's B·HW/4 runs taken image by image (all its
+// loads independent, in flight together; r01 walked the images one after another, a
+// 64-deep dependent chain: 33 us for ∂b or ∂b_off at config 4), then a fixed xor tree and
+// a fixed wave order: deterministic. T: fp32, or bf16 (DCN_BF16's ∂out read directly).
+template <bool VEC, typename T>
+__global__ __launch_bounds__(1024) void channel_sum(const T* __restrict__ in, int B, int Cn,
                                                     int HW, float* __restrict__ out) {
   __shared__ float red[1024 / 64];
   const int ch = blockIdx.x, tid = threadIdx.x;
   float s = 0.f;
-  for (int b = 0; b < B; ++b) {
-    const float* p = in + ((size_t)b * Cn + ch) * HW;
-    if (VEC) {
-      const float4* p4 = reinterpret_cast<const float4*>(p);
-      for (int m = tid; m < HW / 4; m += 1024) {
-        const float4 v = p4[m];
-        s += (v.x + v.y) + (v.z + v.w);
-      }
-    } else {
-      for (int m = tid; m < HW; m += 1024) s += p[m];
+  if (VEC) {
+    const int R = HW / 4;  // runs per image
+    const long tot = (long)B * R;
+#pragma unroll 4
+    for (long i = tid; i < tot; i += 1024) {
+      const int b = (int)(i / R), m = (int)(i - (long)b * R);
+      const float4 v = ld4(in + ((size_t)b * Cn + ch) * HW + 4 * m);
+      s += (v.x + v.y) + (v.z + v.w);
+    }
+  } else {
+    const long tot = (long)B * HW;
+#pragma unroll 4
+    for (long i = tid; i < tot; i += 1024) {
+      const int b = (int)(i / HW), m = (int)(i - (long)b * HW);
+      s += to_f32(in[((size_t)b * Cn + ch) * HW + m]);
     }
   }
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
@@ -36,9 +44,16 @@ __global__ __launch_bounds__(1024) void channel_sum(const float* __restrict__ in
 
 void launch_channel_sum(const float* in, int B, int Cn, int HW, float* out, hipStream_t s) {
   if (HW % 4 == 0)
-    hipLaunchKernelGGL(channel_sum<true>, dim3(Cn), dim3(1024), 0, s, in, B, Cn, HW, out);
+    hipLaunchKernelGGL((channel_sum<true, float>), dim3(Cn), dim3(1024), 0, s, in, B, Cn, HW, out);
   else
-    hipLaunchKernelGGL(channel_sum<false>, dim3(Cn), dim3(1024), 0, s, in, B, Cn, HW, out);
+    hipLaunchKernelGGL((channel_sum<false, float>), dim3(Cn), dim3(1024), 0, s, in, B, Cn, HW, out);
+}
+void launch_channel_sum_bf16(const bf16_t* in, int B, int Cn, int HW, float* out, hipStream_t s) {
+  if (HW % 4 == 0 && ((uintptr_t)in & 7) == 0)
+    hipLaunchKernelGGL((channel_sum<true, bf16_t>), dim3(Cn), dim3(1024), 0, s, in, B, Cn, HW, out);
+  else
+    hipLaunchKernelGGL((channel_sum<false, bf16_t>), dim3(Cn), dim3(1024), 0, s, in, B, Cn, HW,
+                       out);
 }
 
 // ---------------------------------------------------------------------------
@@ -148,6 +163,20 @@ __global__ __launch_bounds__(256) void bias_to_bf16_kernel(const float* __restri
     out[i] = f2bf(v);
   }
 }
+// 4 per thread (HW % 4 == 0): 16-B loads, 8-B stores
+__global__ __launch_bounds__(256) void bias_to_bf16_vec4(const float4* __restrict__ in,
+                                                         const float* __restrict__ bias,
+                                                         bf16_t* __restrict__ out, int O, int HW4,
+                                                         size_t n4) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+    float4 v = in[i];
+    if (bias) {
+      const float bv = bias[(i / HW4) % O];
+      v.x += bv, v.y += bv, v.z += bv, v.w += bv;
+    }
+    st4<false>(out + 4 * i, v);
+  }
+}
 
 static unsigned grid_for(size_t n, size_t per_thread) {
   const size_t b = (n + 256 * per_thread - 1) / (256 * per_thread);
@@ -169,8 +198,12 @@ hipError_t launch_round_to_bf16(float* v, bf16_t* out, size_t n, hipStream_t s) 
 hipError_t launch_bias_to_bf16(const Geo& g, const float* out32, const float* bias, bf16_t* out,
                                hipStream_t s) {
   const size_t n = (size_t)g.B * g.O * g.HW;
-  hipLaunchKernelGGL(bias_to_bf16_kernel, dim3(grid_for(n, 1)), dim3(256), 0, s, out32, bias, out,
-                     g.O, g.HW, n);
+  if (g.HW % 4 == 0 && ((uintptr_t)out32 & 15) == 0 && ((uintptr_t)out & 7) == 0)
+    hipLaunchKernelGGL(bias_to_bf16_vec4, dim3(grid_for(n, 4)), dim3(256), 0, s,
+                       reinterpret_cast<const float4*>(out32), bias, out, g.O, g.HW / 4, n / 4);
+  else
+    hipLaunchKernelGGL(bias_to_bf16_kernel, dim3(grid_for(n, 1)), dim3(256), 0, s, out32, bias,
+                       out, g.O, g.HW, n);
   return hipGetLastError();
 }
 
