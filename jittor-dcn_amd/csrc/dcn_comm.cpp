@@ -53,10 +53,20 @@ Rccl* rccl(std::string* err) {
   static bool tried = false;
   if (!tried) {
     tried = true;
-    for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
-      r.lib = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+    // An RCCL already in the process (torch's own copy, whose NEEDED name is librccl.so)
+    // is reused as is. Otherwise one is loaded RTLD_LOCAL: with RTLD_GLOBAL, a second copy
+    // that torch loads later (libtorch_hip NEEDs "librccl.so", not the "librccl.so.1" this
+    // loads) bound its symbols into ours, and the process aborted at exit with a corrupted
+    // heap (r02, test_gpu_configs.py run alone, torch imported after the first comm test).
+    for (const char* name : {"librccl.so", "librccl.so.1"}) {
+      r.lib = dlopen(name, RTLD_NOW | RTLD_NOLOAD);
       if (r.lib) break;
     }
+    if (!r.lib)
+      for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+        r.lib = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+        if (r.lib) break;
+      }
     if (r.lib) {
       r.get_id = (GetUniqueId_t)dlsym(r.lib, "ncclGetUniqueId");
       r.init = (CommInitRank_t)dlsym(r.lib, "ncclCommInitRank");

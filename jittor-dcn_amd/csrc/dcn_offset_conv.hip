@@ -825,23 +825,36 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16(
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
   const int KK = g.kh * g.kw;
-  for (int t = 0; t < KK; ++t) {
-    const int i = t / g.kw, k = t - i * g.kw;
+  // software pipeline over the taps: tap t+1's operands are loaded before tap t's MFMAs
+  // (one memory latency per kernel instead of one per tap)
+  bf16x8_t a[2][SPT], bv[2][SPT];
+  auto load = [&](int t, bf16x8_t(&ra)[SPT], bf16x8_t(&rb)[SPT]) {
+    const int tt = min(t, KK - 1);  // past the last tap: a harmless re-load
+    const int i = tt / g.kw, k = tt - i * g.kw;
     const int y = ho * g.sh - g.ph + i * g.dh, x = wo * g.sw - g.pw + k * g.dw;
     const bool ok = pok && y >= 0 && y < g.H && x >= 0 && x < g.W;
     const bf16_t* xp = xb + (size_t)(ok ? y * g.W + x : 0) * g.C;
-    const bf16_t* wp = wb + ((size_t)t * 32 + r) * Cp;
-    bf16x8_t a[SPT], bv[SPT];
+    const bf16_t* wp = wb + ((size_t)tt * 32 + r) * Cp;
 #pragma unroll
     for (int u = 0; u < SPT; ++u) {
       const int c = c0 + 16 * u;
       const bool cin = c < g.C;  // the launcher takes C % 16 == 0: whole 8-channel runs
-      a[u] = ld_bf16x8(xp + (cin ? c : 0));
-      if (!(ok && cin)) a[u] = bf16x8_t{};
-      bv[u] = ld_bf16x8(wp + (c < Cp ? c : 0));  // zero-padded to Cp (multiple of 64)
+      ra[u] = ld_bf16x8(xp + (cin ? c : 0));
+      if (!(ok && cin)) ra[u] = bf16x8_t{};
+      rb[u] = ld_bf16x8(wp + (c < Cp ? c : 0));  // zero-padded to Cp (multiple of 64)
     }
+  };
+  load(0, a[0], bv[0]);
+  for (int t = 0; t < KK; t += 2) {
+    load(t + 1, a[1], bv[1]);
 #pragma unroll
-    for (int u = 0; u < SPT; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[u], bv[u], acc, 0, 0, 0);
+    for (int u = 0; u < SPT; ++u)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][u], bv[0][u], acc, 0, 0, 0);
+    if (t + 1 >= KK) break;
+    load(t + 2, a[0], bv[0]);
+#pragma unroll
+    for (int u = 0; u < SPT; ++u)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][u], bv[1][u], acc, 0, 0, 0);
   }
   if (w > 0) red[w - 1][lane] = acc;
   __syncthreads();
@@ -852,17 +865,23 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16(
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] += o[i];
   }
-  const int j = r;
-  if (j >= g.J) return;
-  const float bj = b_off[j];
+  // + bias, bf16 rounding; the tile goes through LDS as [j][pixel] so that the stores are
+  // runs of 32 consecutive pixels per offset channel (lane = pixel), not 4-byte scatters
+  // (lane = channel: every store instruction touched 64 lines)
+  __shared__ float T[32][33];
+  const float bj = r < g.J ? b_off[r] : 0.f;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int pp = tile * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-    if (pp < g.HW) {
-      const bf16_t v = f2bf(acc[i] + bj);
+  for (int i = 0; i < 16; ++i) T[r][(i & 3) + 8 * (i >> 2) + 4 * hh] = bf2f(f2bf(acc[i] + bj));
+  // wave 0 alone reads back what its own lanes wrote: LDS ops of one wave run in order, so
+  // only the compiler must not move the reads above the writes
+  __builtin_amdgcn_wave_barrier();
+  const int pp = tile * 32 + r;
+  if (pp < g.HW) {
+    for (int j = hh; j < g.J; j += 2) {
+      const float v = T[j][r];
       const size_t o = ((size_t)b * g.J + j) * g.HW + pp;
-      off[o] = v;
-      off32[o] = bf2f(v);
+      off32[o] = v;
+      off[o] = f2bf(v);  // exact: v is a bf16 value
     }
   }
 }

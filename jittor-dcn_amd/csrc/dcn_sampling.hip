@@ -215,6 +215,28 @@ struct Win {
 
 // xT element type XT: float, or bf16 (DCN_BF16: the channels-last copy of the bf16 input,
 // half the window bytes; staged into LDS as fp32, so the arithmetic is unchanged)
+// LDS image of 4 channels of the xT window: float4 for fp32, the raw 8 bytes for bf16 (half
+// the LDS per block, twice the blocks per CU: the bf16 K1 was LDS-occupancy bound)
+template <typename XT>
+struct WinT;
+template <>
+struct WinT<float> {
+  typedef float4 T;
+  __device__ static T raw(const float* p) { return *reinterpret_cast<const float4*>(p); }
+  __device__ static T zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  __device__ static float4 f(T v) { return v; }
+};
+template <>
+struct WinT<bf16_t> {
+  typedef uint2 T;
+  __device__ static T raw(const bf16_t* p) { return *reinterpret_cast<const uint2*>(p); }
+  __device__ static T zero() { return make_uint2(0u, 0u); }
+  __device__ static float4 f(T u) {
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                       __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+  }
+};
+
 template <int TH, int TW, int MAR, int CS, bool NT, typename OT = float, typename XT = float>
 __global__ __launch_bounds__(256) void im2col_lds(Geo g, const XT* __restrict__ xT,
                                                   const float* __restrict__ off,
@@ -222,7 +244,8 @@ __global__ __launch_bounds__(256) void im2col_lds(Geo g, const XT* __restrict__ 
   typedef Win<TH, TW, MAR> Wn;
   constexpr int kTP = TH * TW;
   constexpr int LPS = CS / 4, GS = 256 / LPS;  // lanes per sample, samples per block step
-  __shared__ float4 win[Wn::PIX * LPS];
+  typedef WinT<XT> WT;
+  __shared__ typename WT::T win[Wn::PIX * LPS];
   __shared__ int4 rec[kTP * kMaxTaps];
   const int tid = threadIdx.x;
   const Block3 blk = xcd_block();
@@ -253,7 +276,7 @@ __global__ __launch_bounds__(256) void im2col_lds(Geo g, const XT* __restrict__ 
     __syncthreads();  // records ready / previous slice consumed
     {
       constexpr int TOT = Wn::PIX * LPS, IT = (TOT + 255) / 256;
-      float4 v[IT];
+      typename WT::T v[IT];
 #pragma unroll
       for (int k = 0; k < IT; ++k) {
         const int idx = tid + k * 256;
@@ -261,7 +284,7 @@ __global__ __launch_bounds__(256) void im2col_lds(Geo g, const XT* __restrict__ 
         const int rr = pix / Wn::Q, qq = pix - rr * Wn::Q;
         const int r = rlo + rr, q = qlo + qq, cc = cs + l * 4;
         const bool ok = idx < TOT && r >= 0 && r < g.H && q >= 0 && q < g.W && cc < g.C;
-        v[k] = ok ? ld4(xb + ((size_t)r * g.W + q) * g.C + cc) : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[k] = ok ? WT::raw(xb + ((size_t)r * g.W + q) * g.C + cc) : WT::zero();
       }
 #pragma unroll
       for (int k = 0; k < IT; ++k)
@@ -279,11 +302,11 @@ __global__ __launch_bounds__(256) void im2col_lds(Geo g, const XT* __restrict__ 
         const int rr = r.x - rlo, qq = r.y - qlo;
         float4 a, bq, cq, d;
         if (rr >= 0 && rr + 1 < Wn::R && qq >= 0 && qq + 1 < Wn::Q) {
-          const float4* w4 = win + (rr * Wn::Q + qq) * LPS + cl;
-          a = w4[0];
-          bq = w4[LPS];
-          cq = w4[Wn::Q * LPS];
-          d = w4[(Wn::Q + 1) * LPS];
+          const typename WT::T* w4 = win + (rr * Wn::Q + qq) * LPS + cl;
+          a = WT::f(w4[0]);
+          bq = WT::f(w4[LPS]);
+          cq = WT::f(w4[Wn::Q * LPS]);
+          d = WT::f(w4[(Wn::Q + 1) * LPS]);
         } else {  // outside the staged window: global corner reads
           const bool r0ok = r.x >= 0, r1ok = r.x + 1 < g.H, c0ok = r.y >= 0, c1ok = r.y + 1 < g.W;
           const XT* p00 = xb + ((long)r.x * g.W + r.y) * (long)g.C + c;

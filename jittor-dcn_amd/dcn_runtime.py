@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -103,8 +104,29 @@ _lib = None
 _lock = threading.Lock()
 
 
+def _one_hip_runtime():
+    """torch-rocm bundles its own HIP runtime (torch/lib/libamdhip64.so, NEEDed unversioned),
+    while libdcn NEEDs libamdhip64.so.7 (RUNPATH /opt/rocm/lib). Loaded first, libdcn maps
+    /opt/rocm's runtime, and a torch imported later maps its own beside it: two HIP runtimes
+    in one process (torch's streams handed to libdcn are then foreign objects; r02: heap
+    corruption in a test that imported torch after libdcn). Loaded after torch, libdcn's
+    NEEDED name matches torch's runtime (same soname) and the process keeps one. So where
+    torch is installed it is imported before libdcn; torch-free callers (the Jittor / NumPy
+    path) are unaffected. DCN_NO_TORCH_PRELOAD=1 skips this."""
+    if "torch" in sys.modules or os.environ.get("DCN_NO_TORCH_PRELOAD") == "1":
+        return
+    try:
+        import importlib.util
+        if importlib.util.find_spec("torch") is None:
+            return
+    except (ImportError, ValueError):
+        return
+    import torch  # noqa: F401
+
+
 def load(path: str | None = None):
     """Load libdcn.so and declare every prototype. Raises if it is missing."""
+    _one_hip_runtime()
     global _lib
     with _lock:
         if _lib is not None and path is None:
