@@ -526,15 +526,21 @@ __global__ __launch_bounds__(kC2iThreads) void col2im_tile(Geo g, const XT* __re
   const int c = lane * 4;
   const bool cok = c < g.C;
   const XT* xb = xT + (size_t)b * g.HWi * g.C;
-  // stage xT rows R0..R0+kTR, cols Q0..Q0+kTQ (zero outside the image)
-  for (int idx = tid; idx < WIN; idx += kC2iThreads) {
+  // xT rows R0..R0+kTR, cols Q0..Q0+kTQ (zero outside the image) into registers; they go
+  // to LDS after each wave has started its record / ∂col row stream, and the barrier
+  // orders LDS only, so the stream's first rows are in flight across it (r01 staged the
+  // window first: the stream began a full staging round trip later)
+  constexpr int WIT = (WIN + kC2iThreads - 1) / kC2iThreads;
+  float4 wv[WIT];
+#pragma unroll
+  for (int k = 0; k < WIT; ++k) {
+    const int idx = tid + k * kC2iThreads;
     const int pix = idx >> 6, l = idx & 63;
     const int r = R0 + pix / WQ, q = Q0 + pix % WQ, cc = l * 4;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (r < g.H && q < g.W && cc < g.C) v = ld4(xb + ((size_t)r * g.W + q) * g.C + cc);
-    lds[idx] = v;
+    wv[k] = (idx < WIN && r < g.H && q < g.W && cc < g.C)
+                ? ld4(xb + ((size_t)r * g.W + q) * g.C + cc)
+                : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  __syncthreads();
   const int NB = (g.H + 1) * (g.W + 1);
   const int* st = start + (size_t)bl * (NB + 1);
   const int4* rb = brec + (size_t)bl * g.HW * g.N;
@@ -547,42 +553,47 @@ __global__ __launch_bounds__(kC2iThreads) void col2im_tile(Geo g, const XT* __re
 #pragma unroll
   for (int j = 0; j < kTQ; ++j) up[j] = dn[j] = z4;
   const int br = R0 + w;  // bin row = r0 + 1
-  if (br <= g.H) {
-    const bool drow = w >= 1 || br == 0;  // owns the ∂offset of this bin row
-    // the row's bins (br, Q0..Q0+kTQ) are consecutive, so their records are one
-    // contiguous range: fetch it 64 records per vector load (lane l <- record l) and
-    // take each with v_readlane — no scalar-load round trip per sample
-    const int bin0 = br * (g.W + 1) + Q0;
-    const int nbin = min(kTQ, g.W - Q0) + 1;
-    int bst[kTQ + 2];
+  const bool act = br <= g.H;
+  const bool drow = w >= 1 || br == 0;  // owns the ∂offset of this bin row
+  // the row's bins (br, Q0..Q0+kTQ) are consecutive, so their records are one
+  // contiguous range: fetch it 64 records per vector load (lane l <- record l) and
+  // take each with v_readlane — no scalar-load round trip per sample
+  const int bin0 = min(br, g.H) * (g.W + 1) + Q0;
+  const int nbin = min(kTQ, g.W - Q0) + 1;
+  int bst[kTQ + 2];
 #pragma unroll
-    for (int k = 0; k <= kTQ + 1; ++k) bst[k] = st[bin0 + min(k, nbin)];
-    const int rowlo = bst[0], rowhi = bst[nbin];
-    const int cc = cok ? c : 0;  // clamped channel: loads never need a guard
-    // Software pipeline over the row's records (contiguous across its bins): batch k+1's
-    // records (v_readlane from a 64-record page) and ∂colT rows are issued before batch
-    // k is consumed. Batches never straddle a bin, so each bin's compute keeps static
-    // accumulator indices while the prefetch flows across bin boundaries.
-    int p0 = rowlo;
-    int4 pg = p0 + lane < rowhi ? rb[p0 + lane] : make_int4(0, 0, 0, 0);
-    int4 nR[U];
-    float4 nx[U];
-    auto issue = [&](int ni) {
-      if (ni >= rowhi) return;
-      if (ni + U > p0 + 64) {  // next page (rows of more than 64 samples)
-        p0 = ni;
-        pg = p0 + lane < rowhi ? rb[p0 + lane] : make_int4(0, 0, 0, 0);
-      }
+  for (int k = 0; k <= kTQ + 1; ++k) bst[k] = act ? st[bin0 + min(k, nbin)] : 0;
+  const int rowlo = bst[0], rowhi = bst[nbin];
+  const int cc = cok ? c : 0;  // clamped channel: loads never need a guard
+  // Software pipeline over the row's records (contiguous across its bins): batch k+1's
+  // records (v_readlane from a 64-record page) and ∂colT rows are issued before batch
+  // k is consumed. Batches never straddle a bin, so each bin's compute keeps static
+  // accumulator indices while the prefetch flows across bin boundaries.
+  int p0 = rowlo;
+  int4 pg = p0 + lane < rowhi ? rb[p0 + lane] : make_int4(0, 0, 0, 0);
+  int4 nR[U];
+  float4 nx[U];
+  auto issue = [&](int ni) {
+    if (ni >= rowhi) return;
+    if (ni + U > p0 + 64) {  // next page (rows of more than 64 samples)
+      p0 = ni;
+      pg = p0 + lane < rowhi ? rb[p0 + lane] : make_int4(0, 0, 0, 0);
+    }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int l = min(ni + u, rowhi - 1) - p0;
-        nR[u] = make_int4(__builtin_amdgcn_readlane(pg.x, l), __builtin_amdgcn_readlane(pg.y, l),
-                          __builtin_amdgcn_readlane(pg.z, l), __builtin_amdgcn_readlane(pg.w, l));
-      }
+    for (int u = 0; u < U; ++u) {
+      const int l = min(ni + u, rowhi - 1) - p0;
+      nR[u] = make_int4(__builtin_amdgcn_readlane(pg.x, l), __builtin_amdgcn_readlane(pg.y, l),
+                        __builtin_amdgcn_readlane(pg.z, l), __builtin_amdgcn_readlane(pg.w, l));
+    }
 #pragma unroll
-      for (int u = 0; u < U; ++u) nx[u] = ld4(gb + nR[u].x + cc);
-    };
-    issue(rowlo);
+    for (int u = 0; u < U; ++u) nx[u] = ld4(gb + nR[u].x + cc);
+  };
+  issue(rowlo);  // (nothing for a wave past the last bin row: rowlo == rowhi == 0)
+#pragma unroll
+  for (int k = 0; k < WIT; ++k)
+    if (tid + k * kC2iThreads < WIN) lds[tid + k * kC2iThreads] = wv[k];
+  lds_barrier();
+  if (act) {
 #pragma unroll
     for (int bj = 0; bj <= kTQ; ++bj) {
       if (bj >= nbin) break;
@@ -1091,6 +1102,8 @@ template <typename GT, typename XT>
 static void launch_k5_fused(const Geo& g, const XT* xT, const BinsWs& P, const GT* gcolT,
                             float* gxT, float* goff, int b0, int nb, hipStream_t s) {
   const int tr_n = (g.H + kTR - 1) / kTR, tq_n = (g.W + 4 - 1) / 4;
+  // U = 2 rows in flight per wave for both element types: U = 4 for the half-length bf16
+  // rows measured slower (r02, config 4: 0.192 against 0.187 ms; 95 VGPRs, 5 waves/SIMD)
   hipLaunchKernelGGL((col2im_tile<2, 4, GT, XT>), dim3(tr_n * tq_n, 1, nb), dim3(kC2iThreads), 0,
                      s, g, xT, P.brec, P.start, gcolT, gxT, goff, b0, tq_n);
 }
