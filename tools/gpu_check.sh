@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 TAG=${1:-r01}
 STEPS=${STEPS:-10}
 echo "== pytest -m gpu" && \
-timeout -k 10 420 python -m pytest tests -m gpu -q -rf > gpurun_out/pytest_gpu_$TAG.log 2>&1; rc=$?
+timeout -k 10 420 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1; rc=$?
 tail -25 gpurun_out/pytest_gpu_$TAG.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || { echo "pytest aborted rc=$rc"; exit $rc; }
 echo "== smoke" && \
