@@ -139,7 +139,8 @@ WsLayout ws_layout(const Geo& g, bool bwd) {
     // (which always uses the forward-only layout) wrote
     L.x32 = take((size_t)g.B * g.C * g.HWi * f);
     L.xT32 = take((size_t)g.B * g.C * g.HWi * f);  // fp32 channels-last x (VALU fallbacks)
-    L.wb16 = take(dcn::offset_fwd_bf16_wb_elems(g) * sizeof(dcn::bf16_t));
+    L.wb16 = take(std::max(dcn::offset_fwd_bf16_wb_elems(g), dcn::offset_bwd_bf16_wc_elems(g)) *
+                  sizeof(dcn::bf16_t));
     L.woff32 = take((size_t)g.J * g.C * g.N * f);
     L.boff32 = take((size_t)g.J * f);
     L.b32 = take((size_t)g.O * f);
@@ -619,7 +620,12 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
                                     g.B, true, st));
   }
   ProfScope ps(h, DCN_K_OFFSET_BWD);
-  if (dcn::offset_bwd_chunkable(g)) {
+  if (dcn::offset_bwd_bf16_ok(g)) {
+    // bf16 MFMA: bf16 x and w_off, the fp32 ∂offset split into two bf16 planes; writes the
+    // bf16 grad_x directly (transpose of the sampling route + the offset-conv route)
+    HIP_TRY(dcn::launch_offset_conv_bwd_bf16(g, x, w_off, goff32, F32(L.gxT), BF(L.wb16),
+                                             F32(L.goffT), gx, F32(L.gwo32), F32(L.gbo32), st));
+  } else if (dcn::offset_bwd_chunkable(g)) {
     // f32 MFMA on the bf16 xT (exact products of the bf16 values) and the fp32 ∂offset
     HIP_TRY(dcn::launch_offset_bwd_prep(g, F32(L.woff32), F32(L.wt), st));
     HIP_TRY(dcn::launch_offset_bwd_chunk(g, xT, true, goff32, F32(L.goffT), F32(L.wt), gx32,
@@ -633,7 +639,7 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
                                         F32(L.wt), gx32, F32(L.gwo32), F32(L.gbo32), F32(L.gxT),
                                         st));
   }
-  HIP_TRY(dcn::launch_f32_to_bf16(gx32, gx, nx, st));
+  if (!dcn::offset_bwd_bf16_ok(g)) HIP_TRY(dcn::launch_f32_to_bf16(gx32, gx, nx, st));
   if (goff_out) HIP_TRY(dcn::launch_f32_to_bf16(goff32, goff_out, noff, st));
   if (exch) return grads_final(h, F32(L.gwo32), F32(L.gbo32), g, gw_off, gb_off);
   HIP_TRY(dcn::launch_f32_to_bf16(F32(L.gwo32), gw_off, nwo, st));

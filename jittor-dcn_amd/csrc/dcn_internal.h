@@ -84,6 +84,15 @@ size_t offset_fwd_bf16_wb_elems(const Geo& g);
 hipError_t launch_offset_conv_fwd_bf16(const Geo& g, const bf16_t* xT, const bf16_t* w_off,
                                        const float* b_off, float* off32, bf16_t* off, bf16_t* wb,
                                        hipStream_t s);
+// DCN_BF16 offset-conv backward on bf16 MFMA (stride 1, C % 64 == 0, H·W % 8 == 0): gx is
+// the bf16 NCHW grad_x = transpose(gxT_in) + the offset-conv route. part: the goffT scratch;
+// wc: offset_bwd_bf16_wc_elems(g) bf16 values.
+bool offset_bwd_bf16_ok(const Geo& g);
+size_t offset_bwd_bf16_wc_elems(const Geo& g);
+hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16_t* w_off,
+                                       const float* goff, const float* gxT_in, bf16_t* wc,
+                                       float* part, bf16_t* gx, float* gw_off, float* gb_off,
+                                       hipStream_t s);
 // xT: channels-last x; goffT: scratch of offset_conv_goffT_floats(g). gxT_in == NULL:
 // grad_x is accumulated; else grad_x = transpose(gxT_in) + the offset-conv route, written
 // once (gxT_in: the sampling-route ∂x left channels-last by launch_col2im_*).

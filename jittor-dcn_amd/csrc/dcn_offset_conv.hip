@@ -804,6 +804,11 @@ __global__ __launch_bounds__(256) void woff_to_tjc_bf16(const bf16_t* __restrict
 __device__ __forceinline__ bf16x8_t ld_bf16x8(const bf16_t* p) {
   return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(p));
 }
+// the same from an address that is only 8-byte aligned (two 8-byte loads)
+__device__ __forceinline__ bf16x8_t ld_bf16x8_a8(const bf16_t* p) {
+  const uint2 lo = *reinterpret_cast<const uint2*>(p), hi = *reinterpret_cast<const uint2*>(p + 4);
+  return __builtin_bit_cast(bf16x8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
+}
 
 template <int SPT>  // 16-channel k-steps per tap and wave, loads issued together
 __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16(
@@ -912,6 +917,306 @@ hipError_t launch_offset_conv_fwd_bf16(const Geo& g, const bf16_t* xT, const bf1
   else if (spt == 2) go(offset_conv_fwd_mfma_bf16<2>);
   else if (spt == 3) go(offset_conv_fwd_mfma_bf16<3>);
   else go(offset_conv_fwd_mfma_bf16<4>);  // C <= 256 on the bf16 path
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// K7 on the bf16 matrix cores (DCN_BF16, stride 1). x and w_off are bf16 values; the fp32
+// ∂offset is split exactly-enough into hi = bf16(g) and lo = bf16(g - hi) (|g - hi - lo|
+// <= 2^-16 |g|), each product is exact in fp32 and the sums are fp32, so the results
+// match the fp32 kernels' to about fp32 rounding before their final bf16 rounding.
+// K index k = tap·J8 + j (offset channels padded to J8 = a multiple of 8), so a lane's 8
+// consecutive k are 8 consecutive offset channels of one tap: one 32-B run of the staged
+// ∂offset rows S[(sr·SW + sc)·J8 + j] (stage_goff8: the f32 kernels' staging with a J8
+// stride and zero padding channels).
+//   ∂x_b[c][q]      = Σ_k Wc[c][k] · G[q][k]     M = c, N = q (pixels), K = (tap, j)
+//   ∂w_off[j][c][t] = Σ_q x[c][q]  · G[q][k]     M = c, N = k,          K = q
+// with G[q][t·J8 + j] = ∂off[j][q - shift_t] = S[base(q) + toff8(t) + j].
+// ---------------------------------------------------------------------------
+__host__ __device__ static inline int j8(int J) { return (J + 7) / 8 * 8; }
+__host__ __device__ static inline int kt16(const Geo& g) {
+  return (g.kh * g.kw * j8(g.J) + 15) / 16 * 16;
+}
+
+// Wc[c][t·J8 + j] = w_off[j][c][t] (bf16), 0 for padding
+__global__ __launch_bounds__(256) void woff_to_ck_bf16(const bf16_t* __restrict__ w,
+                                                      bf16_t* __restrict__ wc, int J, int J8,
+                                                      int C, int KK, int KT16) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= C * KT16) return;
+  const int c = i / KT16, k = i - c * KT16;
+  const int t = k / J8, j = k - t * J8;
+  wc[i] = (t < KK && j < J) ? w[((size_t)j * C + c) * KK + t] : (bf16_t)0;
+}
+
+__device__ __forceinline__ void stage_goff8(const Geo& g, const float* __restrict__ goff, int b,
+                                            int y0, int SR, int SW, int J8, float* S) {
+  constexpr int kU = 8;
+  const int plane = SR * SW, n = plane * J8;
+  const unsigned mp = 0xffffffffu / (unsigned)plane + 1u, ms = 0xffffffffu / (unsigned)SW + 1u;
+  const float* gb = goff + (size_t)b * g.J * g.HW;
+  for (int i0 = threadIdx.x; i0 < n; i0 += blockDim.x * kU) {
+    float v[kU];
+    int dst[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {  // sc fastest: coalesced reads
+      const int idx = min(i0 + u * (int)blockDim.x, n - 1);
+      const int j = (int)__umulhi((unsigned)idx, mp), rem = idx - j * plane;
+      const int sr = (int)__umulhi((unsigned)rem, ms), sc = rem - sr * SW;
+      const int ho = y0 + sr - (g.kh - 1) * g.dh + g.ph, wo = sc - (g.kw - 1) * g.dw + g.pw;
+      const bool ok = j < g.J && ho >= 0 && ho < g.Ho && wo >= 0 && wo < g.Wo;
+      const int hc = min(max(ho, 0), g.Ho - 1), wc = min(max(wo, 0), g.Wo - 1);
+      v[u] = gb[(size_t)min(j, g.J - 1) * g.HW + hc * g.Wo + wc];
+      v[u] = ok ? v[u] : 0.f;
+      dst[u] = rem * J8 + j;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (i0 + u * (int)blockDim.x < n) S[dst[u]] = v[u];
+  }
+}
+
+__device__ __forceinline__ int toff8(const Geo& g, int t, int SW, int J8) {
+  const int i = t / g.kw, k = t - i * g.kw;
+  return ((g.kh - 1 - i) * g.dh * SW + (g.kw - 1 - k) * g.dw) * J8;
+}
+
+// 8 fp32 -> (hi, lo) bf16 fragments
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8_t& hi, bf16x8_t& lo) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const __bf16 h = (__bf16)v[e];
+    hi[e] = h;
+    lo[e] = (__bf16)(v[e] - (float)h);
+  }
+}
+
+// ∂x: block = 64 input pixels of one image (2 N-tiles) x all channels; wave w = channels
+// 64w..64w+63 (2 M-tiles); D[c][q] + the sampling route's channels-last ∂x, written as
+// bf16 NCHW (the API's grad_x).
+__global__ __launch_bounds__(256) void offset_dgrad_bf16(Geo g, const bf16_t* __restrict__ wc,
+                                                        int KT16, const float* __restrict__ goff,
+                                                        const float* __restrict__ gxT_in,
+                                                        bf16_t* __restrict__ gx, int spi) {
+  extern __shared__ float S[];
+  const int J8 = j8(g.J), KK = g.kh * g.kw, KT = KK * J8;
+  const int bid = blockIdx.x;
+  const int b = bid / spi, p0 = (bid - b * spi) * kDgPx;
+  const int np = min(kDgPx, g.HWi - p0);
+  const int y0 = p0 / g.W, y1 = (p0 + np - 1) / g.W;
+  const int SW = g.W + (g.kw - 1) * g.dw;
+  stage_goff8(g, goff, b, y0, y1 - y0 + 1 + (g.kh - 1) * g.dh, SW, J8, S);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int cw = 64 * w;
+  if (cw >= g.C) return;
+  int base[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int p = p0 + min(32 * u + r, np - 1);
+    const int y = p / g.W, x = p - y * g.W;
+    base[u] = ((y - y0) * SW + x) * J8;
+  }
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[m][u][i] = 0.f;
+  const bf16_t* wr0 = wc + (size_t)(cw + r) * KT16 + 8 * hh;
+  const bf16_t* wr1 = wr0 + (size_t)32 * KT16;
+  for (int k0 = 0; k0 < KT16; k0 += 16) {
+    const int k = k0 + 8 * hh;  // this lane's 8 k: one tap, offset channels j0..j0+7
+    const int t = k / J8, j0 = k - t * J8;
+    const bf16x8_t a0 = ld_bf16x8(wr0 + k0), a1 = ld_bf16x8(wr1 + k0);
+    bf16x8_t bh[2], bl[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float v[8];
+      if (k < KT) {
+        const float4* sp = reinterpret_cast<const float4*>(S + base[u] + toff8(g, t, SW, J8) + j0);
+        const float4 q0 = sp[0], q1 = sp[1];
+        v[0] = q0.x, v[1] = q0.y, v[2] = q0.z, v[3] = q0.w;
+        v[4] = q1.x, v[5] = q1.y, v[6] = q1.z, v[7] = q1.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = 0.f;
+      }
+      split8(v, bh[u], bl[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bh[u], acc[0][u], 0, 0, 0);
+      acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bh[u], acc[1][u], 0, 0, 0);
+      acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bl[u], acc[0][u], 0, 0, 0);
+      acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bl[u], acc[1][u], 0, 0, 0);
+    }
+  }
+  // D[row c][col q]: register i of lane (r, hh) = row (i&3) + 8(i>>2) + 4hh, column r
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int pl = 32 * u + r;
+    if (pl >= np) continue;
+    const size_t p = (size_t)p0 + pl;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {  // 4 consecutive channels per register group
+        const int c = cw + 32 * m + 8 * gq + 4 * hh;
+        if (c >= g.C) continue;  // C % 32 == 0 on this path
+        const float4 tv = *reinterpret_cast<const float4*>(gxT_in + ((size_t)b * g.HWi + p) * g.C + c);
+        bf16_t* d = gx + ((size_t)b * g.C + c) * g.HWi + p;
+        d[0] = f2bf(tv.x + acc[m][u][4 * gq + 0]);
+        d[g.HWi] = f2bf(tv.y + acc[m][u][4 * gq + 1]);
+        d[2 * (size_t)g.HWi] = f2bf(tv.z + acc[m][u][4 * gq + 2]);
+        d[3 * (size_t)g.HWi] = f2bf(tv.w + acc[m][u][4 * gq + 3]);
+      }
+  }
+}
+
+// ∂w_off partials: block = (chunk of rowsB input rows of one image, 64 channels); wave w
+// owns N-tiles w and w+4 of the KT16/32 (t, j) tiles x both 32-channel M-tiles.
+// part[chunk][c][j·KK + t] (the f32 kernel's format: wgrad_mfma_reduce folds it).
+__global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __restrict__ x,
+                                                        const float* __restrict__ goff,
+                                                        float* __restrict__ part, int rowsB,
+                                                        int cpi) {
+  extern __shared__ float S[];
+  const int J8 = j8(g.J), KK = g.kh * g.kw, KT = KK * J8;
+  const int chunk = blockIdx.x;
+  const int b = chunk / cpi, y0 = (chunk - b * cpi) * rowsB;
+  const int nrows = min(rowsB, g.H - y0);
+  const int SW = g.W + (g.kw - 1) * g.dw;
+  stage_goff8(g, goff, b, y0, nrows + (g.kh - 1) * g.dh, SW, J8, S);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int cb = blockIdx.y * 64;
+  const int NTt = (KT + 31) / 32;  // 32-wide (t, j) tiles
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[m][u][i] = 0.f;
+  // this lane's N column in each owned tile: k = 32·tile + r = t·J8 + j
+  int kofs[2];
+  bool kok[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int kk = 32 * (w + 4 * u) + r;
+    kok[u] = (w + 4 * u) < NTt && kk < KT;
+    const int t = kk / J8, j = kk - t * J8;
+    kofs[u] = kok[u] ? toff8(g, t, SW, J8) + j : 0;
+  }
+  const bool own1 = (w + 4) < NTt;  // wave-uniform
+  const int npx = nrows * g.W;  // a multiple of 4 (W % 4 == 0)
+  const bf16_t* xr0 = x + ((size_t)b * g.C + cb + r) * g.HWi + (size_t)y0 * g.W;
+  const bf16_t* xr1 = xr0 + (size_t)32 * g.HWi;
+  // (row, column) in the chunk of this lane's first pixel q = q0 + 8hh: q and W are
+  // multiples of 4, so pixels q..q+3 share a row, as do q+4..q+7
+  int yq = (8 * hh) / g.W, xq = 8 * hh - yq * g.W;
+  for (int q = 8 * hh; q - 8 * hh < npx; q += 16) {
+    bf16x8_t a0 = bf16x8_t{}, a1 = bf16x8_t{};
+    if (q + 8 <= npx) {  // 8-B aligned runs (H·W % 8 == 0, y0·W % 4 == 0)
+      a0 = ld_bf16x8_a8(xr0 + q);
+      a1 = ld_bf16x8_a8(xr1 + q);
+    } else if (q < npx) {  // the chunk's ragged end (4 pixels): never read past it
+      const uint2 l0 = *reinterpret_cast<const uint2*>(xr0 + q);
+      const uint2 l1 = *reinterpret_cast<const uint2*>(xr1 + q);
+      a0 = __builtin_bit_cast(bf16x8_t, make_uint4(l0.x, l0.y, 0u, 0u));
+      a1 = __builtin_bit_cast(bf16x8_t, make_uint4(l1.x, l1.y, 0u, 0u));
+    }
+    const int s0 = (yq * SW + xq) * J8;
+    const int s1 = xq + 4 < g.W ? s0 + 4 * J8 : (yq + 1) * SW * J8;
+    const bool ok0 = q < npx, ok1 = q + 4 < npx;
+    bf16x8_t bh[2], bl[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = (ok0 && kok[u]) ? S[s0 + e * J8 + kofs[u]] : 0.f;
+        v[4 + e] = (ok1 && kok[u]) ? S[s1 + e * J8 + kofs[u]] : 0.f;
+      }
+      split8(v, bh[u], bl[u]);
+    }
+    xq += 16;
+    while (xq >= g.W) xq -= g.W, ++yq;
+    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bh[0], acc[0][0], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bh[0], acc[1][0], 0, 0, 0);
+    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bl[0], acc[0][0], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bl[0], acc[1][0], 0, 0, 0);
+    if (own1) {
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bh[1], acc[0][1], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bh[1], acc[1][1], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bl[1], acc[0][1], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bl[1], acc[1][1], 0, 0, 0);
+    }
+  }
+  // D[row c][col k]: register i of lane (r, hh) = row (i&3) + 8(i>>2) + 4hh, column r
+  const int TJ = g.J * KK;
+  float* pp = part + (size_t)chunk * g.C * TJ;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (!kok[u]) continue;
+    const int kk = 32 * (w + 4 * u) + r;
+    const int t = kk / J8, j = kk - t * J8;
+    if (j >= g.J) continue;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int c = cb + 32 * m + (i & 3) + 8 * (i >> 2) + 4 * hh;
+        if (c < g.C) pp[(size_t)c * TJ + j * KK + t] = acc[m][u][i];
+      }
+  }
+}
+
+// Which bf16 offset backwards the MFMA kernels take (else the fp32 ones on fp32 copies)
+static void bwd_bf16_lds(const Geo& g, const MfmaStage& ms, size_t* lds_w, size_t* lds_x) {
+  const size_t row = (size_t)ms.SW * j8(g.J) * sizeof(float);
+  *lds_w = (size_t)(ms.rowsB + (g.kh - 1) * g.dh) * row;
+  *lds_x = (size_t)ms.SRx * row;
+}
+bool offset_bwd_bf16_ok(const Geo& g) {
+  MfmaStage ms;
+  // (H·W % 8 and W % 4: a chunk's pixel runs start 8-byte aligned in every channel plane)
+  if (!(g.dt == DCN_BF16 && mfma_stage(g, &ms) && g.C % 64 == 0 && g.HWi % 8 == 0 &&
+        g.W % 4 == 0 && g.kh * g.kw * j8(g.J) <= 256 && !get_force_generic()))
+    return false;
+  size_t lw, lx;
+  bwd_bf16_lds(g, ms, &lw, &lx);
+  return lw <= (size_t)kMfmaLds && lx <= (size_t)kMfmaLds;
+}
+size_t offset_bwd_bf16_wc_elems(const Geo& g) { return (size_t)g.C * kt16(g); }
+
+// DCN_BF16 offset-conv backward: x bf16 NCHW, w_off bf16, goff fp32; writes gw_off /
+// gb_off (fp32) and gx (bf16 NCHW) = transpose(gxT_in) + the offset-conv route.
+// part: the goffT scratch (offset_conv_goffT_floats); wc: offset_bwd_bf16_wc_elems.
+hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16_t* w_off,
+                                       const float* goff, const float* gxT_in, bf16_t* wc,
+                                       float* part, bf16_t* gx, float* gw_off, float* gb_off,
+                                       hipStream_t s) {
+  MfmaStage ms;
+  if (!offset_bwd_bf16_ok(g) || !mfma_stage(g, &ms)) return hipErrorInvalidValue;
+  const int KK = g.kh * g.kw, J8 = j8(g.J), KT16 = kt16(g);
+  const int n = g.C * KT16;
+  hipLaunchKernelGGL(woff_to_ck_bf16, dim3((n + 255) / 256), dim3(256), 0, s, w_off, wc, g.J, J8,
+                     g.C, KK, KT16);
+  size_t lds_w, lds_x;
+  bwd_bf16_lds(g, ms, &lds_w, &lds_x);
+  hipLaunchKernelGGL(offset_wgrad_bf16, dim3(g.B * ms.cpi, g.C / 64), dim3(256), lds_w, s, g, x,
+                     goff, part, ms.rowsB, ms.cpi);
+  const long E = (long)g.C * g.J * KK;
+  hipLaunchKernelGGL(wgrad_mfma_reduce, dim3((unsigned)((E + 63) / 64)), dim3(1024), 0, s, g,
+                     part, g.B * ms.cpi, gw_off);
+  if (gb_off) launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
+  hipLaunchKernelGGL(offset_dgrad_bf16, dim3(g.B * ms.spi), dim3(256), lds_x, s, g, wc, KT16, goff,
+                     gxT_in, gx, ms.spi);
   return hipGetLastError();
 }
 

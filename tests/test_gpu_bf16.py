@@ -133,6 +133,11 @@ def _bf16_sweep(i):
     dict(seed=2, B=3, C=32, O_=16, H=17, W=15, s=(2, 2)),
     dict(seed=3, B=1, C=256, O_=64, H=14, W=14, off_scale=2.0),
     dict(seed=4, B=2, C=12, O_=8, H=11, W=13),
+    # the bf16 MFMA offset-conv backward (C % 64, H·W % 8, W % 4): ragged 5-row ∂W_off
+    # chunks (60 px: a 4-pixel tail), W = 4 (a k-step spans four rows), 3 channel waves
+    dict(seed=5, B=3, C=64, O_=32, H=10, W=12, off_scale=2.0),
+    dict(seed=6, B=2, C=128, O_=64, H=8, W=4),
+    dict(seed=7, B=1, C=192, O_=16, H=13, W=16, off_scale=2.5),
 ] + [_bf16_sweep(i) for i in range(6)])
 def test_bf16_forward_backward_vs_oracle(gpu_handle, case):
     bits, v, s = _case(**case)
@@ -172,12 +177,15 @@ def test_bf16_config4_full_size_every_tensor(gpu_handle):
     assert not bad, f"bf16 relative errors {errs}"
 
 
-@pytest.mark.parametrize("k,pad", [((1, 3), (0, 1)), ((3, 1), (1, 0)), ((2, 2), (1, 1))])
-def test_bf16_nonsquare_kernels_vs_oracle(gpu_handle, k, pad):
+@pytest.mark.parametrize("k,pad,C,H,W", [((1, 3), (0, 1), 24, 13, 11), ((3, 1), (1, 0), 24, 13, 11),
+                                         ((2, 2), (1, 1), 24, 13, 11),
+                                         ((1, 3), (0, 1), 64, 9, 8), ((2, 2), (1, 1), 128, 6, 12)])
+def test_bf16_nonsquare_kernels_vs_oracle(gpu_handle, k, pad, C, H, W):
     """kh*kw outside {1,4,6,9} takes the generic offset-conv backward, which reads the fp32
     copy of x that the forward left in the workspace (the layouts of dcn_forward and
-    dcn_backward share that region): ∂W_off must match the oracle."""
-    bits, v, s = _case(31, B=2, C=24, O_=16, H=13, W=11, k=k, p=pad)
+    dcn_backward share that region): ∂W_off must match the oracle. With C % 64 == 0 the
+    bf16 MFMA backward takes them instead (J = 6 and 8 offset channels: J8 padding)."""
+    bits, v, s = _case(31, B=2, C=C, O_=16, H=H, W=W, k=k, p=pad)
     out, off, g = _device(gpu_handle, bits, s, pad=pad)
     ro, _, cache = O.forward(v["x"], v["w_off"], v["b_off"], v["w"], v["b"], s, pad,
                              offsets=off)
