@@ -15,6 +15,7 @@
 namespace dcn {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // ---- bf16 storage (DCN_BF16): round-to-nearest-even conversions (v_cvt_pk_bf16_f32) and
 // 4-channel loads / stores, so kernels can be templated on the element type.

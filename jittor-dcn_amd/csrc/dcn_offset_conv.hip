@@ -790,14 +790,17 @@ __global__ __launch_bounds__(256, 4) void offset_dgrad_mfma(Geo g, const float* 
 // ---------------------------------------------------------------------------
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 
-// wb[(tap*32 + j)*Cp + c] = w_off[j][c][tap] (bf16), 0 for j >= J or c >= C
+// The B fragments in MFMA lane order, so a wave's B load is one contiguous 1 KiB:
+// wb[((tap*NKS + ks)*64 + lane)*8 + e] = w_off[j = lane&31][c = 16ks + 8(lane>>5) + e][tap]
+// (bf16), 0 for j >= J or c >= C; NKS = Cp/16 k-steps per tap
 __global__ __launch_bounds__(256) void woff_to_tjc_bf16(const bf16_t* __restrict__ w,
                                                        bf16_t* __restrict__ wb, int J, int C,
                                                        int Cp, int KK) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= KK * 32 * Cp) return;
-  const int c = i % Cp, tj = i / Cp;
-  const int j = tj % 32, t = tj / 32;
+  const int e = i & 7, lane = (i >> 3) & 63, tks = i >> 9;
+  const int NKS = Cp / 16, t = tks / NKS, ks = tks - t * NKS;
+  const int j = lane & 31, c = 16 * ks + 8 * (lane >> 5) + e;
   wb[i] = (j < J && c < C) ? w[((size_t)j * C + c) * KK + t] : (bf16_t)0;
 }
 
@@ -839,14 +842,14 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16(
     const int y = ho * g.sh - g.ph + i * g.dh, x = wo * g.sw - g.pw + k * g.dw;
     const bool ok = pok && y >= 0 && y < g.H && x >= 0 && x < g.W;
     const bf16_t* xp = xb + (size_t)(ok ? y * g.W + x : 0) * g.C;
-    const bf16_t* wp = wb + ((size_t)tt * 32 + r) * Cp;
+    const bf16_t* wp = wb + ((size_t)(tt * (Cp / 16) + w * SPT) * 64 + lane) * 8;
 #pragma unroll
     for (int u = 0; u < SPT; ++u) {
       const int c = c0 + 16 * u;
       const bool cin = c < g.C;  // the launcher takes C % 16 == 0: whole 8-channel runs
       ra[u] = ld_bf16x8(xp + (cin ? c : 0));
       if (!(ok && cin)) ra[u] = bf16x8_t{};
-      rb[u] = ld_bf16x8(wp + (c < Cp ? c : 0));  // zero-padded to Cp (multiple of 64)
+      rb[u] = ld_bf16x8(wp + 512 * u);  // zero-padded to Cp (multiple of 64)
     }
   };
   load(0, a[0], bv[0]);
@@ -891,6 +894,128 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16(
   }
 }
 
+// The same product with the x window in LDS: block = up to 32 output pixels of ONE output
+// row (Wo >= 16), so the window is kh input rows x SWc columns. Each wave stages its own
+// channel slice ([row][col][16·SPT channels + 8 pad] bf16: 16-B lane reads conflict-free)
+// with coalesced 128-B-per-pixel loads (zeros outside the image via buffer-resource range
+// checks), then reads its A fragments from LDS: each x byte leaves L2 once per block, not
+// once per tap and pixel, and the global loads touch whole lines (the register-direct
+// kernel's 16-B-per-pixel gathers touched 32 lines per load instruction).
+template <int SPT>
+__global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
+    Geo g, const bf16_t* __restrict__ xT, const bf16_t* __restrict__ wb, int Cp,
+    const float* __restrict__ b_off, float* __restrict__ off32, bf16_t* __restrict__ off,
+    int tpr, int SWc) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_row[];
+  constexpr int P = 16 * SPT + 8;  // LDS pixel pitch (bf16)
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const Block3 blk = xcd_block();
+  const int ho = blk.x / tpr, wo0 = (blk.x - ho * tpr) * 32, b = blk.z;
+  const int r = lane & 31, hh = lane >> 5;
+  const int KH = g.kh, KK = g.kh * g.kw;
+  bf16_t* L = reinterpret_cast<bf16_t*>(smem_row) + (size_t)w * KH * SWc * P;
+  const int cw = w * SPT * 16;  // this wave's first channel
+  {
+    const auto rx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(xT + (size_t)b * g.HWi * g.C), 0, (int)((size_t)g.HWi * g.C * 2),
+        0x00020000);
+    constexpr int CPP = 2 * SPT;  // 16-B chunks per pixel in the slice
+    const int total = KH * SWc * CPP;
+    const int x0 = wo0 * g.sw - g.pw;
+    constexpr int kU = 4;
+    for (int c0 = lane; c0 < total; c0 += 64 * kU) {
+      uint4 v[kU];
+      int dst[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int ci = c0 + 64 * u;
+        const int pix = ci / CPP, part = ci - pix * CPP;
+        const int i = pix / SWc, col = pix - i * SWc;
+        const int y = ho * g.sh - g.ph + i * g.dh, x = x0 + col;
+        const int c = cw + 8 * part;
+        const bool ok = ci < total && y >= 0 && y < g.H && x >= 0 && x < g.W && c < g.C;
+        const unsigned o = ok ? (unsigned)(((y * g.W + x) * g.C + c) * 2) : 0x80000000u;
+        const auto q = __builtin_amdgcn_raw_buffer_load_b128(rx, o, 0, 0);
+        v[u] = make_uint4(q[0], q[1], q[2], q[3]);
+        dst[u] = ci < total ? pix * P + 8 * part : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (dst[u] >= 0) *reinterpret_cast<uint4*>(L + dst[u]) = v[u];
+    }
+  }
+  // the wave reads only its own slice: LDS ops of one wave run in order, so only the
+  // compiler must keep the reads below the writes
+  __builtin_amdgcn_wave_barrier();
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  bf16x8_t bv[2][SPT];
+  // lanes past the row's last pixel (Wo < 32) read the last pixel's window (discarded)
+  const int rc = min(r, (SWc - 1 - (g.kw - 1) * g.dw) / g.sw);
+  auto ldb = [&](int t, bf16x8_t(&rb)[SPT]) {
+    const int tt = min(t, KK - 1);
+    const bf16_t* wp = wb + ((size_t)(tt * (Cp / 16) + w * SPT) * 64 + lane) * 8;
+#pragma unroll
+    for (int u = 0; u < SPT; ++u) rb[u] = ld_bf16x8(wp + 512 * u);
+  };
+  auto mma = [&](int t, const bf16x8_t(&rb)[SPT]) {
+    const int i = t / g.kw, k = t - i * g.kw;
+    const bf16_t* ap = L + (i * SWc + rc * g.sw + k * g.dw) * P + 8 * hh;
+    bf16x8_t a[SPT];
+#pragma unroll
+    for (int u = 0; u < SPT; ++u) a[u] = ld_bf16x8(ap + 16 * u);
+#pragma unroll
+    for (int u = 0; u < SPT; ++u)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[u], rb[u], acc, 0, 0, 0);
+  };
+  ldb(0, bv[0]);
+  for (int t = 0; t < KK; t += 2) {
+    ldb(t + 1, bv[1]);
+    mma(t, bv[0]);
+    if (t + 1 >= KK) break;
+    ldb(t + 2, bv[0]);
+    mma(t + 1, bv[1]);
+  }
+  // fold the 4 channel partials in wave order through the (now free) window LDS
+  __syncthreads();
+  f32x16* red = reinterpret_cast<f32x16*>(smem_row);
+  if (w > 0) red[(w - 1) * 64 + lane] = acc;
+  __syncthreads();
+  if (w != 0) return;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const f32x16 o = red[q * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] += o[i];
+  }
+  float(*T)[33] = reinterpret_cast<float(*)[33]>(smem_row + 3 * 64 * sizeof(f32x16));
+  const float bj = r < g.J ? b_off[r] : 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) T[r][(i & 3) + 8 * (i >> 2) + 4 * hh] = bf2f(f2bf(acc[i] + bj));
+  __builtin_amdgcn_wave_barrier();
+  if (wo0 + r < g.Wo) {
+    const int pp = ho * g.Wo + wo0 + r;
+    for (int j = hh; j < g.J; j += 2) {
+      const float v = T[j][r];
+      const size_t o = ((size_t)b * g.J + j) * g.HW + pp;
+      off32[o] = v;
+      off[o] = f2bf(v);  // exact: v is a bf16 value
+    }
+  }
+}
+
+// LDS bytes of offset_conv_fwd_mfma_bf16_row (0: the row kernel does not apply)
+static size_t fwd_bf16_row_lds(const Geo& g, int* SWc) {
+  if (g.Wo < 16) return 0;
+  const int spt = (g.C + 63) / 64;
+  *SWc = (std::min(32, g.Wo) - 1) * g.sw + (g.kw - 1) * g.dw + 1;
+  const size_t win = (size_t)4 * g.kh * *SWc * (16 * spt + 8) * 2;
+  const size_t need = std::max(win, (size_t)3 * 64 * 64 + 32 * 33 * 4);
+  return need <= 64 * 1024 ? need : 0;
+}
+
 bool offset_fwd_mfma_bf16_ok(const Geo& g) {
   return g.dt == DCN_BF16 && g.G == 1 && g.J <= 32 && g.C % 16 == 0;
 }
@@ -909,6 +1034,20 @@ hipError_t launch_offset_conv_fwd_bf16(const Geo& g, const bf16_t* xT, const bf1
   hipLaunchKernelGGL(woff_to_tjc_bf16, dim3((n + 255) / 256), dim3(256), 0, s, w_off, wb, g.J,
                      g.C, Cp, KK);
   const int tiles = (g.HW + 31) / 32, spt = Cp / 64;  // 16-channel steps per tap and wave
+  int SWc = 0;
+  const size_t lds = exp_flag(10) ? 0 : fwd_bf16_row_lds(g, &SWc);
+  if (lds) {
+    const int tpr = (g.Wo + 31) / 32;
+    dim3 grid(tpr * g.Ho, 1, g.B);
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g, xT, wb, Cp, b_off, off32, off, tpr, SWc);
+    };
+    if (spt == 1) go(offset_conv_fwd_mfma_bf16_row<1>);
+    else if (spt == 2) go(offset_conv_fwd_mfma_bf16_row<2>);
+    else if (spt == 3) go(offset_conv_fwd_mfma_bf16_row<3>);
+    else go(offset_conv_fwd_mfma_bf16_row<4>);
+    return hipGetLastError();
+  }
   dim3 grid(tiles, 1, g.B);
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, g, xT, wb, Cp, b_off, off32, off, tiles);
