@@ -1077,13 +1077,18 @@ __host__ __device__ static inline int kt16(const Geo& g) {
   return (g.kh * g.kw * j8(g.J) + 15) / 16 * 16;
 }
 
-// Wc[c][t·J8 + j] = w_off[j][c][t] (bf16), 0 for padding
+// Wc[c][k = t·J8 + j] = w_off[j][c][t] (bf16, 0 for padding), stored in MFMA A-fragment
+// order so that a wave's A load is one contiguous 1 KiB: element e of lane l of k-step ks
+// of 32-channel M-tile mt is Wc[32mt + (l&31)][16ks + 8(l>>5) + e], at
+// wc[((mt·NKS + ks)·64 + l)·8 + e], NKS = KT16/16.
 __global__ __launch_bounds__(256) void woff_to_ck_bf16(const bf16_t* __restrict__ w,
                                                       bf16_t* __restrict__ wc, int J, int J8,
                                                       int C, int KK, int KT16) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= C * KT16) return;
-  const int c = i / KT16, k = i - c * KT16;
+  const int e = i & 7, l = (i >> 3) & 63, mks = i >> 9;
+  const int NKS = KT16 / 16, mt = mks / NKS, ks = mks - mt * NKS;
+  const int c = 32 * mt + (l & 31), k = 16 * ks + 8 * (l >> 5) + e;
   const int t = k / J8, j = k - t * J8;
   wc[i] = (t < KK && j < J) ? w[((size_t)j * C + c) * KK + t] : (bf16_t)0;
 }
@@ -1164,25 +1169,24 @@ __global__ __launch_bounds__(256) void offset_dgrad_bf16(Geo g, const bf16_t* __
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[m][u][i] = 0.f;
-  const bf16_t* wr0 = wc + (size_t)(cw + r) * KT16 + 8 * hh;
-  const bf16_t* wr1 = wr0 + (size_t)32 * KT16;
-  for (int k0 = 0; k0 < KT16; k0 += 16) {
-    const int k = k0 + 8 * hh;  // this lane's 8 k: one tap, offset channels j0..j0+7
-    const int t = k / J8, j0 = k - t * J8;
-    const bf16x8_t a0 = ld_bf16x8(wr0 + k0), a1 = ld_bf16x8(wr1 + k0);
+  const int NKS = KT16 / 16;
+  const bf16_t* wr0 = wc + ((size_t)(2 * w) * NKS * 64 + lane) * 8;  // M-tiles 2w, 2w+1
+  const bf16_t* wr1 = wr0 + (size_t)NKS * 512;
+  for (int ks = 0; ks < NKS; ++ks) {
+    const int k = 16 * ks + 8 * hh;  // this lane's 8 k: one tap, offset channels j0..j0+7
+    const bool kin = k < KT;  // the K padding step: zero operands (Wc is 0 there too)
+    const int kc = kin ? k : 0;
+    const int t = kc / J8, j0 = kc - t * J8;
+    const unsigned keep = kin ? 0xffffffffu : 0u;
+    const bf16x8_t a0 = ld_bf16x8(wr0 + 512 * ks), a1 = ld_bf16x8(wr1 + 512 * ks);
     bf16x8_t bh[2], bl[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      float v[8];
-      if (k < KT) {
-        const float4* sp = reinterpret_cast<const float4*>(S + base[u] + toff8(g, t, SW, J8) + j0);
-        const float4 q0 = sp[0], q1 = sp[1];
-        v[0] = q0.x, v[1] = q0.y, v[2] = q0.z, v[3] = q0.w;
-        v[4] = q1.x, v[5] = q1.y, v[6] = q1.z, v[7] = q1.w;
-      } else {
+      const float4* sp = reinterpret_cast<const float4*>(S + base[u] + toff8(g, t, SW, J8) + j0);
+      const float4 q0 = sp[0], q1 = sp[1];
+      float v[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = 0.f;
-      }
+      for (int e = 0; e < 8; ++e) v[e] = __uint_as_float(__float_as_uint(v[e]) & keep);
       split8(v, bh[u], bl[u]);
     }
 #pragma unroll
@@ -1233,7 +1237,6 @@ __global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 31, hh = lane >> 5;
   const int cb = blockIdx.y * 64;
-  const int NTt = (KT + 31) / 32;  // 32-wide (t, j) tiles
   f32x16 acc[2][2];
 #pragma unroll
   for (int m = 0; m < 2; ++m)
@@ -1241,17 +1244,19 @@ __global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[m][u][i] = 0.f;
-  // this lane's N column in each owned tile: k = 32·tile + r = t·J8 + j
+  // this lane's N column in each owned tile: k = 32·tile + r = t·J8 + j. A wave's second
+  // tile may not exist (w + 4 >= NTt): its MFMAs then multiply zeros, which costs that wave
+  // nothing the other waves do not spend anyway and keeps the loop free of branches.
   int kofs[2];
-  bool kok[2];
+  unsigned kmask[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int kk = 32 * (w + 4 * u) + r;
-    kok[u] = (w + 4 * u) < NTt && kk < KT;
+    const bool kok = kk < KT;
     const int t = kk / J8, j = kk - t * J8;
-    kofs[u] = kok[u] ? toff8(g, t, SW, J8) + j : 0;
+    kofs[u] = kok ? toff8(g, t, SW, J8) + j : 0;
+    kmask[u] = kok ? 0xffffffffu : 0u;
   }
-  const bool own1 = (w + 4) < NTt;  // wave-uniform
   const int npx = nrows * g.W;  // a multiple of 4 (W % 4 == 0)
   const bf16_t* xr0 = x + ((size_t)b * g.C + cb + r) * g.HWi + (size_t)y0 * g.W;
   const bf16_t* xr1 = xr0 + (size_t)32 * g.HWi;
@@ -1269,31 +1274,30 @@ __global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __
       a0 = __builtin_bit_cast(bf16x8_t, make_uint4(l0.x, l0.y, 0u, 0u));
       a1 = __builtin_bit_cast(bf16x8_t, make_uint4(l1.x, l1.y, 0u, 0u));
     }
-    const int s0 = (yq * SW + xq) * J8;
-    const int s1 = xq + 4 < g.W ? s0 + 4 * J8 : (yq + 1) * SW * J8;
+    // pixels past the chunk read a staged row in range (S[0..]) and are masked to zero
     const bool ok0 = q < npx, ok1 = q + 4 < npx;
+    const int s0 = ok0 ? (yq * SW + xq) * J8 : 0;
+    const int s1 = !ok1 ? 0 : xq + 4 < g.W ? s0 + 4 * J8 : (yq + 1) * SW * J8;
+    const unsigned m0 = ok0 ? 0xffffffffu : 0u, m1 = ok1 ? 0xffffffffu : 0u;
     bf16x8_t bh[2], bl[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       float v[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        v[e] = (ok0 && kok[u]) ? S[s0 + e * J8 + kofs[u]] : 0.f;
-        v[4 + e] = (ok1 && kok[u]) ? S[s1 + e * J8 + kofs[u]] : 0.f;
+        v[e] = __uint_as_float(__float_as_uint(S[s0 + e * J8 + kofs[u]]) & (m0 & kmask[u]));
+        v[4 + e] = __uint_as_float(__float_as_uint(S[s1 + e * J8 + kofs[u]]) & (m1 & kmask[u]));
       }
       split8(v, bh[u], bl[u]);
     }
     xq += 16;
     while (xq >= g.W) xq -= g.W, ++yq;
-    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bh[0], acc[0][0], 0, 0, 0);
-    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bh[0], acc[1][0], 0, 0, 0);
-    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bl[0], acc[0][0], 0, 0, 0);
-    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bl[0], acc[1][0], 0, 0, 0);
-    if (own1) {
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bh[1], acc[0][1], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bh[1], acc[1][1], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bl[1], acc[0][1], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bl[1], acc[1][1], 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bh[u], acc[0][u], 0, 0, 0);
+      acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bh[u], acc[1][u], 0, 0, 0);
+      acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bl[u], acc[0][u], 0, 0, 0);
+      acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bl[u], acc[1][u], 0, 0, 0);
     }
   }
   // D[row c][col k]: register i of lane (r, hh) = row (i&3) + 8(i>>2) + 4hh, column r
@@ -1301,7 +1305,7 @@ __global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __
   float* pp = part + (size_t)chunk * g.C * TJ;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    if (!kok[u]) continue;
+    if (!kmask[u]) continue;
     const int kk = 32 * (w + 4 * u) + r;
     const int t = kk / J8, j = kk - t * J8;
     if (j >= g.J) continue;
