@@ -439,6 +439,7 @@ struct MfmaStage {
 };
 constexpr int kMfmaLds = 64 * 1024;
 constexpr int kDgPx = 64;  // ∂x pixels per block (4 waves = 4 x 64 channels)
+constexpr int kDgTP = 68;  // bf16 ∂x epilogue: LDS pitch (floats) of a 64-channel pixel row
 constexpr int kWgMfmaRows = 7;  // config 3: 56 rows = 8 chunks, 2048 blocks = 2 full rounds
 
 static int tj_pad4(const Geo& g) { return (g.J * g.kh * g.kw + 3) / 4 * 4; }
@@ -1066,13 +1067,17 @@ hipError_t launch_offset_conv_fwd_bf16(const Geo& g, const bf16_t* xT, const bf1
 // match the fp32 kernels' to about fp32 rounding before their final bf16 rounding.
 // K index k = tap·J8 + j (offset channels padded to J8 = a multiple of 8), so a lane's 8
 // consecutive k are 8 consecutive offset channels of one tap: one 32-B run of the staged
-// ∂offset rows S[(sr·SW + sc)·J8 + j] (stage_goff8: the f32 kernels' staging with a J8
+// ∂offset rows S[(sr·SW + sc)·PJ + j] (stage_goff8: the f32 kernels' staging with a PJ
 // stride and zero padding channels).
 //   ∂x_b[c][q]      = Σ_k Wc[c][k] · G[q][k]     M = c, N = q (pixels), K = (tap, j)
 //   ∂w_off[j][c][t] = Σ_q x[c][q]  · G[q][k]     M = c, N = k,          K = q
 // with G[q][t·J8 + j] = ∂off[j][q - shift_t] = S[base(q) + toff8(t) + j].
 // ---------------------------------------------------------------------------
 __host__ __device__ static inline int j8(int J) { return (J + 7) / 8 * 8; }
+// LDS pixel pitch of the staged ∂offset rows: J8 + 4 floats (an odd number of 16-B bank
+// groups), so lanes 8 pixels apart (∂x: 16-B reads) or 8 pixels apart across the two lane
+// halves (∂W_off) fall on different banks; J8 itself put them on the same bank
+__host__ __device__ static inline int pj8(int J) { return j8(J) + 4; }
 __host__ __device__ static inline int kt16(const Geo& g) {
   return (g.kh * g.kw * j8(g.J) + 15) / 16 * 16;
 }
@@ -1094,7 +1099,7 @@ __global__ __launch_bounds__(256) void woff_to_ck_bf16(const bf16_t* __restrict_
 }
 
 __device__ __forceinline__ void stage_goff8(const Geo& g, const float* __restrict__ goff, int b,
-                                            int y0, int SR, int SW, int J8, float* S) {
+                                            int y0, int SR, int SW, int J8, int PJ, float* S) {
   constexpr int kU = 8;
   const int plane = SR * SW, n = plane * J8;
   const unsigned mp = 0xffffffffu / (unsigned)plane + 1u, ms = 0xffffffffu / (unsigned)SW + 1u;
@@ -1112,7 +1117,7 @@ __device__ __forceinline__ void stage_goff8(const Geo& g, const float* __restric
       const int hc = min(max(ho, 0), g.Ho - 1), wc = min(max(wo, 0), g.Wo - 1);
       v[u] = gb[(size_t)min(j, g.J - 1) * g.HW + hc * g.Wo + wc];
       v[u] = ok ? v[u] : 0.f;
-      dst[u] = rem * J8 + j;
+      dst[u] = rem * PJ + j;
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u)
@@ -1120,9 +1125,9 @@ __device__ __forceinline__ void stage_goff8(const Geo& g, const float* __restric
   }
 }
 
-__device__ __forceinline__ int toff8(const Geo& g, int t, int SW, int J8) {
+__device__ __forceinline__ int toff8(const Geo& g, int t, int SW, int PJ) {
   const int i = t / g.kw, k = t - i * g.kw;
-  return ((g.kh - 1 - i) * g.dh * SW + (g.kw - 1 - k) * g.dw) * J8;
+  return ((g.kh - 1 - i) * g.dh * SW + (g.kw - 1 - k) * g.dw) * PJ;
 }
 
 // 8 fp32 -> (hi, lo) bf16 fragments
@@ -1149,18 +1154,34 @@ __global__ __launch_bounds__(256) void offset_dgrad_bf16(Geo g, const bf16_t* __
   const int np = min(kDgPx, g.HWi - p0);
   const int y0 = p0 / g.W, y1 = (p0 + np - 1) / g.W;
   const int SW = g.W + (g.kw - 1) * g.dw;
-  stage_goff8(g, goff, b, y0, y1 - y0 + 1 + (g.kh - 1) * g.dh, SW, J8, S);
-  __syncthreads();
+  const int PJ = pj8(g.J);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 31, hh = lane >> 5;
   const int cw = 64 * w;
-  if (cw >= g.C) return;
+  // A = Wc fragments (L2-resident), kPf k-steps ahead in a register ring; the first ones
+  // are issued before the ∂offset staging so that their latency hides behind it
+  const int NKS = KT16 / 16;
+  const int wt = cw < g.C ? w : 0;  // idle waves (C < 256) load wave 0's (in range)
+  const bf16_t* wr0 = wc + ((size_t)(2 * wt) * NKS * 64 + lane) * 8;  // M-tiles 2w, 2w+1
+  const bf16_t* wr1 = wr0 + (size_t)NKS * 512;
+  constexpr int kPf = 3;
+  bf16x8_t ra0[kPf], ra1[kPf];
+  auto lda = [&](int ks, int d) {
+    const int kc = min(ks, NKS - 1);
+    ra0[d] = ld_bf16x8(wr0 + 512 * kc);
+    ra1[d] = ld_bf16x8(wr1 + 512 * kc);
+  };
+#pragma unroll
+  for (int d = 0; d < kPf - 1; ++d) lda(d, d);
+  stage_goff8(g, goff, b, y0, y1 - y0 + 1 + (g.kh - 1) * g.dh, SW, J8, PJ, S);
+  __syncthreads();
+  const bool live = cw < g.C;  // (C < 256: idle waves still meet the epilogue barrier)
   int base[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int p = p0 + min(32 * u + r, np - 1);
     const int y = p / g.W, x = p - y * g.W;
-    base[u] = ((y - y0) * SW + x) * J8;
+    base[u] = ((y - y0) * SW + x) * PJ;
   }
   f32x16 acc[2][2];
 #pragma unroll
@@ -1169,53 +1190,69 @@ __global__ __launch_bounds__(256) void offset_dgrad_bf16(Geo g, const bf16_t* __
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[m][u][i] = 0.f;
-  const int NKS = KT16 / 16;
-  const bf16_t* wr0 = wc + ((size_t)(2 * w) * NKS * 64 + lane) * 8;  // M-tiles 2w, 2w+1
-  const bf16_t* wr1 = wr0 + (size_t)NKS * 512;
-  for (int ks = 0; ks < NKS; ++ks) {
-    const int k = 16 * ks + 8 * hh;  // this lane's 8 k: one tap, offset channels j0..j0+7
-    const bool kin = k < KT;  // the K padding step: zero operands (Wc is 0 there too)
-    const int kc = kin ? k : 0;
-    const int t = kc / J8, j0 = kc - t * J8;
-    const unsigned keep = kin ? 0xffffffffu : 0u;
-    const bf16x8_t a0 = ld_bf16x8(wr0 + 512 * ks), a1 = ld_bf16x8(wr1 + 512 * ks);
-    bf16x8_t bh[2], bl[2];
+  for (int ks0 = 0; ks0 < (live ? NKS : 0); ks0 += kPf) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const float4* sp = reinterpret_cast<const float4*>(S + base[u] + toff8(g, t, SW, J8) + j0);
-      const float4 q0 = sp[0], q1 = sp[1];
-      float v[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+    for (int d = 0; d < kPf; ++d) {
+      const int ks = ks0 + d;
+      lda(ks + kPf - 1, (d + kPf - 1) % kPf);
+      __builtin_amdgcn_sched_barrier(0);
+      if (ks < NKS) {  // wave-uniform
+        const int k = 16 * ks + 8 * hh;  // this lane's 8 k: one tap, channels j0..j0+7
+        const bool kin = k < KT;  // the K padding step: zero operands (Wc is 0 there too)
+        const int kc = kin ? k : 0;
+        const int t = kc / J8, j0 = kc - t * J8;
+        const unsigned keep = kin ? 0xffffffffu : 0u;
+        bf16x8_t bh[2], bl[2];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = __uint_as_float(__float_as_uint(v[e]) & keep);
-      split8(v, bh[u], bl[u]);
-    }
+        for (int u = 0; u < 2; ++u) {
+          const float4* sp =
+              reinterpret_cast<const float4*>(S + base[u] + toff8(g, t, SW, PJ) + j0);
+          const float4 q0 = sp[0], q1 = sp[1];
+          float v[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bh[u], acc[0][u], 0, 0, 0);
-      acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bh[u], acc[1][u], 0, 0, 0);
-      acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bl[u], acc[0][u], 0, 0, 0);
-      acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bl[u], acc[1][u], 0, 0, 0);
+          for (int e = 0; e < 8; ++e) v[e] = __uint_as_float(__float_as_uint(v[e]) & keep);
+          split8(v, bh[u], bl[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra0[d], bh[u], acc[0][u], 0, 0, 0);
+          acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra1[d], bh[u], acc[1][u], 0, 0, 0);
+          acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra0[d], bl[u], acc[0][u], 0, 0, 0);
+          acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra1[d], bl[u], acc[1][u], 0, 0, 0);
+        }
+      }
     }
   }
-  // D[row c][col q]: register i of lane (r, hh) = row (i&3) + 8(i>>2) + 4hh, column r
+  // ∂x = the sampling route (channels-last gxT_in) + D, as bf16 NCHW. gxT_in is read as
+  // whole 256-B pixel rows (this wave's 64 channels) into LDS and read back per D lane
+  // (pixel r, channel of register i); the bf16 stores are 64-B pixel runs per channel.
+  __syncthreads();  // every wave is done with S: its space holds the transposes
+  if (!live) return;
+  float* T = S + w * 32 * kDgTP;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    const int pl = 32 * u + r;
-    if (pl >= np) continue;
-    const size_t p = (size_t)p0 + pl;
+    float4 tv[8];
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int it = 0; it < 8; ++it) {
+      const int pl = min(32 * u + 4 * it + (lane >> 4), np - 1);
+      tv[it] = *reinterpret_cast<const float4*>(gxT_in + ((size_t)b * g.HWi + p0 + pl) * g.C + cw +
+                                                 4 * (lane & 15));
+    }
 #pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {  // 4 consecutive channels per register group
-        const int c = cw + 32 * m + 8 * gq + 4 * hh;
-        if (c >= g.C) continue;  // C % 32 == 0 on this path
-        const float4 tv = *reinterpret_cast<const float4*>(gxT_in + ((size_t)b * g.HWi + p) * g.C + c);
-        bf16_t* d = gx + ((size_t)b * g.C + c) * g.HWi + p;
-        d[0] = f2bf(tv.x + acc[m][u][4 * gq + 0]);
-        d[g.HWi] = f2bf(tv.y + acc[m][u][4 * gq + 1]);
-        d[2 * (size_t)g.HWi] = f2bf(tv.z + acc[m][u][4 * gq + 2]);
-        d[3 * (size_t)g.HWi] = f2bf(tv.w + acc[m][u][4 * gq + 3]);
-      }
+    for (int it = 0; it < 8; ++it)
+      *reinterpret_cast<float4*>(T + (4 * it + (lane >> 4)) * kDgTP + 4 * (lane & 15)) = tv[it];
+    __builtin_amdgcn_wave_barrier();
+    if (32 * u + r < np) {
+      const size_t p = (size_t)p0 + 32 * u + r;
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int cl = 32 * m + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          gx[((size_t)b * g.C + cw + cl) * g.HWi + p] = f2bf(T[r * kDgTP + cl] + acc[m][u][i]);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();  // the next half overwrites T
   }
 }
 
@@ -1232,11 +1269,35 @@ __global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __
   const int b = chunk / cpi, y0 = (chunk - b * cpi) * rowsB;
   const int nrows = min(rowsB, g.H - y0);
   const int SW = g.W + (g.kw - 1) * g.dw;
-  stage_goff8(g, goff, b, y0, nrows + (g.kh - 1) * g.dh, SW, J8, S);
-  __syncthreads();
+  const int PJ = pj8(g.J);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 31, hh = lane >> 5;
   const int cb = blockIdx.y * 64;
+  const int npx = nrows * g.W;  // a multiple of 4 (W % 4 == 0)
+  // A = this block's 64 channel planes of x through a buffer resource, kPf steps ahead in a
+  // register ring. A step past the chunk loads nothing (offset out of range: zeros); the
+  // ragged last step's upper 4 pixels read x beyond the chunk (or zeros past the planes),
+  // which meet zero B rows.
+  const auto rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(x + ((size_t)b * g.C + cb) * g.HWi), 0, (int)(64 * (size_t)g.HWi * 2),
+      0x00020000);
+  const unsigned xl0 = (unsigned)((r * g.HWi + y0 * g.W + 8 * hh) * 2);
+  const unsigned xl1 = xl0 + (unsigned)(32 * g.HWi * 2);
+  const int nsteps = (npx + 15) / 16;
+  constexpr int kPf = 3;
+  bf16x8_t ra0[kPf], ra1[kPf];
+  auto lda = [&](int i, int d) {
+    const bool in = i < nsteps && 16 * i + 8 * hh < npx;
+    const unsigned o = (unsigned)(32 * i);
+    ra0[d] = __builtin_bit_cast(bf16x8_t,
+                                __builtin_amdgcn_raw_buffer_load_b128(rx, in ? xl0 + o : 0x80000000u, 0, 0));
+    ra1[d] = __builtin_bit_cast(bf16x8_t,
+                                __builtin_amdgcn_raw_buffer_load_b128(rx, in ? xl1 + o : 0x80000000u, 0, 0));
+  };
+#pragma unroll
+  for (int d = 0; d < kPf - 1; ++d) lda(d, d);
+  stage_goff8(g, goff, b, y0, nrows + (g.kh - 1) * g.dh, SW, J8, PJ, S);
+  __syncthreads();
   f32x16 acc[2][2];
 #pragma unroll
   for (int m = 0; m < 2; ++m)
@@ -1254,76 +1315,107 @@ __global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __
     const int kk = 32 * (w + 4 * u) + r;
     const bool kok = kk < KT;
     const int t = kk / J8, j = kk - t * J8;
-    kofs[u] = kok ? toff8(g, t, SW, J8) + j : 0;
+    kofs[u] = kok ? toff8(g, t, SW, PJ) + j : 0;
     kmask[u] = kok ? 0xffffffffu : 0u;
   }
-  const int npx = nrows * g.W;  // a multiple of 4 (W % 4 == 0)
-  const bf16_t* xr0 = x + ((size_t)b * g.C + cb + r) * g.HWi + (size_t)y0 * g.W;
-  const bf16_t* xr1 = xr0 + (size_t)32 * g.HWi;
-  // (row, column) in the chunk of this lane's first pixel q = q0 + 8hh: q and W are
+  // (row, column) in the chunk of this lane's first pixel q = 16i + 8hh: q and W are
   // multiples of 4, so pixels q..q+3 share a row, as do q+4..q+7
   int yq = (8 * hh) / g.W, xq = 8 * hh - yq * g.W;
-  for (int q = 8 * hh; q - 8 * hh < npx; q += 16) {
-    bf16x8_t a0 = bf16x8_t{}, a1 = bf16x8_t{};
-    if (q + 8 <= npx) {  // 8-B aligned runs (H·W % 8 == 0, y0·W % 4 == 0)
-      a0 = ld_bf16x8_a8(xr0 + q);
-      a1 = ld_bf16x8_a8(xr1 + q);
-    } else if (q < npx) {  // the chunk's ragged end (4 pixels): never read past it
-      const uint2 l0 = *reinterpret_cast<const uint2*>(xr0 + q);
-      const uint2 l1 = *reinterpret_cast<const uint2*>(xr1 + q);
-      a0 = __builtin_bit_cast(bf16x8_t, make_uint4(l0.x, l0.y, 0u, 0u));
-      a1 = __builtin_bit_cast(bf16x8_t, make_uint4(l1.x, l1.y, 0u, 0u));
-    }
-    // pixels past the chunk read a staged row in range (S[0..]) and are masked to zero
-    const bool ok0 = q < npx, ok1 = q + 4 < npx;
-    const int s0 = ok0 ? (yq * SW + xq) * J8 : 0;
-    const int s1 = !ok1 ? 0 : xq + 4 < g.W ? s0 + 4 * J8 : (yq + 1) * SW * J8;
-    const unsigned m0 = ok0 ? 0xffffffffu : 0u, m1 = ok1 ? 0xffffffffu : 0u;
-    bf16x8_t bh[2], bl[2];
+  for (int i0 = 0; i0 < nsteps; i0 += kPf) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      float v[8];
+    for (int d = 0; d < kPf; ++d) {
+      const int i = i0 + d;
+      lda(i + kPf - 1, (d + kPf - 1) % kPf);
+      __builtin_amdgcn_sched_barrier(0);
+      if (i < nsteps) {  // wave-uniform
+        const int q = 16 * i + 8 * hh;
+        // pixels past the chunk read a staged row in range (S[0..]) and are masked to zero
+        const bool ok0 = q < npx, ok1 = q + 4 < npx;
+        const int s0 = ok0 ? (yq * SW + xq) * PJ : 0;
+        const int s1 = !ok1 ? 0 : xq + 4 < g.W ? s0 + 4 * PJ : (yq + 1) * SW * PJ;
+        const unsigned m0 = ok0 ? 0xffffffffu : 0u, m1 = ok1 ? 0xffffffffu : 0u;
+        bf16x8_t bh[2], bl[2];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = __uint_as_float(__float_as_uint(S[s0 + e * J8 + kofs[u]]) & (m0 & kmask[u]));
-        v[4 + e] = __uint_as_float(__float_as_uint(S[s1 + e * J8 + kofs[u]]) & (m1 & kmask[u]));
+        for (int u = 0; u < 2; ++u) {
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = __uint_as_float(__float_as_uint(S[s0 + e * PJ + kofs[u]]) & (m0 & kmask[u]));
+            v[4 + e] =
+                __uint_as_float(__float_as_uint(S[s1 + e * PJ + kofs[u]]) & (m1 & kmask[u]));
+          }
+          split8(v, bh[u], bl[u]);
+        }
+        xq += 16;
+        while (xq >= g.W) xq -= g.W, ++yq;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra0[d], bh[u], acc[0][u], 0, 0, 0);
+          acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra1[d], bh[u], acc[1][u], 0, 0, 0);
+          acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra0[d], bl[u], acc[0][u], 0, 0, 0);
+          acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra1[d], bl[u], acc[1][u], 0, 0, 0);
+        }
       }
-      split8(v, bh[u], bl[u]);
-    }
-    xq += 16;
-    while (xq >= g.W) xq -= g.W, ++yq;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bh[u], acc[0][u], 0, 0, 0);
-      acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bh[u], acc[1][u], 0, 0, 0);
-      acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bl[u], acc[0][u], 0, 0, 0);
-      acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bl[u], acc[1][u], 0, 0, 0);
     }
   }
-  // D[row c][col k]: register i of lane (r, hh) = row (i&3) + 8(i>>2) + 4hh, column r
-  const int TJ = g.J * KK;
-  float* pp = part + (size_t)chunk * g.C * TJ;
+  // partials in MFMA fragment order (each lane's 16 accumulators are 64 contiguous bytes,
+  // a wave's tile one 4 KiB run): part[(((chunk·CG + cg)·NT + tile)·2 + m)·64 + lane][16]
+  // with NT = ceil(KT/32) tiles; wgrad_frag_reduce folds the chunks and scatters to ∂w_off
+  const int NT = (KT + 31) / 32, CG = g.C / 64;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    if (!kmask[u]) continue;
-    const int kk = 32 * (w + 4 * u) + r;
-    const int t = kk / J8, j = kk - t * J8;
-    if (j >= g.J) continue;
+    const int tile = w + 4 * u;
+    if (tile >= NT) continue;  // wave-uniform
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int m = 0; m < 2; ++m) {
+      float* pp = part + (((((size_t)chunk * CG + blockIdx.y) * NT + tile) * 2 + m) * 64 + lane) * 16;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int c = cb + 32 * m + (i & 3) + 8 * (i >> 2) + 4 * hh;
-        if (c < g.C) pp[(size_t)c * TJ + j * KK + t] = acc[m][u][i];
-      }
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<float4*>(pp + 4 * q) =
+            make_float4(acc[m][u][4 * q], acc[m][u][4 * q + 1], acc[m][u][4 * q + 2],
+                        acc[m][u][4 * q + 3]);
+    }
   }
+}
+
+// ∂w_off[j][c][t] = Σ_chunk (fragment-ordered partials of offset_wgrad_bf16), chunks in
+// order: 64 fragment elements per 1024-thread block, wave w sums chunks ≡ w (mod 16), the
+// 16 wave sums fold in order (deterministic); each element then lands at its (j, c, t).
+__global__ __launch_bounds__(1024) void wgrad_frag_reduce(Geo g, const float* __restrict__ part,
+                                                         int nchunk, float* __restrict__ gw) {
+  const int J8 = j8(g.J), KK = g.kh * g.kw, NT = (KK * J8 + 31) / 32;
+  const long E = (long)(g.C / 64) * NT * 2 * 1024;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long i = (long)blockIdx.x * 64 + lane;
+  const long ic = i < E ? i : 0;
+  float s = 0.f;
+#pragma unroll 4
+  for (int ch = w; ch < nchunk; ch += 16) s += part[(size_t)ch * E + ic];
+  __shared__ float red[16][64];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w != 0 || i >= E) return;
+  s = red[0][lane];
+#pragma unroll
+  for (int k = 1; k < 16; ++k) s += red[k][lane];
+  const int reg = (int)(i & 15), fl = (int)((i >> 4) & 63);
+  const long tm = i >> 10;  // ((cg·NT + tile)·2 + m)
+  const int m = (int)(tm & 1), tile = (int)((tm >> 1) % NT), cg = (int)((tm >> 1) / NT);
+  const int row = (reg & 3) + 8 * (reg >> 2) + 4 * (fl >> 5);
+  const int c = 64 * cg + 32 * m + row, k = 32 * tile + (fl & 31);
+  const int t = k / J8, j = k - t * J8;
+  if (t < KK && j < g.J) gw[((size_t)j * g.C + c) * KK + t] = s;
+}
+static size_t wgrad_frag_part_floats(const Geo& g, const MfmaStage& ms) {
+  const int NT = (g.kh * g.kw * j8(g.J) + 31) / 32;
+  return (size_t)g.B * ms.cpi * (g.C / 64) * NT * 2 * 1024;
 }
 
 // Which bf16 offset backwards the MFMA kernels take (else the fp32 ones on fp32 copies)
 static void bwd_bf16_lds(const Geo& g, const MfmaStage& ms, size_t* lds_w, size_t* lds_x) {
-  const size_t row = (size_t)ms.SW * j8(g.J) * sizeof(float);
+  const size_t row = (size_t)ms.SW * pj8(g.J) * sizeof(float);
   *lds_w = (size_t)(ms.rowsB + (g.kh - 1) * g.dh) * row;
-  *lds_x = (size_t)ms.SRx * row;
+  *lds_x = std::max((size_t)ms.SRx * row, (size_t)4 * 32 * kDgTP * sizeof(float));
 }
 bool offset_bwd_bf16_ok(const Geo& g) {
   MfmaStage ms;
@@ -1354,8 +1446,8 @@ hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16
   bwd_bf16_lds(g, ms, &lds_w, &lds_x);
   hipLaunchKernelGGL(offset_wgrad_bf16, dim3(g.B * ms.cpi, g.C / 64), dim3(256), lds_w, s, g, x,
                      goff, part, ms.rowsB, ms.cpi);
-  const long E = (long)g.C * g.J * KK;
-  hipLaunchKernelGGL(wgrad_mfma_reduce, dim3((unsigned)((E + 63) / 64)), dim3(1024), 0, s, g,
+  const long E = (long)(g.C / 64) * ((KK * J8 + 31) / 32) * 2 * 1024;
+  hipLaunchKernelGGL(wgrad_frag_reduce, dim3((unsigned)((E + 63) / 64)), dim3(1024), 0, s, g,
                      part, g.B * ms.cpi, gw_off);
   if (gb_off) launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
   hipLaunchKernelGGL(offset_dgrad_bf16, dim3(g.B * ms.spi), dim3(256), lds_x, s, g, wc, KT16, goff,
@@ -1433,6 +1525,7 @@ size_t offset_conv_goffT_floats(const Geo& g) {
   size_t n = goffT_rows_floats(g) + (size_t)w.nbx * w.ny * w.nz * kJB * w.cper;
   MfmaStage ms;
   if (mfma_stage(g, &ms)) n = std::max(n, wgrad_mfma_part_floats(g, ms));
+  if (offset_bwd_bf16_ok(g)) n = std::max(n, wgrad_frag_part_floats(g, ms));
   return n;
 }
 
