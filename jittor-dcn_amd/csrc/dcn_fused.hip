@@ -295,6 +295,7 @@ fwd_fused(Geo g, const float* __restrict__ xT, const float* __restrict__ off,
 constexpr int kBNB = 2;         // 32-px MFMA blocks per tile
 constexpr int kBP = 32 * kBNB;  // pixels per tile
 constexpr int kBS = 40;         // LDS pitch (bf16) of a pixel's 32-k slice (80 B: b128 reads conflict-free)
+constexpr int kGD = 2;          // gather ring depth (steps of corner loads in flight); even
 
 typedef __bf16 bf16x8f_t __attribute__((ext_vector_type(8)));
 
@@ -365,7 +366,7 @@ __global__ __launch_bounds__(256) void fwd_fused_bf16(Geo g, const bf16_t* __res
     float fr, fc;
     int okm;
   };
-  Gath G[2];
+  Gath G[kGD];
   bf16x8f_t a[2][2][2];  // [register set][output block][16-k half]
 
   auto kbase = [&](int s) {
@@ -441,39 +442,48 @@ __global__ __launch_bounds__(256) void fwd_fused_bf16(Geo g, const bf16_t* __res
         for (int q = 0; q < kBNB; ++q)
           acc[j][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[d][j][h], bv[h][q], acc[j][q], 0, 0, 0);
   };
-  // sched_barriers: the next steps' gathers and A loads are issued above the MFMAs and the
-  // LDS staging below them. Measured (gfx950, ROCm 7.2): when the scheduler interleaved those
-  // loads among the MFMAs, a load landing in a register an earlier-issued MFMA of the step
-  // still had to read corrupted ~3 % of the outputs, nondeterministically
-  // (tools/mfma_src_scan.py finds the pattern in the ISA; tools/fused_det.py the effect).
+  // sched_barriers: the next steps' gathers and A loads are issued above a step's MFMA block
+  // and the LDS staging below it
   auto mm = [&](int buf, int d) {
     __builtin_amdgcn_sched_barrier(0);
     mfma(buf, d);
     __builtin_amdgcn_sched_barrier(0);
   };
-
+  // A step ends with a full __syncthreads(), i.e. with every wave's loads and stores drained
+  // (vmcnt(0)), not an LDS-only barrier. Measured at config 4 (tools/fused_det.py): with
+  // lds_barrier() (gathers, A loads and column stores left in flight across the barrier)
+  // 0.01-3 % of the outputs differed from run to run in several schedules (ring depth 2 and
+  // 4, with or without s_nop padding after the MFMAs), though no LDS hazard is visible in the
+  // source; with the drain every run is bitwise identical to the unfused path.
+  auto step_barrier = [&]() { __syncthreads(); };
   __syncthreads();  // records
-  gather(0, G[0]);
-  gather(1, G[1]);
+#pragma unroll
+  for (int d = 0; d < kGD; ++d) gather(d, G[d]);
   load_a(0, 0);
   store(0, 0, G[0]);
-  lds_barrier();
-  // step s multiplies LDS buffer / A set s&1; its gather for step s+2 is issued first (two
-  // steps of memory latency in flight), then step s+1's corners (gathered a step earlier)
-  // are interpolated into the other LDS buffer. Unrolled by two: compile-time register sets.
-  for (int s = 0; s < nsteps; s += 2) {
-    gather(s + 2, G[0]);
-    load_a(s + 1, 1);
-    mm(0, 0);
-    if (s + 1 >= nsteps) break;  // workgroup-uniform
-    store(s + 1, 1, G[1]);
-    lds_barrier();
-    gather(s + 3, G[1]);
-    load_a(s + 2, 0);
-    mm(1, 1);
-    if (s + 2 >= nsteps) break;
-    store(s + 2, 0, G[0]);
-    lds_barrier();
+  step_barrier();
+  // step s multiplies LDS buffer / A set s&1 after issuing the gather of step s+kGD into the
+  // ring slot step s's corners left free (kGD steps of memory latency in flight); then step
+  // s+1's corners (gathered kGD-1 steps earlier) are interpolated into the other LDS buffer.
+  // Unrolled by kGD (even): ring slots, buffers and A sets are compile-time indices.
+  for (int s0 = 0; s0 < nsteps; s0 += kGD) {
+    bool done = false;
+#pragma unroll
+    for (int d = 0; d < kGD; ++d) {
+      if (!done) {
+        const int s = s0 + d;
+        gather(s + kGD, G[d]);
+        load_a(s + 1, (d + 1) & 1);
+        mm(d & 1, d & 1);
+        if (s + 1 >= nsteps) {
+          done = true;  // workgroup-uniform
+        } else {
+          store(s + 1, (d + 1) & 1, G[(d + 1) % kGD]);
+          step_barrier();
+        }
+      }
+    }
+    if (done) break;
   }
   // D[row o][col px]: register r of lane (c = lane&31, hh) = row (r&3) + 8(r>>2) + 4hh
 #pragma unroll
