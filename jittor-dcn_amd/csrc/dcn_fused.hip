@@ -292,7 +292,7 @@ fwd_fused(Geo g, const float* __restrict__ xT, const float* __restrict__ off,
 //     per wave load from L2, a step ahead in registers;
 //   * epilogue: + bias, bf16 rounding (the unfused path's launch_bias_to_bf16 arithmetic).
 // ---------------------------------------------------------------------------
-constexpr int kBNB = 2;         // 32-px MFMA blocks per tile
+constexpr int kBNB = 2;         // 32-px MFMA blocks per tile (4: 128-px tiles, 389 VGPRs, 282 us at config 4)
 constexpr int kBP = 32 * kBNB;  // pixels per tile
 constexpr int kBS = 40;         // LDS pitch (bf16) of a pixel's 32-k slice (80 B: b128 reads conflict-free)
 constexpr int kGD = 2;          // gather ring depth (steps of corner loads in flight); even
@@ -342,14 +342,20 @@ __global__ __launch_bounds__(256) void fwd_fused_bf16(Geo g, const bf16_t* __res
     }
     rec[tp * kFTaps + n] = r;
   }
-  // staging role: pixel sp of the tile, channels 8sq..8sq+7 of the step's 32-channel slice
+  // staging roles: pixels sp + 64u of the tile, channels 8sq..8sq+7 of the step's slice
+  constexpr int kU = kBP / 64;
   const int sp = tid >> 2, sq = tid & 3;
-  const long ps = p0 + sp;
-  const bool pv = ps < P;
-  const int bs = pv ? (int)(ps / g.HW) : 0;
-  const char* xc = reinterpret_cast<const char*>(xT) + (size_t)bs * g.HWi * g.C * 2 + sq * 16;
+  const char* xc[kU];
+  unsigned colrow[kU];
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const long ps = p0 + sp + 64 * u;
+    const bool pv = ps < P;
+    const int bs = pv ? (int)(ps / g.HW) : 0;
+    xc[u] = reinterpret_cast<const char*>(xT) + (size_t)bs * g.HWi * g.C * 2 + sq * 16;
+    colrow[u] = pv ? (unsigned)(((size_t)ps * g.K + sq * 8) * 2) : ~0u;
+  }
   const unsigned rowb = (unsigned)g.W * g.C * 2u, pixb = (unsigned)g.C * 2u;
-  const unsigned colrow = pv ? (unsigned)(((size_t)ps * g.K + sq * 8) * 2) : ~0u;
   const __amdgpu_buffer_rsrc_t col_rsrc = __builtin_amdgcn_make_buffer_rsrc(
       colT, 0, colT ? (int)((size_t)P * g.K * 2) : 0, 0x00020000);
 
@@ -366,7 +372,7 @@ __global__ __launch_bounds__(256) void fwd_fused_bf16(Geo g, const bf16_t* __res
     float fr, fc;
     int okm;
   };
-  Gath G[kGD];
+  Gath G[kGD][kU];
   bf16x8f_t a[2][2][2];  // [register set][output block][16-k half]
 
   auto kbase = [&](int s) {
@@ -381,10 +387,10 @@ __global__ __launch_bounds__(256) void fwd_fused_bf16(Geo g, const bf16_t* __res
       for (int h = 0; h < 2; ++h)
         a[d][j][h] = ld_frag(wf + ((size_t)((ob0 + j) * NKS + ks + h) * 64 + lane) * 8);
   };
-  auto gather = [&](int s0, Gath& q) {
+  auto gather1 = [&](int s0, int u, Gath& q) {
     const int s = min(s0, nsteps - 1);  // past the last step: a harmless re-gather
     const int cs = s / g.N, n = s - cs * g.N;
-    const int4 r = rec[sp * kFTaps + n];
+    const int4 r = rec[(sp + 64 * u) * kFTaps + n];
     const bool lv = r.x != INT_MIN;
     const int r0 = lv ? r.x : 0, q0 = r.y;
     q.fr = __int_as_float(r.z);
@@ -396,13 +402,13 @@ __global__ __launch_bounds__(256) void fwd_fused_bf16(Geo g, const bf16_t* __res
             ((r1ok && c0ok) ? 4 : 0) | ((r1ok && c1ok) ? 8 : 0);
     const int ra = min(max(r0, 0), g.H - 1), rb = min(r0 + 1, g.H - 1);
     const int qa = min(max(q0, 0), g.W - 1), qb = min(max(q0 + 1, 0), g.W - 1);
-    const char* base = xc + cs * 64;
+    const char* base = xc[u] + cs * 64;
     q.a = *reinterpret_cast<const uint4*>(base + ((unsigned)ra * rowb + (unsigned)qa * pixb));
     q.b = *reinterpret_cast<const uint4*>(base + ((unsigned)ra * rowb + (unsigned)qb * pixb));
     q.c = *reinterpret_cast<const uint4*>(base + ((unsigned)rb * rowb + (unsigned)qa * pixb));
     q.d = *reinterpret_cast<const uint4*>(base + ((unsigned)rb * rowb + (unsigned)qb * pixb));
   };
-  auto store = [&](int s, int buf, const Gath& q) {
+  auto store1 = [&](int s, int buf, int u, const Gath& q) {
     const int m = q.okm;
     const unsigned za = (m & 1) ? ~0u : 0u, zb = (m & 2) ? ~0u : 0u;
     const unsigned zc = (m & 4) ? ~0u : 0u, zd = (m & 8) ? ~0u : 0u;
@@ -418,11 +424,19 @@ __global__ __launch_bounds__(256) void fwd_fused_bf16(Geo g, const bf16_t* __res
       o[e] = (m & 16) ? ((unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16)) : 0u;
     }
     const uint4 v = make_uint4(o[0], o[1], o[2], o[3]);
-    *reinterpret_cast<uint4*>(&Bs[buf][sp * kBS + 8 * sq]) = v;
+    *reinterpret_cast<uint4*>(&Bs[buf][(sp + 64 * u) * kBS + 8 * sq]) = v;
     if (colT)
       __builtin_amdgcn_raw_buffer_store_b128(
           __builtin_bit_cast(u32x4, v), col_rsrc,
-          (int)(colrow == ~0u ? ~0u : colrow + (unsigned)kbase(s) * 2u), 0, kAuxNT);
+          (int)(colrow[u] == ~0u ? ~0u : colrow[u] + (unsigned)kbase(s) * 2u), 0, kAuxNT);
+  };
+  auto gather = [&](int s, Gath(&q)[kU]) {
+#pragma unroll
+    for (int u = 0; u < kU; ++u) gather1(s, u, q[u]);
+  };
+  auto store = [&](int s, int buf, const Gath(&q)[kU]) {
+#pragma unroll
+    for (int u = 0; u < kU; ++u) store1(s, buf, u, q[u]);
   };
   auto mfma = [&](int buf, int d) {
     // every B fragment of the step is read before the first MFMA (no LDS load may land in a
