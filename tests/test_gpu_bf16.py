@@ -232,8 +232,11 @@ def _fused_vs_unfused(h, case):
         h.set_fwd_path(rt.DCN_FWD_UNFUSED)
     try:
         unfused = _device(h, bits, s, pad=pad)
+        again = _device(h, bits, s, pad=pad)
     finally:
         h.set_fwd_path(rt.DCN_FWD_AUTO)
+    for k in unfused[2]:  # the unfused schedule itself is bitwise reproducible
+        np.testing.assert_array_equal(again[2][k], unfused[2][k], err_msg=f"unfused ∂{k} run to run")
     return bits, v, s, pad, fused, unfused
 
 
