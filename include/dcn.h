@@ -281,10 +281,11 @@ int dcn_get_math(dcn_handle* h, int* math);
 
 /* ---- forward schedule ----------------------------------------------------------- */
 /* How the fp32 forward (deform_conv.py:41-80) runs after the offset conv.
- * DCN_FWD_FUSED: the fused kernel (bilinear im2col gathered straight into the f32 MFMA
+ * DCN_FWD_FUSED: the fused kernel (bilinear im2col gathered straight into the MFMA
  * GEMM's LDS tiles, bias in the epilogue; the columns are still written for the backward)
- * wherever it applies: DCN_F32, deform_groups 1, kh*kw <= 9, C % 32 == 0, O % 128 == 0,
- * native math; otherwise the unfused schedule. DCN_FWD_UNFUSED: K1 im2col, then the
+ * wherever it applies: DCN_F32 (f32 MFMA) with deform_groups 1, kh*kw <= 9, C % 32 == 0,
+ * O % 128 == 0, native math; DCN_BF16 (bf16 MFMA) with deform_groups 1, kh*kw <= 9,
+ * C % 32 == 0, O % 256 == 0; otherwise the unfused schedule. DCN_FWD_UNFUSED: K1 im2col, then the
  * vendor GEMM, then the bias. DCN_FWD_AUTO (default): the schedule measured faster for the
  * geometry. Same results to fp32 rounding (the columns bit for bit). */
 typedef enum { DCN_FWD_AUTO = 0, DCN_FWD_UNFUSED = 1, DCN_FWD_FUSED = 2 } dcn_fwd_path;
@@ -302,7 +303,10 @@ int dcn_set_fwd_path(dcn_handle* h, int path);
  *   7  n > 0: output rows per wave of the VALU ∂w_off kernel (default 4)
  *   8  1: fused forward workgroup shape 0 (4 waves x 2 per CU) instead of shape 1
  *   9  n > 0: bf16/fp32 ∂W as n grouped GEMMs; n < 0: one GEMM per image
- * Slots 0, 1, 3 and 10-15 are unused. */
+ *  10  1: bf16 offset conv forward on the register-direct MFMA kernel instead of the
+ *        LDS-windowed row kernel
+ *  12  1: DCN_FWD_AUTO picks the bf16 fused forward (measured slower at config 4)
+ * Slots 0, 1, 3, 11 and 13-15 are unused. */
 
 /* ---- testing ------------------------------------------------------------------ */
 /* One fp32 GEMM through the handle's engine under its current math mode, BLAS

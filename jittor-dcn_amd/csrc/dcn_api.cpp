@@ -531,8 +531,7 @@ int forward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x,
     // (and still stored for the ∂W GEMM of the backward), bias + rounding in the epilogue
     ProfScope ps(h, DCN_K_GEMM_FWD);
     HIP_TRY(dcn::launch_fused_fwd_bf16(g, xT, off32, w, has_bias ? F32(L.b32) : nullptr, out,
-                                       dcn::exp_flag(13) == 2 ? nullptr : BF(L.col), BF(L.wf16), st));
-    if (dcn::exp_flag(13) >= 2) HIP_TRY(dcn::launch_im2col_bf16(g, xT, off32, BF(L.col), 0, g.B, st));
+                                       BF(L.col), BF(L.wf16), st));
     return DCN_OK;
   }
   {
