@@ -281,11 +281,10 @@ int dcn_get_math(dcn_handle* h, int* math);
 
 /* ---- forward schedule ----------------------------------------------------------- */
 /* How the fp32 forward (deform_conv.py:41-80) runs after the offset conv.
- * DCN_FWD_FUSED: the fused kernel (bilinear im2col gathered straight into the MFMA
+ * DCN_FWD_FUSED: the fused kernel (bilinear im2col gathered straight into the f32 MFMA
  * GEMM's LDS tiles, bias in the epilogue; the columns are still written for the backward)
- * wherever it applies: DCN_F32 (f32 MFMA) with deform_groups 1, kh*kw <= 9, C % 32 == 0,
- * O % 128 == 0, native math; DCN_BF16 (bf16 MFMA) with deform_groups 1, kh*kw <= 9,
- * C % 32 == 0, O % 256 == 0; otherwise the unfused schedule. DCN_FWD_UNFUSED: K1 im2col, then the
+ * wherever it applies: DCN_F32, deform_groups 1, kh*kw <= 9, C % 32 == 0, O % 128 == 0,
+ * native math; otherwise (and for DCN_BF16) the unfused schedule. DCN_FWD_UNFUSED: K1 im2col, then the
  * vendor GEMM, then the bias. DCN_FWD_AUTO (default): the schedule measured faster for the
  * geometry. Same results to fp32 rounding (the columns bit for bit). */
 typedef enum { DCN_FWD_AUTO = 0, DCN_FWD_UNFUSED = 1, DCN_FWD_FUSED = 2 } dcn_fwd_path;
@@ -305,8 +304,8 @@ int dcn_set_fwd_path(dcn_handle* h, int path);
  *   9  n > 0: bf16/fp32 ∂W as n grouped GEMMs; n < 0: one GEMM per image
  *  10  1: bf16 offset conv forward on the register-direct MFMA kernel instead of the
  *        LDS-windowed row kernel
- *  12  1: DCN_FWD_AUTO picks the bf16 fused forward (measured slower at config 4)
- * Slots 0, 1, 3, 11 and 13-15 are unused. */
+ *  11  n > 0: bf16 ∂W_off kernel sums n row chunks per workgroup (default 2)
+ * Slots 0, 1, 3 and 12-15 are unused. */
 
 /* ---- testing ------------------------------------------------------------------ */
 /* One fp32 GEMM through the handle's engine under its current math mode, BLAS

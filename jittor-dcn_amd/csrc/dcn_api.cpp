@@ -116,7 +116,6 @@ struct WsLayout {
   // (DCN_BF16 keeps its channels-last x in `xT` as bf16; xT32 is the fp32 one that only the
   // VALU offset-conv fallbacks read, wb16 the bf16 weights of the MFMA offset conv)
   size_t x32 = 0, xT32 = 0, wb16 = 0, woff32 = 0, boff32 = 0, b32 = 0, off32 = 0, out32 = 0;
-  size_t wf16 = 0;  // the flat weight in MFMA fragment order (bf16 fused forward)
   size_t gx32 = 0, gw32 = 0, gb32 = 0, gwo32 = 0, gbo32 = 0, goff32 = 0;
   size_t total = 0;
 };
@@ -147,7 +146,6 @@ WsLayout ws_layout(const Geo& g, bool bwd) {
     L.b32 = take((size_t)g.O * f);
     L.off32 = take((size_t)g.B * g.J * g.HW * f);
     L.out32 = take((size_t)g.B * g.O * g.HW * f);
-    L.wf16 = take(dcn::fused_bf16_wf_elems(g) * sizeof(dcn::bf16_t));
   }
   if (bwd) {
     // ∂W partials; first also the ∂b tile sums of the fused ∂out transpose
@@ -523,16 +521,6 @@ int forward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x,
                                           F32(L.part), st));
       HIP_TRY(dcn::launch_round_to_bf16(off32, off, (size_t)g.B * g.J * g.HW, st));
     }
-  }
-  const bool want_fused = h->fwd_path == DCN_FWD_FUSED ||
-                          (h->fwd_path == DCN_FWD_AUTO && dcn::fused_bf16_pays(g));
-  if (want_fused && dcn::fused_bf16_ok(g) && !dcn::get_force_generic()) {
-    // f2 on the bf16 matrix cores: the bilinear columns gathered into the GEMM's LDS tiles
-    // (and still stored for the ∂W GEMM of the backward), bias + rounding in the epilogue
-    ProfScope ps(h, DCN_K_GEMM_FWD);
-    HIP_TRY(dcn::launch_fused_fwd_bf16(g, xT, off32, w, has_bias ? F32(L.b32) : nullptr, out,
-                                       BF(L.col), BF(L.wf16), st));
-    return DCN_OK;
   }
   {
     ProfScope ps(h, DCN_K_IM2COL);

@@ -275,246 +275,6 @@ fwd_fused(Geo g, const float* __restrict__ xT, const float* __restrict__ off,
   }
 }
 
-// ---------------------------------------------------------------------------
-// DCN_BF16 fused forward on v_mfma_f32_32x32x16_bf16. The bf16 vendor GEMM is not
-// MFMA-bound here but bound by re-reading the 2·B·HW·K-byte column matrix K1 just wrote
-// (config 4: 231 MB), so the fusion pays at bf16 where at fp32 it did not.
-//   * workgroup = 64 consecutive pixels of the flattened B·Ho·Wo axis x 256 output
-//     channels; wave w owns output rows 64w..64w+63 (2 M-blocks) x the 64 pixels
-//     (2 N-blocks): 4 fp32 accumulators;
-//   * k step = 32 channels of one tap (channel slice outer, taps inner: the 9 taps of a
-//     slice re-read the same corner rows from L1); a thread gathers 8 channels of one
-//     pixel's four corners (16-B bf16 reads), forms the canonical fp32 bilerp, rounds to
-//     bf16 (the very bits K1 writes) into a double-buffered LDS slice [px][32 k] — the B
-//     operand — and, when colT is given, stores the same 16 B to the columns the ∂W GEMM
-//     of the backward reads;
-//   * A = the flat weight in MFMA fragment order (wf_to_frag_bf16), one contiguous 1 KiB
-//     per wave load from L2, a step ahead in registers;
-//   * epilogue: + bias, bf16 rounding (the unfused path's launch_bias_to_bf16 arithmetic).
-// ---------------------------------------------------------------------------
-constexpr int kBNB = 2;         // 32-px MFMA blocks per tile (4: 128-px tiles, 389 VGPRs, 282 us at config 4)
-constexpr int kBP = 32 * kBNB;  // pixels per tile
-constexpr int kBS = 40;         // LDS pitch (bf16) of a pixel's 32-k slice (80 B: b128 reads conflict-free)
-constexpr int kGD = 2;          // gather ring depth (steps of corner loads in flight); even
-
-typedef __bf16 bf16x8f_t __attribute__((ext_vector_type(8)));
-
-__device__ __forceinline__ bf16x8f_t ld_frag(const bf16_t* p) {
-  return __builtin_bit_cast(bf16x8f_t, *reinterpret_cast<const uint4*>(p));
-}
-
-// wf[((ob·NKS + ks)·64 + l)·8 + e] = Wf[32ob + (l&31)][16ks + 8(l>>5) + e], NKS = K/16
-__global__ __launch_bounds__(256) void wf_to_frag_bf16(const bf16_t* __restrict__ w,
-                                                      bf16_t* __restrict__ wf, int O, int K) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long)O * K) return;
-  const int e = (int)(i & 7), l = (int)((i >> 3) & 63);
-  const long obks = i >> 9;
-  const int NKS = K / 16, ob = (int)(obks / NKS), ks = (int)(obks - (long)ob * NKS);
-  wf[i] = w[(size_t)(32 * ob + (l & 31)) * K + 16 * ks + 8 * (l >> 5) + e];
-}
-
-__device__ __forceinline__ float bfl(unsigned u) { return __uint_as_float(u << 16); }
-__device__ __forceinline__ float bfh(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
-
-__global__ __launch_bounds__(256) void fwd_fused_bf16(Geo g, const bf16_t* __restrict__ xT,
-                                                     const float* __restrict__ off,
-                                                     const bf16_t* __restrict__ wf,
-                                                     const float* __restrict__ bias,
-                                                     bf16_t* __restrict__ out,
-                                                     bf16_t* __restrict__ colT) {
-  __shared__ __attribute__((aligned(16))) bf16_t Bs[2][kBP * kBS];
-  __shared__ int4 rec[kBP * kFTaps];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const Block3 blk = xcd_block();
-  const long P = (long)g.B * g.HW;
-  const long p0 = (long)blk.x * kBP;
-  const int ob0 = blk.y * 8 + wave * 2;  // this wave's first 32-row output block
-  const int nsteps = g.N * (g.C / 32), NKS = g.K / 16;
-  for (int s = tid; s < kBP * g.N; s += 256) {
-    const int tp = s / g.N, n = s - tp * g.N;
-    const long p = p0 + tp;
-    int4 r = make_int4(INT_MIN, 0, 0, 0);
-    if (p < P) {
-      const int b = (int)(p / g.HW), m = (int)(p - (long)b * g.HW);
-      const Tap t = sample_tap(g, off, b, 0, n, m);
-      if (t.ok) r = make_int4(t.r0, t.c0, __float_as_int(t.fr), __float_as_int(t.fc));
-    }
-    rec[tp * kFTaps + n] = r;
-  }
-  // staging roles: pixels sp + 64u of the tile, channels 8sq..8sq+7 of the step's slice
-  constexpr int kU = kBP / 64;
-  const int sp = tid >> 2, sq = tid & 3;
-  const char* xc[kU];
-  unsigned colrow[kU];
-#pragma unroll
-  for (int u = 0; u < kU; ++u) {
-    const long ps = p0 + sp + 64 * u;
-    const bool pv = ps < P;
-    const int bs = pv ? (int)(ps / g.HW) : 0;
-    xc[u] = reinterpret_cast<const char*>(xT) + (size_t)bs * g.HWi * g.C * 2 + sq * 16;
-    colrow[u] = pv ? (unsigned)(((size_t)ps * g.K + sq * 8) * 2) : ~0u;
-  }
-  const unsigned rowb = (unsigned)g.W * g.C * 2u, pixb = (unsigned)g.C * 2u;
-  const __amdgpu_buffer_rsrc_t col_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      colT, 0, colT ? (int)((size_t)P * g.K * 2) : 0, 0x00020000);
-
-  f32x16 acc[2][kBNB];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int q = 0; q < kBNB; ++q)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[j][q][r] = 0.f;
-  // gathered corners of a step, two steps in flight (register sets G[0], G[1])
-  struct Gath {
-    uint4 a, b, c, d;
-    float fr, fc;
-    int okm;
-  };
-  Gath G[kGD][kU];
-  bf16x8f_t a[2][2][2];  // [register set][output block][16-k half]
-
-  auto kbase = [&](int s) {
-    const int cs = s / g.N, n = s - cs * g.N;
-    return n * g.C + 32 * cs;
-  };
-  auto load_a = [&](int s, int d) {
-    const int ks = kbase(min(s, nsteps - 1)) / 16;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        a[d][j][h] = ld_frag(wf + ((size_t)((ob0 + j) * NKS + ks + h) * 64 + lane) * 8);
-  };
-  auto gather1 = [&](int s0, int u, Gath& q) {
-    const int s = min(s0, nsteps - 1);  // past the last step: a harmless re-gather
-    const int cs = s / g.N, n = s - cs * g.N;
-    const int4 r = rec[(sp + 64 * u) * kFTaps + n];
-    const bool lv = r.x != INT_MIN;
-    const int r0 = lv ? r.x : 0, q0 = r.y;
-    q.fr = __int_as_float(r.z);
-    q.fc = __int_as_float(r.w);
-    // corner validity bits; the loads read clamped in-image addresses unconditionally
-    const bool r0ok = lv && r0 >= 0, r1ok = lv && r0 + 1 < g.H;
-    const bool c0ok = q0 >= 0, c1ok = q0 + 1 < g.W;
-    q.okm = (lv ? 16 : 0) | ((r0ok && c0ok) ? 1 : 0) | ((r0ok && c1ok) ? 2 : 0) |
-            ((r1ok && c0ok) ? 4 : 0) | ((r1ok && c1ok) ? 8 : 0);
-    const int ra = min(max(r0, 0), g.H - 1), rb = min(r0 + 1, g.H - 1);
-    const int qa = min(max(q0, 0), g.W - 1), qb = min(max(q0 + 1, 0), g.W - 1);
-    const char* base = xc[u] + cs * 64;
-    q.a = *reinterpret_cast<const uint4*>(base + ((unsigned)ra * rowb + (unsigned)qa * pixb));
-    q.b = *reinterpret_cast<const uint4*>(base + ((unsigned)ra * rowb + (unsigned)qb * pixb));
-    q.c = *reinterpret_cast<const uint4*>(base + ((unsigned)rb * rowb + (unsigned)qa * pixb));
-    q.d = *reinterpret_cast<const uint4*>(base + ((unsigned)rb * rowb + (unsigned)qb * pixb));
-  };
-  auto store1 = [&](int s, int buf, int u, const Gath& q) {
-    const int m = q.okm;
-    const unsigned za = (m & 1) ? ~0u : 0u, zb = (m & 2) ? ~0u : 0u;
-    const unsigned zc = (m & 4) ? ~0u : 0u, zd = (m & 8) ? ~0u : 0u;
-    const unsigned A4[4] = {q.a.x & za, q.a.y & za, q.a.z & za, q.a.w & za};
-    const unsigned B4[4] = {q.b.x & zb, q.b.y & zb, q.b.z & zb, q.b.w & zb};
-    const unsigned C4[4] = {q.c.x & zc, q.c.y & zc, q.c.z & zc, q.c.w & zc};
-    const unsigned D4[4] = {q.d.x & zd, q.d.y & zd, q.d.z & zd, q.d.w & zd};
-    unsigned o[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float lo = bilerp(q.fr, q.fc, bfl(A4[e]), bfl(B4[e]), bfl(C4[e]), bfl(D4[e]));
-      const float hi = bilerp(q.fr, q.fc, bfh(A4[e]), bfh(B4[e]), bfh(C4[e]), bfh(D4[e]));
-      o[e] = (m & 16) ? ((unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16)) : 0u;
-    }
-    const uint4 v = make_uint4(o[0], o[1], o[2], o[3]);
-    *reinterpret_cast<uint4*>(&Bs[buf][(sp + 64 * u) * kBS + 8 * sq]) = v;
-    if (colT)
-      __builtin_amdgcn_raw_buffer_store_b128(
-          __builtin_bit_cast(u32x4, v), col_rsrc,
-          (int)(colrow[u] == ~0u ? ~0u : colrow[u] + (unsigned)kbase(s) * 2u), 0, kAuxNT);
-  };
-  auto gather = [&](int s, Gath(&q)[kU]) {
-#pragma unroll
-    for (int u = 0; u < kU; ++u) gather1(s, u, q[u]);
-  };
-  auto store = [&](int s, int buf, const Gath(&q)[kU]) {
-#pragma unroll
-    for (int u = 0; u < kU; ++u) store1(s, buf, u, q[u]);
-  };
-  auto mfma = [&](int buf, int d) {
-    // every B fragment of the step is read before the first MFMA (no LDS load may land in a
-    // register an issued MFMA still reads)
-    bf16x8f_t bv[2][kBNB];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int q = 0; q < kBNB; ++q)
-        bv[h][q] = ld_frag(&Bs[buf][(32 * q + (lane & 31)) * kBS + 16 * h + 8 * (lane >> 5)]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int q = 0; q < kBNB; ++q)
-          acc[j][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[d][j][h], bv[h][q], acc[j][q], 0, 0, 0);
-  };
-  // sched_barriers: the next steps' gathers and A loads are issued above a step's MFMA block
-  // and the LDS staging below it
-  auto mm = [&](int buf, int d) {
-    __builtin_amdgcn_sched_barrier(0);
-    mfma(buf, d);
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  // A step ends with a full __syncthreads(), i.e. with every wave's loads and stores drained
-  // (vmcnt(0)), not an LDS-only barrier. Measured at config 4 (tools/fused_det.py): with
-  // lds_barrier() (gathers, A loads and column stores left in flight across the barrier)
-  // 0.01-3 % of the outputs differed from run to run in several schedules (ring depth 2 and
-  // 4, with or without s_nop padding after the MFMAs), though no LDS hazard is visible in the
-  // source; with the drain every run is bitwise identical to the unfused path.
-  auto step_barrier = [&]() { __syncthreads(); };
-  __syncthreads();  // records
-#pragma unroll
-  for (int d = 0; d < kGD; ++d) gather(d, G[d]);
-  load_a(0, 0);
-  store(0, 0, G[0]);
-  step_barrier();
-  // step s multiplies LDS buffer / A set s&1 after issuing the gather of step s+kGD into the
-  // ring slot step s's corners left free (kGD steps of memory latency in flight); then step
-  // s+1's corners (gathered kGD-1 steps earlier) are interpolated into the other LDS buffer.
-  // Unrolled by kGD (even): ring slots, buffers and A sets are compile-time indices.
-  for (int s0 = 0; s0 < nsteps; s0 += kGD) {
-    bool done = false;
-#pragma unroll
-    for (int d = 0; d < kGD; ++d) {
-      if (!done) {
-        const int s = s0 + d;
-        gather(s + kGD, G[d]);
-        load_a(s + 1, (d + 1) & 1);
-        mm(d & 1, d & 1);
-        if (s + 1 >= nsteps) {
-          done = true;  // workgroup-uniform
-        } else {
-          store(s + 1, (d + 1) & 1, G[(d + 1) % kGD]);
-          step_barrier();
-        }
-      }
-    }
-    if (done) break;
-  }
-  // D[row o][col px]: register r of lane (c = lane&31, hh) = row (r&3) + 8(r>>2) + 4hh
-#pragma unroll
-  for (int q = 0; q < kBNB; ++q) {
-    const long pf = p0 + 32 * q + (lane & 31);
-    if (pf >= P) continue;
-    const int b = (int)(pf / g.HW), m = (int)(pf - (long)b * g.HW);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int o = 32 * (ob0 + j) + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        out[((size_t)b * g.O + o) * g.HW + m] = f2bf(acc[j][q][r] + (bias ? bias[o] : 0.f));
-      }
-  }
-}
-
 }  // namespace
 
 bool fused_fwd_ok(const Geo& g) {
@@ -569,24 +329,4 @@ hipError_t launch_fused_fwd(const Geo& g, const float* xT, const float* off, con
 }
 
 
-bool fused_bf16_ok(const Geo& g) {
-  return g.dt == DCN_BF16 && g.G == 1 && g.N <= kFTaps && g.C % 32 == 0 && g.O % 256 == 0 &&
-         (size_t)g.B * g.HWi * g.C * 2 < (1ull << 31) && (size_t)g.B * g.HW * g.K * 2 < (1ull << 31);
-}
-size_t fused_bf16_wf_elems(const Geo& g) { return (size_t)g.O * g.K; }
-// DCN_EXP slot 12 = 1 lets AUTO pick the bf16 fused forward (A/B until measured)
-bool fused_bf16_pays(const Geo& g) { return fused_bf16_ok(g) && exp_flag(12) == 1; }
-
-hipError_t launch_fused_fwd_bf16(const Geo& g, const bf16_t* xT, const float* off, const bf16_t* w,
-                                 const float* bias, bf16_t* out, bf16_t* colT, bf16_t* wf,
-                                 hipStream_t s) {
-  if (!fused_bf16_ok(g)) return hipErrorInvalidValue;
-  const long n = (long)g.O * g.K;
-  hipLaunchKernelGGL(wf_to_frag_bf16, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w, wf,
-                     g.O, g.K);
-  const long P = (long)g.B * g.HW;
-  hipLaunchKernelGGL(fwd_fused_bf16, dim3((unsigned)((P + kBP - 1) / kBP), g.O / 256), dim3(256),
-                     0, s, g, xT, off, wf, bias, out, colT);
-  return hipGetLastError();
-}
 }  // namespace dcn

@@ -64,14 +64,6 @@ bool col2im_chunkable(const Geo& g);
 // dcn_fused.hip (f2): im2col gathered into the forward GEMM's LDS tiles, bias in the
 // epilogue; still writes colT (for the ∂W GEMM) when colT != NULL.
 bool fused_fwd_ok(const Geo& g);
-// DCN_BF16 fused forward (bf16 MFMA; colT, when given, receives K1's columns bit for bit);
-// wf: scratch of fused_bf16_wf_elems(g) bf16 values
-bool fused_bf16_ok(const Geo& g);
-size_t fused_bf16_wf_elems(const Geo& g);
-bool fused_bf16_pays(const Geo& g);
-hipError_t launch_fused_fwd_bf16(const Geo& g, const bf16_t* xT, const float* off, const bf16_t* w,
-                                 const float* bias, bf16_t* out, bf16_t* colT, bf16_t* wf,
-                                 hipStream_t s);
 bool fused_fwd_pays(const Geo& g);  // DCN_FWD_AUTO picks the fused kernel
 void set_fused_workgroups(int n);    // test hook (dcn_debug_fused_workgroups)
 hipError_t launch_fused_fwd(const Geo& g, const float* xT, const float* off, const float* Wf,

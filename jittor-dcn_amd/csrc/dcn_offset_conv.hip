@@ -1262,17 +1262,42 @@ __global__ __launch_bounds__(256) void offset_dgrad_bf16(Geo g, const bf16_t* __
 __global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __restrict__ x,
                                                         const float* __restrict__ goff,
                                                         float* __restrict__ part, int rowsB,
-                                                        int cpi) {
+                                                        int cpi, int cpb) {
   extern __shared__ float S[];
   const int J8 = j8(g.J), KK = g.kh * g.kw, KT = KK * J8;
-  const int chunk = blockIdx.x;
-  const int b = chunk / cpi, y0 = (chunk - b * cpi) * rowsB;
-  const int nrows = min(rowsB, g.H - y0);
   const int SW = g.W + (g.kw - 1) * g.dw;
   const int PJ = pj8(g.J);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 31, hh = lane >> 5;
   const int cb = blockIdx.y * 64;
+  const int nchunk = g.B * cpi;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[m][u][i] = 0.f;
+  // this lane's N column in each owned tile: k = 32·tile + r = t·J8 + j. A wave's second
+  // tile may not exist (w + 4 >= NTt): its MFMAs then multiply zeros, which costs that wave
+  // nothing the other waves do not spend anyway and keeps the loop free of branches.
+  int kofs[2];
+  unsigned kmask[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int kk = 32 * (w + 4 * u) + r;
+    const bool kok = kk < KT;
+    const int t = kk / J8, j = kk - t * J8;
+    kofs[u] = kok ? toff8(g, t, SW, PJ) + j : 0;
+    kmask[u] = kok ? 0xffffffffu : 0u;
+  }
+  // the block sums cpb consecutive chunks (of any images) into one partial: fewer partial
+  // bytes to write and fold
+  for (int ci = 0; ci < cpb; ++ci) {
+  const int chunk = blockIdx.x * cpb + ci;
+  if (chunk >= nchunk) break;  // workgroup-uniform
+  const int b = chunk / cpi, y0 = (chunk - b * cpi) * rowsB;
+  const int nrows = min(rowsB, g.H - y0);
   const int npx = nrows * g.W;  // a multiple of 4 (W % 4 == 0)
   // A = this block's 64 channel planes of x through a buffer resource, kPf steps ahead in a
   // register ring. A step past the chunk loads nothing (offset out of range: zeros); the
@@ -1296,28 +1321,9 @@ __global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __
   };
 #pragma unroll
   for (int d = 0; d < kPf - 1; ++d) lda(d, d);
+  if (ci > 0) __syncthreads();  // the previous chunk's staged rows are no longer read
   stage_goff8(g, goff, b, y0, nrows + (g.kh - 1) * g.dh, SW, J8, PJ, S);
   __syncthreads();
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[m][u][i] = 0.f;
-  // this lane's N column in each owned tile: k = 32·tile + r = t·J8 + j. A wave's second
-  // tile may not exist (w + 4 >= NTt): its MFMAs then multiply zeros, which costs that wave
-  // nothing the other waves do not spend anyway and keeps the loop free of branches.
-  int kofs[2];
-  unsigned kmask[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int kk = 32 * (w + 4 * u) + r;
-    const bool kok = kk < KT;
-    const int t = kk / J8, j = kk - t * J8;
-    kofs[u] = kok ? toff8(g, t, SW, PJ) + j : 0;
-    kmask[u] = kok ? 0xffffffffu : 0u;
-  }
   // (row, column) in the chunk of this lane's first pixel q = 16i + 8hh: q and W are
   // multiples of 4, so pixels q..q+3 share a row, as do q+4..q+7
   int yq = (8 * hh) / g.W, xq = 8 * hh - yq * g.W;
@@ -1358,17 +1364,20 @@ __global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __
       }
     }
   }
+  }  // chunks
   // partials in MFMA fragment order (each lane's 16 accumulators are 64 contiguous bytes,
   // a wave's tile one 4 KiB run): part[(((chunk·CG + cg)·NT + tile)·2 + m)·64 + lane][16]
   // with NT = ceil(KT/32) tiles; wgrad_frag_reduce folds the chunks and scatters to ∂w_off
   const int NT = (KT + 31) / 32, CG = g.C / 64;
+  // (columns j >= J inside a tap are written as zeros; only k >= KT is skipped)
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int tile = w + 4 * u;
     if (tile >= NT) continue;  // wave-uniform
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
-      float* pp = part + (((((size_t)chunk * CG + blockIdx.y) * NT + tile) * 2 + m) * 64 + lane) * 16;
+      float* pp = part + (((((size_t)blockIdx.x * CG + blockIdx.y) * NT + tile) * 2 + m) * 64 + lane) * 16;
+      if (!kmask[u]) continue;  // a padding K column: the fold never reads it
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         *reinterpret_cast<float4*>(pp + 4 * q) =
@@ -1388,9 +1397,13 @@ __global__ __launch_bounds__(1024) void wgrad_frag_reduce(Geo g, const float* __
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const long i = (long)blockIdx.x * 64 + lane;
   const long ic = i < E ? i : 0;
+  // padding K columns (k >= KK·J8) were never written: not read either
+  const int kcol = 32 * (int)(((ic >> 10) >> 1) % NT) + (int)((ic >> 4) & 31);
   float s = 0.f;
+  if (kcol < KK * J8) {
 #pragma unroll 4
-  for (int ch = w; ch < nchunk; ch += 16) s += part[(size_t)ch * E + ic];
+    for (int ch = w; ch < nchunk; ch += 16) s += part[(size_t)ch * E + ic];
+  }
   __shared__ float red[16][64];
   red[w][lane] = s;
   __syncthreads();
@@ -1444,11 +1457,14 @@ hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16
                      g.C, KK, KT16);
   size_t lds_w, lds_x;
   bwd_bf16_lds(g, ms, &lds_w, &lds_x);
-  hipLaunchKernelGGL(offset_wgrad_bf16, dim3(g.B * ms.cpi, g.C / 64), dim3(256), lds_w, s, g, x,
-                     goff, part, ms.rowsB, ms.cpi);
+  // chunks per workgroup (config 4: 1 -> 48 + 11 us, 2 -> 42 + 7, 4 -> 53 + 6 for ∂W_off + fold)
+  const int cpb = exp_flag(11) > 0 ? exp_flag(11) : 2;
+  const int nblk = (g.B * ms.cpi + cpb - 1) / cpb;
+  hipLaunchKernelGGL(offset_wgrad_bf16, dim3(nblk, g.C / 64), dim3(256), lds_w, s, g, x, goff,
+                     part, ms.rowsB, ms.cpi, cpb);
   const long E = (long)(g.C / 64) * ((KK * J8 + 31) / 32) * 2 * 1024;
   hipLaunchKernelGGL(wgrad_frag_reduce, dim3((unsigned)((E + 63) / 64)), dim3(1024), 0, s, g,
-                     part, g.B * ms.cpi, gw_off);
+                     part, nblk, gw_off);
   if (gb_off) launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
   hipLaunchKernelGGL(offset_dgrad_bf16, dim3(g.B * ms.spi), dim3(256), lds_x, s, g, wc, KT16, goff,
                      gxT_in, gx, ms.spi);

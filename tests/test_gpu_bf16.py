@@ -213,57 +213,3 @@ def test_bf16_backward_with_attached_comm_single_rank(gpu_handle):
     for name in ref[2]:
         np.testing.assert_array_equal(got[2][name], ref[2][name], err_msg=name)
 
-
-FUSED_CASES = [
-    dict(seed=71, B=2, C=64, O_=256, H=20, W=20),                  # 800 px: ragged last tile
-    dict(seed=72, B=3, C=32, O_=256, H=17, W=15, s=(2, 2)),        # stride 2, tiles straddle images
-    dict(seed=73, B=1, C=256, O_=512, H=14, W=14, off_scale=2.5),  # two O tiles, many off-image
-    dict(seed=74, B=2, C=96, O_=256, H=9, W=12, k=(2, 2), p=(1, 1)),  # 4 taps
-]
-
-
-def _fused_vs_unfused(h, case):
-    bits, v, s = _case(**case)
-    pad = case.get("p", (1, 1))
-    h.set_fwd_path(rt.DCN_FWD_FUSED)
-    try:
-        fused = _device(h, bits, s, pad=pad)
-    finally:
-        h.set_fwd_path(rt.DCN_FWD_UNFUSED)
-    try:
-        unfused = _device(h, bits, s, pad=pad)
-        again = _device(h, bits, s, pad=pad)
-    finally:
-        h.set_fwd_path(rt.DCN_FWD_AUTO)
-    for k in unfused[2]:  # the unfused schedule itself is bitwise reproducible
-        np.testing.assert_array_equal(again[2][k], unfused[2][k], err_msg=f"unfused ∂{k} run to run")
-    return bits, v, s, pad, fused, unfused
-
-
-@pytest.mark.parametrize("case", FUSED_CASES)
-def test_bf16_fused_forward(gpu_handle, case):
-    """The bf16 fused forward (dcn_fused.hip fwd_fused_bf16): the same bf16 columns as K1 (so
-    the backward, whose ∂W GEMM reads the columns the forward left, is bitwise that of the
-    unfused schedule), the output equal to the unfused one up to the fp32 summation order
-    before the bf16 rounding (at most one bf16 ulp), and within the bf16 tolerance of the
-    oracle."""
-    bits, v, s, pad, (out_f, off_f, g_f), (out_u, off_u, g_u) = _fused_vs_unfused(gpu_handle, case)
-    np.testing.assert_array_equal(off_f, off_u)
-    for k in g_u:
-        np.testing.assert_array_equal(g_f[k], g_u[k], err_msg=f"∂{k}: columns differ")
-    assert np.all(np.abs(out_f - out_u) <= 2.0 ** -7 * np.abs(out_u) + 1e-6), "fused vs unfused"
-    ro, _, _ = O.forward(v["x"], v["w_off"], v["b_off"], v["w"], v["b"], s, pad, offsets=off_f)
-    assert rel_err(out_f, ro) <= BF16_TOL
-
-
-def test_bf16_fused_forward_config4_full_size(gpu_handle):
-    """BASELINE config 4 per GPU (B=64, 256->256, 28x28): fused against unfused over the
-    whole batch, every gradient bitwise (the columns are K1's bits)."""
-    bits, v, s, pad, (out_f, off_f, g_f), (out_u, off_u, g_u) = _fused_vs_unfused(
-        gpu_handle, dict(seed=75, B=64, C=256, O_=256, H=28, W=28))
-    np.testing.assert_array_equal(off_f, off_u)
-    for k in g_u:
-        np.testing.assert_array_equal(g_f[k], g_u[k], err_msg=f"∂{k}: columns differ")
-    d = np.abs(out_f - out_u)
-    assert np.all(d <= 2.0 ** -7 * np.abs(out_u) + 1e-6), "fused vs unfused"
-    assert (d > 0).mean() < 0.01  # rounding flips only where the fp32 sums straddle a bf16 tie
