@@ -625,6 +625,8 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
     // bf16 grad_x directly (transpose of the sampling route + the offset-conv route)
     HIP_TRY(dcn::launch_offset_conv_bwd_bf16(g, x, w_off, goff32, F32(L.gxT), BF(L.wb16),
                                              F32(L.goffT), gx, F32(L.gwo32), F32(L.gbo32), st));
+    // (r02: the Wc swizzle and ∂b_off sums on the side stream beside ∂W_off measured slower,
+    // offset bwd 0.115 -> 0.121 ms at config 4: concurrent kernels slow each other)
   } else if (dcn::offset_bwd_chunkable(g)) {
     // f32 MFMA on the bf16 xT (exact products of the bf16 values) and the fp32 ∂offset
     HIP_TRY(dcn::launch_offset_bwd_prep(g, F32(L.woff32), F32(L.wt), st));

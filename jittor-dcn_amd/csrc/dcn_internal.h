@@ -89,10 +89,13 @@ hipError_t launch_offset_conv_fwd_bf16(const Geo& g, const bf16_t* xT, const bf1
 // wc: offset_bwd_bf16_wc_elems(g) bf16 values.
 bool offset_bwd_bf16_ok(const Geo& g);
 size_t offset_bwd_bf16_wc_elems(const Geo& g);
+// aux / fork / join (optional, aux = nullptr: all on s): the Wc swizzle and the ∂b_off sums
+// run on aux beside ∂W_off, joined before ∂x
 hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16_t* w_off,
                                        const float* goff, const float* gxT_in, bf16_t* wc,
                                        float* part, bf16_t* gx, float* gw_off, float* gb_off,
-                                       hipStream_t s);
+                                       hipStream_t s, hipStream_t aux = nullptr,
+                                       hipEvent_t fork = nullptr, hipEvent_t join = nullptr);
 // xT: channels-last x; goffT: scratch of offset_conv_goffT_floats(g). gxT_in == NULL:
 // grad_x is accumulated; else grad_x = transpose(gxT_in) + the offset-conv route, written
 // once (gxT_in: the sampling-route ∂x left channels-last by launch_col2im_*).

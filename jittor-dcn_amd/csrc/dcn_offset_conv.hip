@@ -1448,13 +1448,23 @@ size_t offset_bwd_bf16_wc_elems(const Geo& g) { return (size_t)g.C * kt16(g); }
 hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16_t* w_off,
                                        const float* goff, const float* gxT_in, bf16_t* wc,
                                        float* part, bf16_t* gx, float* gw_off, float* gb_off,
-                                       hipStream_t s) {
+                                       hipStream_t s, hipStream_t aux, hipEvent_t fork,
+                                       hipEvent_t join) {
   MfmaStage ms;
   if (!offset_bwd_bf16_ok(g) || !mfma_stage(g, &ms)) return hipErrorInvalidValue;
   const int KK = g.kh * g.kw, J8 = j8(g.J), KT16 = kt16(g);
+  // side stream (when given): the Wc swizzle for ∂x and the ∂b_off channel sums, beside ∂W_off
+  hipStream_t s2 = aux ? aux : s;
+  hipError_t e = hipSuccess;
+  if (aux) {
+    e = hipEventRecord(fork, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(aux, fork, 0);
+    if (e != hipSuccess) return e;
+  }
   const int n = g.C * KT16;
-  hipLaunchKernelGGL(woff_to_ck_bf16, dim3((n + 255) / 256), dim3(256), 0, s, w_off, wc, g.J, J8,
+  hipLaunchKernelGGL(woff_to_ck_bf16, dim3((n + 255) / 256), dim3(256), 0, s2, w_off, wc, g.J, J8,
                      g.C, KK, KT16);
+  if (gb_off) launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s2);
   size_t lds_w, lds_x;
   bwd_bf16_lds(g, ms, &lds_w, &lds_x);
   // chunks per workgroup (config 4: 1 -> 48 + 11 us, 2 -> 42 + 7, 4 -> 53 + 6 for ∂W_off + fold)
@@ -1465,7 +1475,11 @@ hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16
   const long E = (long)(g.C / 64) * ((KK * J8 + 31) / 32) * 2 * 1024;
   hipLaunchKernelGGL(wgrad_frag_reduce, dim3((unsigned)((E + 63) / 64)), dim3(1024), 0, s, g,
                      part, nblk, gw_off);
-  if (gb_off) launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
+  if (aux) {
+    e = hipEventRecord(join, aux);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(offset_dgrad_bf16, dim3(g.B * ms.spi), dim3(256), lds_x, s, g, wc, KT16, goff,
                      gxT_in, gx, ms.spi);
   return hipGetLastError();
