@@ -129,6 +129,7 @@ void launch_channel_sum_bf16(const bf16_t* in, int B, int Cn, int HW, float* out
 // in[b][c][p] -> out[b][p][c] and chsum[c] = Σ_{b,p} in[b][c][p] (deterministic); tsum is
 // scratch of xpose_chsum_floats(B, C, P) floats.
 size_t xpose_chsum_floats(int B, int C, int P);
+bool launch_xpose_f4(const float* in, float* out, int B, int C, int P, hipStream_t s);
 // ∂out -> ∂outT with ∂b; the per-channel fold of the tile sums runs on s_sum (after event ev)
 // when given, so tsum must then stay untouched until s_sum is joined.
 hipError_t launch_xpose_chsum(const float* in, float* out, float* tsum, float* chsum, int B,

@@ -216,6 +216,7 @@ hipError_t launch_bias_to_bf16(const Geo& g, const float* out32, const float* bi
 // B x ceil(HW/(64*kXpSub)) partials per channel in order (deterministic, no atomics).
 // ---------------------------------------------------------------------------
 constexpr int kXpSub = 8;
+static int xpose_blocks_x(int P) { return (P + 64 * kXpSub - 1) / (64 * kXpSub); }
 
 __global__ __launch_bounds__(256) void xpose_chsum(const float* __restrict__ in,
                                                    float* __restrict__ out,
@@ -261,6 +262,68 @@ __global__ __launch_bounds__(256) void xpose_chsum(const float* __restrict__ in,
         ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];  // [C][partials]
 }
 
+// 16-byte form (P % 4 == 0, C % 64 == 0, 16-B aligned): a thread loads 4 pixels of one
+// channel row (float4; a wave reads 4 rows x 256 B), the tile goes through LDS, and a thread
+// stores 4 channels of one pixel (float4; a wave writes 4 pixel rows x 256 B): 1 KiB per wave
+// instruction each way instead of 256 B. With SUMS, the channel sums ride along: a thread's
+// 4-pixel sums, then the 16 lanes of its channel row folded by DPP (fixed order).
+template <bool SUMS>
+__global__ __launch_bounds__(256) void xpose_f4(const float* __restrict__ in, float* __restrict__ out,
+                                                float* __restrict__ tsum, int C, int P) {
+  __shared__ float t[64][65];
+  const int c0 = blockIdx.y * 64, b = blockIdx.z;
+  const float* ib = in + (size_t)b * C * P;
+  float* ob = out + (size_t)b * C * P;
+  const int tid = threadIdx.x, lr = tid >> 4, lq = tid & 15;
+  const int pb = blockIdx.x * 64 * kXpSub;
+  const int nsub = min(kXpSub, (P - pb + 63) / 64);
+  float4 r[4];
+  auto load = [&](int p0) {
+    const int p = p0 + 4 * lq;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      r[k] = p < P ? *reinterpret_cast<const float4*>(ib + (size_t)(c0 + lr + 16 * k) * P + p)
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  load(pb);
+  for (int sub = 0; sub < nsub; ++sub) {
+    const int p0 = pb + 64 * sub;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float* row = &t[lr + 16 * k][4 * lq];
+      row[0] = r[k].x, row[1] = r[k].y, row[2] = r[k].z, row[3] = r[k].w;
+      if (SUMS) cs[k] += ((r[k].x + r[k].y) + r[k].z) + r[k].w;
+    }
+    __syncthreads();
+    if (sub + 1 < nsub) load(p0 + 64);  // in flight while this tile is written
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int pr = lr + 16 * k, p = p0 + pr;
+      const float4 v = make_float4(t[4 * lq][pr], t[4 * lq + 1][pr], t[4 * lq + 2][pr],
+                                   t[4 * lq + 3][pr]);
+      if (p < P) *reinterpret_cast<float4*>(ob + (size_t)p * C + c0 + 4 * lq) = v;
+    }
+    __syncthreads();
+  }
+  if (SUMS) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float v = cs[k];  // the 16 lanes of channel row lr + 16k form one DPP row
+      v += dpp_f<0xB1>(v);
+      v += dpp_f<0x4E>(v);
+      v += dpp_f<0x141>(v);
+      v += dpp_f<0x140>(v);
+      if (lq == 0)
+        tsum[(size_t)(c0 + lr + 16 * k) * gridDim.x * gridDim.z + (size_t)b * gridDim.x + blockIdx.x] = v;
+    }
+  }
+}
+
+static bool xpose_f4_ok(const float* in, const float* out, int C, int P) {
+  return P % 4 == 0 && C % 64 == 0 && ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0;
+}
+
 // One wave per channel: lane l sums partials i ≡ l (mod 64) (all loads in flight
 // together), then a fixed DPP tree (wave_sum) folds the 64 lane sums: deterministic.
 __global__ __launch_bounds__(64) void tile_sum_to_channels(const float* __restrict__ tsum,
@@ -274,7 +337,13 @@ __global__ __launch_bounds__(64) void tile_sum_to_channels(const float* __restri
   if (lane == 0) out[c] = s;
 }
 
-static int xpose_blocks_x(int P) { return (P + 64 * kXpSub - 1) / (64 * kXpSub); }
+// the plain fp32 NCHW -> NHWC transpose in the 16-byte form; false when it does not apply
+bool launch_xpose_f4(const float* in, float* out, int B, int C, int P, hipStream_t s) {
+  if (!xpose_f4_ok(in, out, C, P) || exp_flag(13)) return false;
+  dim3 grid(xpose_blocks_x(P), C / 64, B);
+  hipLaunchKernelGGL(xpose_f4<false>, grid, dim3(256), 0, s, in, out, nullptr, C, P);
+  return true;
+}
 
 size_t xpose_chsum_floats(int B, int C, int P) { return (size_t)B * xpose_blocks_x(P) * C; }
 
@@ -282,7 +351,10 @@ hipError_t launch_xpose_chsum(const float* in, float* out, float* tsum, float* c
                               int C, int P, hipStream_t s, hipStream_t s_sum,
                               hipEvent_t ev) {
   dim3 grid(xpose_blocks_x(P), (C + 63) / 64, B);
-  hipLaunchKernelGGL(xpose_chsum, grid, dim3(256), 0, s, in, out, tsum, C, P);
+  if (xpose_f4_ok(in, out, C, P) && !exp_flag(13))
+    hipLaunchKernelGGL(xpose_f4<true>, grid, dim3(256), 0, s, in, out, tsum, C, P);
+  else
+    hipLaunchKernelGGL(xpose_chsum, grid, dim3(256), 0, s, in, out, tsum, C, P);
   if (s_sum && s_sum != s) {  // the fold only feeds ∂b: off the main stream's critical path
     hipError_t e = hipEventRecord(ev, s);
     if (e == hipSuccess) e = hipStreamWaitEvent(s_sum, ev, 0);

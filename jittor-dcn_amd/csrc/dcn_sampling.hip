@@ -829,6 +829,7 @@ __global__ __launch_bounds__(256) void nhwc_to_nchw(const float* __restrict__ in
 }
 
 hipError_t launch_nchw_to_nhwc(const float* in, float* out, int B, int C, int P, hipStream_t s) {
+  if (launch_xpose_f4(in, out, B, C, P, s)) return hipGetLastError();
   dim3 grid((P + 63) / 64, (C + 63) / 64, B);
   hipLaunchKernelGGL(nchw_to_nhwc<float>, grid, dim3(256), 0, s, in, out, C, P);
   return hipGetLastError();
