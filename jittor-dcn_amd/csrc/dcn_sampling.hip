@@ -323,6 +323,126 @@ __global__ __launch_bounds__(256) void im2col_lds(Geo g, const XT* __restrict__ 
   }
 }
 
+// K1 for bf16 x and columns with 8 channels per lane: a sample's 512-B column row (C = 256)
+// is one half-wave's 16-B-per-lane store, so a wave instruction writes two samples (1 KiB)
+// and gathers its corners with 16-B LDS reads. The 4-channel form moved 8 B per lane and ran
+// at the fp32 kernel's samples/s (r02 config 4: 0.087 ms, 0.37 of HBM). Same window, records
+// and arithmetic (canonical bilerp per channel, one rounding to bf16): the same column bits.
+__device__ __forceinline__ void bf8_unpack(uint4 u, float4& lo, float4& hi) {
+  lo = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                   __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+  hi = make_float4(__uint_as_float(u.z << 16), __uint_as_float(u.z & 0xffff0000u),
+                   __uint_as_float(u.w << 16), __uint_as_float(u.w & 0xffff0000u));
+}
+__device__ __forceinline__ uint4 ld8_if(const bf16_t* p, bool ok) {
+  return ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0u, 0u, 0u, 0u);
+}
+
+template <int TH, int TW, int MAR, int CS, bool NT = true>
+__global__ __launch_bounds__(256) void im2col_lds_b8(Geo g, const bf16_t* __restrict__ xT,
+                                                     const float* __restrict__ off,
+                                                     bf16_t* __restrict__ colT, int b0, int tw_n) {
+  typedef Win<TH, TW, MAR> Wn;
+  constexpr int kTP = TH * TW;
+  constexpr int LPW = CS / 4;                // window slots (4 channels, 8 B) per pixel
+  constexpr int LPS = CS / 8, GS = 256 / LPS;  // lanes per sample, samples per block step
+  __shared__ uint2 win[Wn::PIX * LPW];
+  __shared__ int4 rec[kTP * kMaxTaps];
+  const int tid = threadIdx.x;
+  const Block3 blk = xcd_block();
+  const int bl = blk.z, b = b0 + bl;
+  const int th_i = blk.x / tw_n, tw_i = blk.x - th_i * tw_n;
+  const int h0 = th_i * TH, w0 = tw_i * TW;
+  const int rlo = (int)floorf((float)w0 * (float)(g.H - 1) / (float)(g.Wo - 1)) - MAR;
+  const int qlo = (int)floorf((float)h0 * (float)(g.W - 1) / (float)(g.Ho - 1)) - MAR;
+  const int NSB = kTP * g.N;
+  for (int sidx = tid; sidx < NSB; sidx += 256) {
+    const int p = sidx / g.N, n = sidx - p * g.N;
+    const int h = h0 + p / TW, w = w0 + p % TW;
+    int4 r = make_int4(kSkip, 0, 0, 0);
+    if (h < g.Ho && w < g.Wo) {
+      const Tap t = sample_tap(g, off, b, 0, n, h * g.Wo + w);
+      r = t.ok ? make_int4(t.r0, t.c0, __float_as_int(t.fr), __float_as_int(t.fc))
+               : make_int4(kZero, 0, 0, 0);
+    }
+    rec[sidx] = r;
+  }
+  const bf16_t* xb = xT + (size_t)b * g.HWi * g.C;
+  bf16_t* cb = colT + (size_t)bl * g.HW * g.K;
+  const int grp = tid / LPS, cl = tid % LPS;
+  for (int cs = 0; cs < g.C; cs += CS) {
+    const int c = cs + cl * 8;
+    const bool cok = c < g.C;  // C % 8 == 0: whole 8-channel runs
+    __syncthreads();  // records ready / previous slice consumed
+    {
+      constexpr int TOT = Wn::PIX * LPW, IT = (TOT + 255) / 256;
+      uint2 v[IT];
+#pragma unroll
+      for (int k = 0; k < IT; ++k) {
+        const int idx = tid + k * 256;
+        const int pix = idx / LPW, l = idx % LPW;
+        const int rr = pix / Wn::Q, qq = pix - rr * Wn::Q;
+        const int r = rlo + rr, q = qlo + qq, cc = cs + l * 4;
+        const bool ok = idx < TOT && r >= 0 && r < g.H && q >= 0 && q < g.W && cc < g.C;
+        v[k] = ok ? *reinterpret_cast<const uint2*>(xb + ((size_t)r * g.W + q) * g.C + cc)
+                  : make_uint2(0u, 0u);
+      }
+#pragma unroll
+      for (int k = 0; k < IT; ++k)
+        if (tid + k * 256 < TOT) win[tid + k * 256] = v[k];
+    }
+    __syncthreads();
+    for (int s = grp; s < NSB; s += GS) {
+      const int4 r = rec[s];
+      if (r.x == kSkip) continue;
+      const int p = s / g.N, n = s - p * g.N;
+      const int m = (h0 + p / TW) * g.Wo + w0 + p % TW;
+      uint4 o = make_uint4(0u, 0u, 0u, 0u);
+      if (r.x != kZero) {
+        const float fr = __int_as_float(r.z), fc = __int_as_float(r.w);
+        const int rr = r.x - rlo, qq = r.y - qlo;
+        uint4 ua, ub, uc, ud;
+        if (rr >= 0 && rr + 1 < Wn::R && qq >= 0 && qq + 1 < Wn::Q) {
+          const uint4* w8 = reinterpret_cast<const uint4*>(win + (rr * Wn::Q + qq) * LPW) + cl;
+          ua = w8[0];
+          ub = w8[LPW / 2];
+          uc = w8[Wn::Q * LPW / 2];
+          ud = w8[(Wn::Q + 1) * LPW / 2];
+        } else {  // outside the staged window: global corner reads
+          const bool r0ok = r.x >= 0, r1ok = r.x + 1 < g.H, c0ok = r.y >= 0, c1ok = r.y + 1 < g.W;
+          const bf16_t* p00 = xb + ((long)r.x * g.W + r.y) * (long)g.C + c;
+          const long rs = (long)g.W * g.C;
+          ua = ld8_if(p00, cok && r0ok && c0ok);
+          ub = ld8_if(p00 + g.C, cok && r0ok && c1ok);
+          uc = ld8_if(p00 + rs, cok && r1ok && c0ok);
+          ud = ld8_if(p00 + rs + g.C, cok && r1ok && c1ok);
+        }
+        float4 a0, a1, b0v, b1v, c0v, c1v, d0, d1;
+        bf8_unpack(ua, a0, a1);
+        bf8_unpack(ub, b0v, b1v);
+        bf8_unpack(uc, c0v, c1v);
+        bf8_unpack(ud, d0, d1);
+        const float4 lo = bilerp4(fr, fc, a0, b0v, c0v, d0), hi = bilerp4(fr, fc, a1, b1v, c1v, d1);
+        o = make_uint4((unsigned)f2bf(lo.x) | ((unsigned)f2bf(lo.y) << 16),
+                       (unsigned)f2bf(lo.z) | ((unsigned)f2bf(lo.w) << 16),
+                       (unsigned)f2bf(hi.x) | ((unsigned)f2bf(hi.y) << 16),
+                       (unsigned)f2bf(hi.z) | ((unsigned)f2bf(hi.w) << 16));
+      }
+      if (cok) {
+        unsigned* dst = reinterpret_cast<unsigned*>(cb + (size_t)m * g.K + (size_t)n * g.C + c);
+        if constexpr (NT) {
+          __builtin_nontemporal_store(o.x, dst);
+          __builtin_nontemporal_store(o.y, dst + 1);
+          __builtin_nontemporal_store(o.z, dst + 2);
+          __builtin_nontemporal_store(o.w, dst + 3);
+        } else {
+          *reinterpret_cast<uint4*>(dst) = o;
+        }
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // K5a: ∂off for every sample from its ∂colT row and the four xT corner rows.
 // ---------------------------------------------------------------------------
@@ -1170,7 +1290,15 @@ hipError_t launch_im2col_bf16(const Geo& g, const bf16_t* xT, const float* off, 
     hipLaunchKernelGGL(kern, dim3(th_n * tw_n, 1, nb), dim3(256), 0, s, g, xT, off, colT, b0,
                        tw_n);
   };
-  if (g.C <= 32)
+  const int v = exp_flag(14);
+  if (g.C % 8 == 0 && g.C > 128 && v != 1) {
+    if (v == 2) go(im2col_lds_b8<8, 4, 1, 256>, 8, 4);
+    else if (v == 3) go(im2col_lds_b8<4, 8, 1, 256>, 4, 8);
+    else if (v == 4) go(im2col_lds_b8<8, 8, 1, 256>, 8, 8);
+    else if (v == 5) go(im2col_lds_b8<4, 4, 2, 256>, 4, 4);
+    else if (v == 6) go(im2col_lds_b8<4, 4, 1, 256, false>, 4, 4);
+    else go(im2col_lds_b8<4, 4, 1, 256>, 4, 4);
+  } else if (g.C <= 32)
     go(im2col_lds<8, 8, 2, 32, true, bf16_t, bf16_t>, 8, 8);
   else if (g.C <= 64)
     go(im2col_lds<8, 8, 2, 64, true, bf16_t, bf16_t>, 8, 8);
