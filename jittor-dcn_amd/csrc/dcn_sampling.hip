@@ -355,26 +355,6 @@ __global__ __launch_bounds__(256) void im2col_lds_b8(Geo g, const bf16_t* __rest
   const int h0 = th_i * TH, w0 = tw_i * TW;
   const int rlo = (int)floorf((float)w0 * (float)(g.H - 1) / (float)(g.Wo - 1)) - MAR;
   const int qlo = (int)floorf((float)h0 * (float)(g.W - 1) / (float)(g.Ho - 1)) - MAR;
-  const bf16_t* xb = xT + (size_t)b * g.HWi * g.C;
-  bf16_t* cb = colT + (size_t)bl * g.HW * g.K;
-  const int grp = tid / LPS, cl = tid % LPS;
-  constexpr int TOT = Wn::PIX * LPW, IT = (TOT + 255) / 256;
-  uint2 v[IT];
-  // window loads of channel slice cs (issued before the sample records of the first slice,
-  // so the two global round trips overlap)
-  auto load_win = [&](int cs) {
-#pragma unroll
-    for (int k = 0; k < IT; ++k) {
-      const int idx = tid + k * 256;
-      const int pix = idx / LPW, l = idx % LPW;
-      const int rr = pix / Wn::Q, qq = pix - rr * Wn::Q;
-      const int r = rlo + rr, q = qlo + qq, cc = cs + l * 4;
-      const bool ok = idx < TOT && r >= 0 && r < g.H && q >= 0 && q < g.W && cc < g.C;
-      v[k] = ok ? *reinterpret_cast<const uint2*>(xb + ((size_t)r * g.W + q) * g.C + cc)
-                : make_uint2(0u, 0u);
-    }
-  };
-  load_win(0);
   const int NSB = kTP * g.N;
   for (int sidx = tid; sidx < NSB; sidx += 256) {
     const int p = sidx / g.N, n = sidx - p * g.N;
@@ -387,17 +367,31 @@ __global__ __launch_bounds__(256) void im2col_lds_b8(Geo g, const bf16_t* __rest
     }
     rec[sidx] = r;
   }
+  const bf16_t* xb = xT + (size_t)b * g.HWi * g.C;
+  bf16_t* cb = colT + (size_t)bl * g.HW * g.K;
+  const int grp = tid / LPS, cl = tid % LPS;
   for (int cs = 0; cs < g.C; cs += CS) {
     const int c = cs + cl * 8;
     const bool cok = c < g.C;  // C % 8 == 0: whole 8-channel runs
-    if (cs > 0) {
-      __syncthreads();  // previous slice consumed
-      load_win(cs);
-    }
+    __syncthreads();  // records ready / previous slice consumed
+    {
+      constexpr int TOT = Wn::PIX * LPW, IT = (TOT + 255) / 256;
+      uint2 v[IT];
 #pragma unroll
-    for (int k = 0; k < IT; ++k)
-      if (tid + k * 256 < TOT) win[tid + k * 256] = v[k];
-    __syncthreads();  // records and window ready
+      for (int k = 0; k < IT; ++k) {
+        const int idx = tid + k * 256;
+        const int pix = idx / LPW, l = idx % LPW;
+        const int rr = pix / Wn::Q, qq = pix - rr * Wn::Q;
+        const int r = rlo + rr, q = qlo + qq, cc = cs + l * 4;
+        const bool ok = idx < TOT && r >= 0 && r < g.H && q >= 0 && q < g.W && cc < g.C;
+        v[k] = ok ? *reinterpret_cast<const uint2*>(xb + ((size_t)r * g.W + q) * g.C + cc)
+                  : make_uint2(0u, 0u);
+      }
+#pragma unroll
+      for (int k = 0; k < IT; ++k)
+        if (tid + k * 256 < TOT) win[tid + k * 256] = v[k];
+    }
+    __syncthreads();
     for (int s = grp; s < NSB; s += GS) {
       const int4 r = rec[s];
       if (r.x == kSkip) continue;
