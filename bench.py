@@ -197,7 +197,9 @@ def load_traffic(path, bf16=False):
     except (OSError, ValueError):
         return None, None
     for name, v in doc.get("config4" if bf16 else "kernels", {}).items():
-        if name.startswith(K1_KERNEL) and (("unsigned short" in name) == bf16):
+        # bf16 K1: the 8-channel kernel (im2col_lds_b8) or the bf16 instantiation
+        is_bf16 = "unsigned short" in name or name.startswith(K1_KERNEL + "_b8")
+        if name.startswith(K1_KERNEL) and is_bf16 == bf16:
             return int(v["hbm_bytes"]), f"{os.path.relpath(paths[-1], ROOT)}:{name}"
     return None, None
 
