@@ -21,6 +21,7 @@
 // reproducible.
 #include <climits>
 #include <cstdlib>
+#include <type_traits>
 
 #include "dcn_device.h"
 
@@ -627,7 +628,7 @@ __device__ __forceinline__ float4 add4(float4 a, float4 b) {
 }
 
 template <int U, int kTQ, typename GT = float, typename XT = float>
-__global__ __launch_bounds__(kC2iThreads) void col2im_tile(Geo g, const XT* __restrict__ xT,
+__global__ __launch_bounds__(kC2iThreads) __attribute__((amdgpu_waves_per_eu(6))) void col2im_tile(Geo g, const XT* __restrict__ xT,
                                                            const int4* __restrict__ brec,
                                                            const int* __restrict__ start,
                                                            const GT* __restrict__ gcolT,
@@ -692,7 +693,9 @@ __global__ __launch_bounds__(kC2iThreads) void col2im_tile(Geo g, const XT* __re
   int p0 = rowlo;
   int4 pg = p0 + lane < rowhi ? rb[p0 + lane] : make_int4(0, 0, 0, 0);
   int4 nR[U];
-  float4 nx[U];
+  // rows in flight as loaded (bf16: 8 B per lane, converted when consumed)
+  typedef typename std::conditional<sizeof(GT) == 2, uint2, float4>::type RowT;
+  RowT nx[U];
   auto issue = [&](int ni) {
     if (ni >= rowhi) return;
     if (ni + U > p0 + 64) {  // next page (rows of more than 64 samples)
@@ -706,7 +709,7 @@ __global__ __launch_bounds__(kC2iThreads) void col2im_tile(Geo g, const XT* __re
                         __builtin_amdgcn_readlane(pg.z, l), __builtin_amdgcn_readlane(pg.w, l));
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) nx[u] = ld4(gb + nR[u].x + cc);
+    for (int u = 0; u < U; ++u) nx[u] = *reinterpret_cast<const RowT*>(gb + nR[u].x + cc);
   };
   issue(rowlo);  // (nothing for a wave past the last bin row: rowlo == rowhi == 0)
 #pragma unroll
@@ -726,7 +729,14 @@ __global__ __launch_bounds__(kC2iThreads) void col2im_tile(Geo g, const XT* __re
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           R[u] = nR[u];
-          gv[u] = cok ? nx[u] : z4;
+          if constexpr (sizeof(GT) == 2) {
+            const uint2 q = nx[u];
+            gv[u] = cok ? make_float4(__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
+                                      __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u))
+                        : z4;
+          } else {
+            gv[u] = cok ? nx[u] : z4;
+          }
         }
         issue(i + U < hi ? i + U : hi);  // next batch of this bin, else the next bin's first
 #pragma unroll
@@ -1225,6 +1235,15 @@ static void launch_k5_fused(const Geo& g, const XT* xT, const BinsWs& P, const G
   const int tr_n = (g.H + kTR - 1) / kTR, tq_n = (g.W + 4 - 1) / 4;
   // U = 2 rows in flight per wave for both element types: U = 4 for the half-length bf16
   // rows measured slower (r02, config 4: 0.192 against 0.187 ms; 95 VGPRs, 5 waves/SIMD)
+  // bf16 rows stay raw (8 B per lane) until consumed, so 3 rows in flight fit the 6-waves-per-
+  // SIMD budget (80 VGPRs): config 4 0.189 (U = 2, converted at load) -> 0.162 (U = 2 raw) ->
+  // 0.154 ms (U = 3 raw); U = 4 spills at 6 waves and runs 0.178 at 5. DCN_EXP slot 12 = 2
+  // keeps U = 2.
+  if (sizeof(GT) == 2 && exp_flag(12) != 2) {
+    hipLaunchKernelGGL((col2im_tile<3, 4, GT, XT>), dim3(tr_n * tq_n, 1, nb), dim3(kC2iThreads), 0,
+                       s, g, xT, P.brec, P.start, gcolT, gxT, goff, b0, tq_n);
+    return;
+  }
   hipLaunchKernelGGL((col2im_tile<2, 4, GT, XT>), dim3(tr_n * tq_n, 1, nb), dim3(kC2iThreads), 0,
                      s, g, xT, P.brec, P.start, gcolT, gxT, goff, b0, tq_n);
 }
