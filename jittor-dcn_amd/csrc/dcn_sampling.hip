@@ -1238,7 +1238,7 @@ static void launch_k5_fused(const Geo& g, const XT* xT, const BinsWs& P, const G
   // bf16 rows stay raw (8 B per lane) until consumed, so 3 rows in flight fit the 6-waves-per-
   // SIMD budget (80 VGPRs): config 4 0.189 (U = 2, converted at load) -> 0.162 (U = 2 raw) ->
   // 0.154 ms (U = 3 raw); U = 4 spills at 6 waves and runs 0.178 at 5. DCN_EXP slot 12 = 2
-  // keeps U = 2.
+  // keeps U = 2. fp32 rows (16 B per lane) with U = 3 spill 32 B at 6 waves: 0.67 -> 0.88 ms.
   if (sizeof(GT) == 2 && exp_flag(12) != 2) {
     hipLaunchKernelGGL((col2im_tile<3, 4, GT, XT>), dim3(tr_n * tq_n, 1, nb), dim3(kC2iThreads), 0,
                        s, g, xT, P.brec, P.start, gcolT, gxT, goff, b0, tq_n);
