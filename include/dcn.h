@@ -305,7 +305,8 @@ int dcn_set_fwd_path(dcn_handle* h, int path);
  *  10  1: bf16 offset conv forward on the register-direct MFMA kernel instead of the
  *        LDS-windowed row kernel
  *  11  n > 0: bf16 ∂W_off kernel sums n row chunks per workgroup (default 2)
- *  12  2: bf16 K5 with 2 ∂col rows in flight per wave instead of 3
+ *  12  1: K5 on 4-row input tiles (5 waves) instead of 7-row tiles (8 waves);
+ *      2: bf16 K5 with 2 ∂col rows in flight per wave instead of 3
  *  13  1: fp32 NCHW -> NHWC transposes (x -> xT, ∂out -> ∂outT + ∂b) with 4-byte accesses
  *        instead of the 16-byte form
  *  14  1: bf16 K1 with 4 channels per lane instead of 8

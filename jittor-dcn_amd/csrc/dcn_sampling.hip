@@ -604,7 +604,7 @@ __global__ __launch_bounds__(256) void bins_fill(Geo g, const float4* __restrict
 
 // ---------------------------------------------------------------------------
 // K5 fused (∂x + ∂offset from ONE pass over the binned ∂col rows).
-// One block = a kTR x kTQ tile of INPUT pixels of one image and kTR+1 waves. Bin
+// One block = a kTR x kTQ tile (template parameters) of INPUT pixels of one image and kTR+1 waves. Bin
 // (br, bc) holds the samples whose top-left corner is (br-1, bc-1) (K5b); wave w walks
 // bin row br = R0+w (bin columns Q0..Q0+kTQ, samples in sorted order), reading each
 // ∂colT row once, and accumulates into the two pixel rows that bin row touches: r0
@@ -617,8 +617,6 @@ __global__ __launch_bounds__(256) void bins_fill(Geo g, const float4* __restrict
 // image: zero). ∂offset uses offgrad_cl's op order (per-lane channel sums, fixed xor
 // tree). Used for deform_groups == 1, C % 4 == 0, C <= 256.
 // ---------------------------------------------------------------------------
-constexpr int kTR = 4;  // tile rows; kTR+1 waves per block (tile cols: template TQ)
-constexpr int kC2iThreads = (kTR + 1) * 64;
 
 __device__ __forceinline__ float4 fma4(float w, float4 g, float4 a) {
   return make_float4(fmaf(w, g.x, a.x), fmaf(w, g.y, a.y), fmaf(w, g.z, a.z), fmaf(w, g.w, a.w));
@@ -627,15 +625,15 @@ __device__ __forceinline__ float4 add4(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
 
-template <int U, int kTQ, typename GT = float, typename XT = float>
-__global__ __launch_bounds__(kC2iThreads) __attribute__((amdgpu_waves_per_eu(6))) void col2im_tile(Geo g, const XT* __restrict__ xT,
+template <int U, int kTQ, typename GT = float, typename XT = float, int WPE = 6, int kTR = 4>
+__global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(WPE))) void col2im_tile(Geo g, const XT* __restrict__ xT,
                                                            const int4* __restrict__ brec,
                                                            const int* __restrict__ start,
                                                            const GT* __restrict__ gcolT,
                                                            float* __restrict__ gxT,
                                                            float* __restrict__ goff, int b0,
                                                            int tq_n) {
-  constexpr int WR = kTR + 1, WQ = kTQ + 1;
+  constexpr int kC2iThreads = (kTR + 1) * 64, WR = kTR + 1, WQ = kTQ + 1;
   constexpr int WIN = WR * WQ * 64, UPR = kTR * kTQ * 64;  // float4 slots
   __shared__ float4 lds[WIN > UPR ? WIN : UPR];  // xT window, then the upper rows
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1229,23 +1227,37 @@ static BinsWs bins_view(const Geo& g, void* bins_ws, int b0, int nb, int bins_nb
 // r01 A/B at config 3 (2-deep prefetch pipeline): U=2 0.92 ms col2im, U=4 0.93, U=8 1.50;
 // 4x6 tiles 1.05x slower, 4x8 tiles no longer unroll (2.7 ms). r02: column sweeps and
 // strips without the tile's bin-row re-read measured no faster (DESIGN.md §4 "K5").
+template <int U, int TQ, int WPE, int TR, typename GT, typename XT>
+static void launch_c2i(const Geo& g, const XT* xT, const BinsWs& P, const GT* gcolT, float* gxT,
+                       float* goff, int b0, int nb, hipStream_t s) {
+  const int tr_n = (g.H + TR - 1) / TR, tq_n = (g.W + TQ - 1) / TQ;
+  hipLaunchKernelGGL((col2im_tile<U, TQ, GT, XT, WPE, TR>), dim3(tr_n * tq_n, 1, nb),
+                     dim3((TR + 1) * 64), 0, s, g, xT, P.brec, P.start, gcolT, gxT, goff, b0, tq_n);
+}
+
 template <typename GT, typename XT>
 static void launch_k5_fused(const Geo& g, const XT* xT, const BinsWs& P, const GT* gcolT,
                             float* gxT, float* goff, int b0, int nb, hipStream_t s) {
-  const int tr_n = (g.H + kTR - 1) / kTR, tq_n = (g.W + 4 - 1) / 4;
   // U = 2 rows in flight per wave for both element types: U = 4 for the half-length bf16
   // rows measured slower (r02, config 4: 0.192 against 0.187 ms; 95 VGPRs, 5 waves/SIMD)
   // bf16 rows stay raw (8 B per lane) until consumed, so 3 rows in flight fit the 6-waves-per-
   // SIMD budget (80 VGPRs): config 4 0.189 (U = 2, converted at load) -> 0.162 (U = 2 raw) ->
   // 0.154 ms (U = 3 raw); U = 4 spills at 6 waves and runs 0.178 at 5. DCN_EXP slot 12 = 2
   // keeps U = 2. fp32 rows (16 B per lane) with U = 3 spill 32 B at 6 waves: 0.67 -> 0.88 ms.
-  if (sizeof(GT) == 2 && exp_flag(12) != 2) {
-    hipLaunchKernelGGL((col2im_tile<3, 4, GT, XT>), dim3(tr_n * tq_n, 1, nb), dim3(kC2iThreads), 0,
-                       s, g, xT, P.brec, P.start, gcolT, gxT, goff, b0, tq_n);
-    return;
+  // Tile rows (kTR; kTR + 1 waves per workgroup): 4 -> 7 (r02) cuts the bin rows read twice
+  // (a tile re-reads the bin row it shares with the tile below: 5/4 -> 8/7 of the ∂col rows)
+  // at the same 24 waves per CU (3 workgroups of 8, 40 KB of window each). Config 3 fp32 /
+  // config 4 bf16: kTR 4 0.667 / 0.152 ms, 5 0.651 / 0.163, 6 0.630 / 0.151, 7 0.568 / 0.129,
+  // 8 (2 workgroups per CU) 0.658 / 0.167, 11 0.585 / 0.137. DCN_EXP slot 12 = 1 keeps kTR 4.
+  const int e = exp_flag(12);
+  if constexpr (sizeof(GT) == 2) {
+    if (e == 1) return launch_c2i<3, 4, 6, 4>(g, xT, P, gcolT, gxT, goff, b0, nb, s);
+    if (e == 2) return launch_c2i<2, 4, 6, 7>(g, xT, P, gcolT, gxT, goff, b0, nb, s);
+    return launch_c2i<3, 4, 6, 7>(g, xT, P, gcolT, gxT, goff, b0, nb, s);
+  } else {
+    if (e == 1) return launch_c2i<2, 4, 6, 4>(g, xT, P, gcolT, gxT, goff, b0, nb, s);
+    return launch_c2i<2, 4, 6, 7>(g, xT, P, gcolT, gxT, goff, b0, nb, s);
   }
-  hipLaunchKernelGGL((col2im_tile<2, 4, GT, XT>), dim3(tr_n * tq_n, 1, nb), dim3(kC2iThreads), 0,
-                     s, g, xT, P.brec, P.start, gcolT, gxT, goff, b0, tq_n);
 }
 
 hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, const float* off,
