@@ -907,6 +907,16 @@ int dcn_forward(dcn_handle* h, const dcn_desc* d, const float* x, const float* w
                         reinterpret_cast<bf16_t*>(off), base, L);
   }
   float* xT = reinterpret_cast<float*>(base + L.xT);
+  if (dcn::offset_fwd_mfma_xt_ok(g)) {
+    // offsets on the f32 matrix cores, writing xT from the same reads of x
+    {
+      ProfScope ps(h, DCN_K_OFFSET_FWD);
+      HIP_TRY(dcn::launch_offset_conv_fwd_xt(g, x, w_off, b_off, off, xT,
+                                             reinterpret_cast<float*>(base + L.wt), h->stream));
+    }
+    return core_forward(h, g, x, off, w, b, d->has_bias != 0, out, xT,
+                        reinterpret_cast<float*>(base + L.col), true);
+  }
   // x -> channels-last on the side stream, beside the offset conv (both only read x)
   DCN_TRY(fork_aux(h));
   {

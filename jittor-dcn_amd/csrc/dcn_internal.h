@@ -74,6 +74,10 @@ size_t offset_conv_wt_floats(const Geo& g);
 size_t offset_conv_goffT_floats(const Geo& g);  // ∂offT rows + ∂w_off block partials
 size_t offset_conv_fpart_floats(const Geo& g);  // forward channel-slice partials
 // part: scratch of offset_conv_fpart_floats(g) floats (channel-slice partial sums).
+bool offset_fwd_mfma_xt_ok(const Geo& g);
+hipError_t launch_offset_conv_fwd_xt(const Geo& g, const float* x, const float* w_off,
+                                     const float* b_off, float* off, float* xT, float* wf,
+                                     hipStream_t s);
 hipError_t launch_offset_conv_fwd(const Geo& g, const float* x, const float* w_off,
                                   const float* b_off, float* off, float* wt, float* part,
                                   hipStream_t s);

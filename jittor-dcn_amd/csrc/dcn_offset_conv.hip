@@ -1542,9 +1542,256 @@ __global__ __launch_bounds__(256) void offset_bwd_generic(Geo g, const float* __
     default: generic = true; break; \
   }
 
+// ---------------------------------------------------------------------------
+// K3 on the f32 matrix cores, fused with the x -> xT transpose (fp32, 3x3, stride 1, pad 1,
+// Ho == H, Wo == W <= 62, W % 4 == 0, C % 16 == 0, J <= 18).
+//   off[b][j][ho][p] = b_off[j] + Σ_{c, tap} w_off[j][c][tap] · x[b][c][ho-1+ty][p-1+tx]
+// One workgroup = ROWS output rows of one image; wave w computes 16 pixels (p = 4m + (w&3),
+// m = 0..15) of row w>>2 over ALL channels, walking them in 16-channel chunks that the
+// workgroup stages together, double-buffered: the ROWS+2 input rows of the chunk (loaded
+// from NCHW x with coalesced 16-B row loads, written channels-last into LDS at a pitch of
+// 20 floats per pixel, so one 16-B LDS read gives a lane 4 consecutive channels) and the
+// chunk's weights in MFMA fragment order. The next chunk's loads are in flight while the
+// current chunk computes; one LDS-only barrier per chunk.
+// v_mfma_f32_16x16x4_f32: A row m = pixel 4m + (w&3), A column k = lane group g (channel
+// 4g + s at step s), B = weights, D = 16 pixels x offset channels 0-15. Offset channels
+// 16-17 run on the VALU from the same A values (lane-group partials summed at the end in a
+// fixed order). The window rows 1..ROWS are the input rows ho0.. (Ho == H): the workgroup
+// writes them to xT, so no separate transpose pass reads x again. Every sum has a fixed
+// order: deterministic.
+// ---------------------------------------------------------------------------
+constexpr int kXtCP = 20, kXtRWmax = 64, kXtWts = 9 * 64 * 4 + 9 * 4 * 8;  // floats
+
+// per 16-channel chunk cg, kXtWts floats: B[t][lane][s] = w_off[j = lane&15][c][t] with
+// c = 16cg + 4(lane>>4) + s, then V[t][g][2s + jj] = w_off[16 + jj][16cg + 4g + s][t]
+// (0 for j >= J)
+__global__ __launch_bounds__(256) void woff_to_f32frag(const float* __restrict__ w,
+                                                       float* __restrict__ wf, int J, int C) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= C / 16 * kXtWts) return;
+  const int cg = i / kXtWts, k = i - cg * kXtWts;
+  int j, c, t;
+  if (k < 9 * 256) {
+    const int s = k & 3, lane = (k >> 2) & 63;
+    t = k >> 8;
+    j = lane & 15;
+    c = 16 * cg + 4 * (lane >> 4) + s;
+  } else {
+    const int v = k - 9 * 256, jj = v & 1, s = (v >> 1) & 3, gg = (v >> 3) & 3;
+    t = v >> 5;
+    j = 16 + jj;
+    c = 16 * cg + 4 * gg + s;
+  }
+  wf[i] = j < J ? w[((size_t)j * C + c) * 9 + t] : 0.f;
+}
+
+template <int ROWS, int RPW>  // output rows per workgroup, rows per wave (same pixel tile)
+__global__ __launch_bounds__(ROWS * 256 / RPW) __attribute__((amdgpu_waves_per_eu(2))) void
+offset_conv_fwd_mfma_xt(Geo g, const float* __restrict__ x, const float* __restrict__ wf,
+                        const float* __restrict__ b_off, float* __restrict__ off,
+                        float* __restrict__ xT) {
+  constexpr int NT = ROWS * 256 / RPW, NR = ROWS + 2, CP = kXtCP;
+  constexpr int RW = kXtRWmax;              // window row pitch (pixels): compile-time offsets
+  constexpr int WIN = NR * RW * CP;         // floats per window buffer
+  constexpr int BUF = WIN + kXtWts;
+  constexpr int kSx = (16 * NR * 16 + NT - 1) / NT, kSw = (kXtWts / 4 + NT - 1) / NT;
+  __shared__ __attribute__((aligned(16))) float lds[2 * BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tt = w & 3, r0 = (w >> 2) * RPW;  // this wave's pixel tile and first row
+  const Block3 blk = xcd_block();
+  const int ho0 = blk.x * ROWS, b = blk.z;
+  const int H = g.H, W = g.W, C = g.C, NQ = W / 4;
+  const int m = lane & 15, gq = lane >> 4;
+  const int nch = C / 16;
+  // zero padding columns 0 and W+1 of both buffers (never overwritten)
+  for (int i = tid; i < 2 * NR * 2 * 16; i += NT) {
+    const int cc = i & 15, z = (i >> 4) & 1, row = (i >> 5) % NR, bf = i / (32 * NR);
+    lds[bf * BUF + (row * RW + (z ? W + 1 : 0)) * CP + cc] = 0.f;
+  }
+  float4 sx0[kSx], sw0[kSw], sx1[kSx], sw1[kSw];  // chunks k+1 and k+2 in flight
+  // per-lane staging addresses, the same for every chunk. Lane = (channel fastest, then 4
+  // pixels): the global loads read 64-B runs of 16 channel rows, and the channels-last LDS
+  // writes of one instruction fall in 64 different banks
+  int gx[kSx], lx[kSx];
+#pragma unroll
+  for (int u = 0; u < kSx; ++u) {
+    const int idx = tid + NT * u, cc = idx & 15, rest = idx >> 4;
+    const int q = rest % NQ, row = rest / NQ;
+    const int y = ho0 - 1 + row;
+    const bool in = row < NR;
+    gx[u] = in && y >= 0 && y < H ? (cc * H + y) * W + 4 * q : -1;
+    lx[u] = in ? (row * RW + 1 + 4 * q) * CP + cc : -1;
+  }
+  // branch-free loads (buffer range checks give the zeros), so no conditional load makes the
+  // compiler drain the prefetch early
+  const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x + (size_t)b * C * H * W),
+                                                    0, (int)((size_t)C * H * W * 4), 0x00020000);
+  const auto rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wf), 0,
+                                                    (int)((size_t)(C / 16) * kXtWts * 4), 0x00020000);
+  auto load_chunk = [&](int k, float4(&sx)[kSx], float4(&sw)[kSw]) __attribute__((always_inline)) {
+    k = min(k, nch - 1);  // past the end: a harmless re-load (no conditional loads)
+#pragma unroll
+    for (int u = 0; u < kSx; ++u) {
+      const unsigned o = gx[u] >= 0 ? (unsigned)(k * 16 * H * W + gx[u]) * 4u : 0x80000000u;
+      const auto q = __builtin_amdgcn_raw_buffer_load_b128(rx, o, 0, 0);
+      sx[u] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]),
+                          __uint_as_float(q[3]));
+    }
+#pragma unroll
+    for (int u = 0; u < kSw; ++u) {
+      const int idx = tid + NT * u;
+      const unsigned o = idx < kXtWts / 4 ? (unsigned)(k * kXtWts + 4 * idx) * 4u : 0x80000000u;
+      const auto q = __builtin_amdgcn_raw_buffer_load_b128(rw, o, 0, 0);
+      sw[u] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]),
+                          __uint_as_float(q[3]));
+    }
+  };
+  auto store_chunk = [&](int bf, const float4(&sx)[kSx], const float4(&sw)[kSw])
+                         __attribute__((always_inline)) {
+    float* L = lds + bf * BUF;
+#pragma unroll
+    for (int u = 0; u < kSx; ++u) {
+      if (lx[u] >= 0) {
+        float* d = L + lx[u];
+        d[0] = sx[u].x;
+        d[CP] = sx[u].y;
+        d[2 * CP] = sx[u].z;
+        d[3 * CP] = sx[u].w;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kSw; ++u) {
+      const int idx = tid + NT * u;
+      if (idx < kXtWts / 4) reinterpret_cast<float4*>(L + WIN)[idx] = sw[u];
+    }
+  };
+  f32x4 acc[RPW];
+  float e0[RPW], e1[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    e0[r] = e1[r] = 0.f;
+  }
+  // A column of each tap: pixel 4m + tt + tx, clamped for the pixels past W (discarded)
+  const int pc = min(4 * m + tt, W - 1);
+  auto step = [&](int k, float4(&sxn)[kSx], float4(&swn)[kSw]) __attribute__((always_inline)) {
+    // LDS buffer k&1 holds chunk k; (sxn, swn) chunk k+1; the other set chunk k+2 (in flight)
+    const int bf = k & 1;
+    const float* L = lds + bf * BUF;
+    {  // input rows ho0.. (window rows 1..ROWS), this chunk's 16 channels -> xT
+      const int part = tid & 3;
+      constexpr int kXs = (ROWS * RW + NT / 4 - 1) / (NT / 4);  // fixed trip count: the
+#pragma unroll                                                // waitcnt pass keeps counting
+      for (int u = 0; u < kXs; ++u) {
+        const int i = (tid >> 2) + u * (NT / 4);
+        const int r = i / W, px = i - r * W, y = ho0 + r;
+        if (i < ROWS * W && y < H)
+          *reinterpret_cast<float4*>(xT + ((size_t)(b * H + y) * W + px) * C + k * 16 + 4 * part) =
+              *reinterpret_cast<const float4*>(L + ((1 + r) * RW + 1 + px) * CP + 4 * part);
+      }
+    }
+    const float* LB = L + WIN;
+#pragma unroll 1
+    for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+    for (int tx = 0; tx < 3; ++tx) {
+      const int t = ty * 3 + tx;
+      const float4 bw = *reinterpret_cast<const float4*>(LB + (t * 64 + lane) * 4);
+      const float4 v0 = *reinterpret_cast<const float4*>(LB + 9 * 256 + (t * 4 + gq) * 8);
+      const float4 v1 = *reinterpret_cast<const float4*>(LB + 9 * 256 + (t * 4 + gq) * 8 + 4);
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) {
+        const float4 a =
+            *reinterpret_cast<const float4*>(L + ((r0 + r + ty) * RW + pc + tx) * CP + 4 * gq);
+        acc[r] = mfma16(a.x, bw.x, acc[r]);
+        acc[r] = mfma16(a.y, bw.y, acc[r]);
+        acc[r] = mfma16(a.z, bw.z, acc[r]);
+        acc[r] = mfma16(a.w, bw.w, acc[r]);
+        e0[r] = fmaf(a.x, v0.x, e0[r]);
+        e1[r] = fmaf(a.x, v0.y, e1[r]);
+        e0[r] = fmaf(a.y, v0.z, e0[r]);
+        e1[r] = fmaf(a.y, v0.w, e1[r]);
+        e0[r] = fmaf(a.z, v1.x, e0[r]);
+        e1[r] = fmaf(a.z, v1.y, e1[r]);
+        e0[r] = fmaf(a.w, v1.z, e0[r]);
+        e1[r] = fmaf(a.w, v1.w, e1[r]);
+      }
+    }
+    if (k + 1 < nch) store_chunk(bf ^ 1, sxn, swn);
+    load_chunk(k + 3, sxn, swn);
+    lds_barrier();
+  };
+  load_chunk(0, sx0, sw0);
+  load_chunk(1, sx1, sw1);
+  store_chunk(0, sx0, sw0);
+  load_chunk(2, sx0, sw0);
+  lds_barrier();
+  for (int k = 0; k < nch; k += 2) {
+    step(k, sx1, sw1);
+    if (k + 1 < nch) step(k + 1, sx0, sw0);
+  }
+  // through LDS as [row][j][64 pixels], then runs of consecutive pixels per offset channel
+  float* T = lds;  // the buffers are free: the last barrier followed the last reads
+  const int j = lane & 15;
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    // lane groups' VALU partials (channels 4g..4g+3 of every chunk) in a fixed order
+    float s0 = e0[r], s1 = e1[r];
+    s0 += __shfl_xor(s0, 16);
+    s1 += __shfl_xor(s1, 16);
+    s0 += __shfl_xor(s0, 32);
+    s1 += __shfl_xor(s1, 32);
+    const int rr = r0 + r;
+    if (j < g.J) {
+      const float bj = b_off[j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) T[(rr * 18 + j) * 64 + 4 * (4 * gq + i) + tt] = acc[r][i] + bj;
+    }
+    if (lane < 16) {
+      if (g.J > 16) T[(rr * 18 + 16) * 64 + 4 * m + tt] = s0 + b_off[16];
+      if (g.J > 17) T[(rr * 18 + 17) * 64 + 4 * m + tt] = s1 + b_off[17];
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < ROWS * g.J * W; i += NT) {
+    const int r = i / (g.J * W), rem = i - r * g.J * W, jo = rem / W, p = rem - jo * W;
+    const int ho = ho0 + r;
+    if (ho < H) off[((size_t)(b * g.J + jo) * H + ho) * W + p] = T[(r * 18 + jo) * 64 + p];
+  }
+}
+
+bool offset_fwd_mfma_xt_ok(const Geo& g) {
+  return g.dt == DCN_F32 && g.kh == 3 && g.kw == 3 && g.sh == 1 && g.sw == 1 && g.dh == 1 &&
+         g.dw == 1 && g.ph == 1 && g.pw == 1 && g.Ho == g.H && g.Wo == g.W &&
+         g.W + 2 <= kXtRWmax && g.W % 4 == 0 && g.C % 16 == 0 && g.J >= 1 && g.J <= 18 &&
+         exp_flag(3) != 1;
+}
+
+// off and xT (channels-last x) from x in one pass; wf: offset_conv_wt_floats(g) scratch
+hipError_t launch_offset_conv_fwd_xt(const Geo& g, const float* x, const float* w_off,
+                                     const float* b_off, float* off, float* xT, float* wf,
+                                     hipStream_t s) {
+  if (!offset_fwd_mfma_xt_ok(g)) return hipErrorInvalidValue;
+  const int n = g.C / 16 * kXtWts;
+  hipLaunchKernelGGL(woff_to_f32frag, dim3((n + 255) / 256), dim3(256), 0, s, w_off, wf, g.J, g.C);
+  if (g.B > 0) {
+    auto go = [&](auto kern, int rows, int nt) {
+      hipLaunchKernelGGL(kern, dim3((g.H + rows - 1) / rows, 1, g.B), dim3(nt), 0, s, g, x, wf,
+                         b_off, off, xT);
+    };
+    const int e = exp_flag(3);
+    if (e == 2) go(offset_conv_fwd_mfma_xt<2, 2>, 2, 256);
+    else if (e == 3) go(offset_conv_fwd_mfma_xt<4, 2>, 4, 512);
+    else go(offset_conv_fwd_mfma_xt<2, 1>, 2, 512);
+  }
+  return hipGetLastError();
+}
+
 size_t offset_conv_wt_floats(const Geo& g) {
   const size_t KK = (size_t)g.kh * g.kw;
-  return std::max((size_t)pad_j(g.J) * g.C * KK, (size_t)tj_pad4(g) * pad_c(g.C));
+  return std::max({(size_t)pad_j(g.J) * g.C * KK, (size_t)tj_pad4(g) * pad_c(g.C),
+                   (size_t)(g.C + 15) / 16 * kXtWts});  // offset_conv_fwd_mfma_xt's weights
 }
 size_t offset_conv_fpart_floats(const Geo& g) { return (size_t)kSplit * g.B * g.J * g.HW; }
 

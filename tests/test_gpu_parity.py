@@ -145,6 +145,10 @@ def _oracle(c, dev_off=None):
     dict(seed=6, B=2, C=12, O_=6, H=11, W=12, k=(3, 2), s=(1, 2), p=(1, 0), bias=False),
     dict(seed=7, B=2, C=320, O_=16, H=9, W=10),                     # C > 256: lane-map loop
     dict(seed=8, B=3, C=6, O_=5, H=13, W=11, s=(2, 1)),              # C % 4 != 0: scalar lanes
+    # f32-MFMA offset conv fused with the x transpose (3x3 s1 p1, W % 4 == 0, C % 16 == 0)
+    dict(seed=9, B=2, C=16, O_=8, H=7, W=4),         # odd H: the last workgroup's 2nd row idle
+    dict(seed=10, B=1, C=48, O_=8, H=6, W=60),       # widest row it stages
+    dict(seed=11, B=2, C=256, O_=16, H=9, W=56, off_scale=2.0),  # config-3 rows and channels
 ])
 def test_device_api_vs_oracle(gpu_handle, case):
     c = _rand_case(**case)
