@@ -297,6 +297,9 @@ int dcn_set_fwd_path(dcn_handle* h, int path);
  * DESIGN.md §4. Slots:
  *   2  1: fp32 K5 as two kernels (offgrad_cl + dx_gather_cl) instead of col2im_tile
  *   4  1: offset conv forward on the per-pixel VALU kernel instead of the 2-px row kernel
+ *   3  1: fp32 offset conv forward on the VALU kernel with the x transpose beside it
+ *        instead of the f32-MFMA kernel that writes xT itself; 2 / 3: that kernel with
+ *        2 rows x 2 pixel tiles per wave / 4 rows per workgroup
  *   5  1 / 2: split-bf16 GEMM form EARLY / LATE (default: picked per shape)
  *   6  1: offset conv backward on the VALU kernels instead of the MFMA ones
  *   7  n > 0: output rows per wave of the VALU ∂w_off kernel (default 4)
@@ -310,7 +313,7 @@ int dcn_set_fwd_path(dcn_handle* h, int path);
  *  13  1: fp32 NCHW -> NHWC transposes (x -> xT, ∂out -> ∂outT + ∂b) with 4-byte accesses
  *        instead of the 16-byte form
  *  14  1: bf16 K1 with 4 channels per lane instead of 8
- * Slots 0, 1, 3 and 15 are unused. */
+ * Slots 0, 1 and 15 are unused. */
 
 /* ---- testing ------------------------------------------------------------------ */
 /* One fp32 GEMM through the handle's engine under its current math mode, BLAS
