@@ -295,6 +295,8 @@ int dcn_set_fwd_path(dcn_handle* h, int path);
  * switches between implementations of the same math for speed experiments; results agree
  * to fp32 rounding (only summation orders change). Each alternative is measured in
  * DESIGN.md §4. Slots:
+ *   1  1: fp32 ∂b_off as one 1024-thread block per offset channel instead of the
+ *        two-level (channel, image) sum
  *   2  1: fp32 K5 as two kernels (offgrad_cl + dx_gather_cl) instead of col2im_tile
  *   4  1: offset conv forward on the per-pixel VALU kernel instead of the 2-px row kernel
  *   3  1: fp32 offset conv forward on the VALU kernel with the x transpose beside it
@@ -313,7 +315,7 @@ int dcn_set_fwd_path(dcn_handle* h, int path);
  *  13  1: fp32 NCHW -> NHWC transposes (x -> xT, ∂out -> ∂outT + ∂b) with 4-byte accesses
  *        instead of the 16-byte form
  *  14  1: bf16 K1 with 4 channels per lane instead of 8
- * Slots 0, 1 and 15 are unused. */
+ * Slots 0 and 15 are unused. */
 
 /* ---- testing ------------------------------------------------------------------ */
 /* One fp32 GEMM through the handle's engine under its current math mode, BLAS

@@ -963,7 +963,11 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
     // ∂b_off = Σ ∂offset (18 channels: a latency-bound reduction) on the side stream, beside
     // the offset-conv ∂W / ∂x kernels
     DCN_TRY(fork_aux(h));
-    dcn::launch_channel_sum(goff, g.B, g.J, g.HW, grad_b_off, h->aux);
+    // (two-level over (channel, image) blocks; DCN_EXP slot 1 = 1: one block per channel)
+    if (dcn::exp_flag(1) == 1)
+      dcn::launch_channel_sum(goff, g.B, g.J, g.HW, grad_b_off, h->aux);
+    else
+      dcn::launch_channel_sum_2l(goff, g.B, g.J, g.HW, F(L.part), grad_b_off, h->aux);
     HIP_TRY(dcn::launch_offset_conv_bwd(g, x, F(L.xT), w_off, goff, F(L.goffT), F(L.wt), grad_x,
                                         grad_w_off, nullptr,
                                         dcn::get_force_generic() ? nullptr : F(L.gxT), h->stream));

@@ -129,6 +129,8 @@ hipError_t launch_round_to_bf16(float* v, bf16_t* out, size_t n, hipStream_t s);
 hipError_t launch_bias_to_bf16(const Geo& g, const float* out32, const float* bias, bf16_t* out,
                                hipStream_t s);
 void launch_channel_sum(const float* in, int B, int Cn, int HW, float* out, hipStream_t s);
+void launch_channel_sum_2l(const float* in, int B, int Cn, int HW, float* part, float* out,
+                           hipStream_t s);
 void launch_channel_sum_bf16(const bf16_t* in, int B, int Cn, int HW, float* out, hipStream_t s);
 // in[b][c][p] -> out[b][p][c] and chsum[c] = Σ_{b,p} in[b][c][p] (deterministic); tsum is
 // scratch of xpose_chsum_floats(B, C, P) floats.

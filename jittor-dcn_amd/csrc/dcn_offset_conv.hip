@@ -538,12 +538,18 @@ __global__ __launch_bounds__(256) void offset_wgrad_mfma(Geo g, const XT* __rest
   const int SW = g.W + (g.kw - 1) * g.dw;
   stage_goff(g, goff, b, y0, nrows + (g.kh - 1) * g.dh, SW, S);
   __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int n = lane & 15, q = lane >> 4;
   const int TJ = g.J * g.kh * g.kw;
   int toff[NTW];
+  // wave-uniform: N-tiles wholly past TJ (config 3: tile 11 = tj 176..191 of 162) are
+  // skipped, not multiplied (their sums were never stored)
+  bool tv[NTW];
 #pragma unroll
-  for (int u = 0; u < NTW; ++u) toff[u] = g_toff(g, 16 * (w + 4 * u) + n, SW);
+  for (int u = 0; u < NTW; ++u) {
+    toff[u] = g_toff(g, 16 * (w + 4 * u) + n, SW);
+    tv[u] = 16 * (w + 4 * u) < TJ;
+  }
   const int cb = blockIdx.y * 64;
   const bool cok = cb + 4 * n < g.C;
   f32x4 acc[4][NTW];
@@ -589,12 +595,13 @@ __global__ __launch_bounds__(256) void offset_wgrad_mfma(Geo g, const XT* __rest
         // A (0 x a stale NaN/Inf bit pattern would poison the accumulator)
         float bv[NTW];
 #pragma unroll
-        for (int u = 0; u < NTW; ++u) bv[u] = __uint_as_float(__float_as_uint(S[sb + bv0[u]]) & keep);
+        for (int u = 0; u < NTW; ++u)
+          bv[u] = tv[u] ? __uint_as_float(__float_as_uint(S[sb + bv0[u]]) & keep) : 0.f;
         sb += 4 * g.J;
         if (++sx == nq) sx = 0, sb += row_skip;
 #pragma unroll
         for (int u = 0; u < NTW; ++u)
-          mfma16x4_acc(acc[0][u], acc[1][u], acc[2][u], acc[3][u], ax, ay, az, aw, bv[u]);
+          if (tv[u]) mfma16x4_acc(acc[0][u], acc[1][u], acc[2][u], acc[3][u], ax, ay, az, aw, bv[u]);
         ring[d] = buf_ld4<XT>(rsrc, lane_x, min(lo, last));
         lo += step_x;
       }
@@ -626,10 +633,10 @@ __global__ __launch_bounds__(256) void offset_wgrad_mfma(Geo g, const XT* __rest
         if (cx >= nq * 4) cx = q, ++cy;
         float bv[NTW];
 #pragma unroll
-        for (int u = 0; u < NTW; ++u) bv[u] = sp[toff[u]];
+        for (int u = 0; u < NTW; ++u) bv[u] = tv[u] ? sp[toff[u]] : 0.f;
 #pragma unroll
         for (int u = 0; u < NTW; ++u)
-          mfma16x4_acc(acc[0][u], acc[1][u], acc[2][u], acc[3][u], ax, ay, az, aw, bv[u]);
+          if (tv[u]) mfma16x4_acc(acc[0][u], acc[1][u], acc[2][u], acc[3][u], ax, ay, az, aw, bv[u]);
         ring[d] = load_next();  // after the slot's last use: no register copy
       }
     }

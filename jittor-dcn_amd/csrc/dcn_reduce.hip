@@ -48,6 +48,44 @@ void launch_channel_sum(const float* in, int B, int Cn, int HW, float* out, hipS
   else
     hipLaunchKernelGGL((channel_sum<false, float>), dim3(Cn), dim3(1024), 0, s, in, B, Cn, HW, out);
 }
+// Two-level form for few channels over many pixels (∂b_off: 18 channels, B·HW = 200k at
+// config 3), so the sum does not hold 18 CUs for 0.11 ms beside the offset-conv backward:
+// part[b][ch] = Σ_m in[b][ch][m] (one 256-thread block per (channel, image), fixed xor tree
+// and wave order), then out[ch] = Σ_b part[b][ch] in image order. Deterministic.
+__global__ __launch_bounds__(256) void plane_sum(const float* __restrict__ in, int HW,
+                                                 float* __restrict__ part) {
+  __shared__ float red[4];
+  const int tid = threadIdx.x;
+  const float* p = in + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * HW;
+  float s = 0.f;
+  if ((HW & 3) == 0) {
+    for (int i = tid; i < HW / 4; i += 256) {
+      const float4 v = ld4(p + 4 * i);
+      s += (v.x + v.y) + (v.z + v.w);
+    }
+  } else {
+    for (int i = tid; i < HW; i += 256) s += p[i];
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
+  if (tid == 0) part[(size_t)blockIdx.y * gridDim.x + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+__global__ __launch_bounds__(64) void fold_images(const float* __restrict__ part, int B, int Cn,
+                                                  float* __restrict__ out) {
+  const int ch = blockIdx.x * 64 + threadIdx.x;
+  if (ch >= Cn) return;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s += part[(size_t)b * Cn + ch];
+  out[ch] = s;
+}
+void launch_channel_sum_2l(const float* in, int B, int Cn, int HW, float* part, float* out,
+                           hipStream_t s) {
+  if (((uintptr_t)in & 15) != 0) return launch_channel_sum(in, B, Cn, HW, out, s);
+  hipLaunchKernelGGL(plane_sum, dim3(Cn, B), dim3(256), 0, s, in, HW, part);
+  hipLaunchKernelGGL(fold_images, dim3((Cn + 63) / 64), dim3(64), 0, s, part, B, Cn, out);
+}
+
 void launch_channel_sum_bf16(const bf16_t* in, int B, int Cn, int HW, float* out, hipStream_t s) {
   if (HW % 4 == 0 && ((uintptr_t)in & 7) == 0)
     hipLaunchKernelGGL((channel_sum<true, bf16_t>), dim3(Cn), dim3(1024), 0, s, in, B, Cn, HW, out);
