@@ -500,8 +500,12 @@ int forward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x,
   hipStream_t st = h->stream;
   bf16_t* xT = BF(L.xT);  // channels-last bf16 x: K1, K5 and the offset conv read it
   float *off32 = F32(L.off32), *out32 = F32(L.out32);
-  HIP_TRY(dcn::launch_bf16_to_f32(b_off, F32(L.boff32), (size_t)g.J, st));
-  if (has_bias) HIP_TRY(dcn::launch_bf16_to_f32(b, F32(L.b32), (size_t)g.O, st));
+  {
+    dcn::ConvBatch cb;  // the fp32 biases, one launch
+    cb.add(b_off, F32(L.boff32), (size_t)g.J, false);
+    if (has_bias) cb.add(b, F32(L.b32), (size_t)g.O, false);
+    HIP_TRY(dcn::launch_convert_multi(cb, st));
+  }
   {
     ProfScope ps(h, DCN_K_XPOSE);
     HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(x, xT, g.B, g.C, g.HWi, st));
@@ -554,8 +558,12 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
   bf16_t* col = BF(L.col);
   const size_t nx = (size_t)g.B * g.C * g.HWi, noff = (size_t)g.B * g.J * g.HW;
   const size_t nwo = (size_t)g.J * g.C * g.N;
-  HIP_TRY(dcn::launch_bf16_to_f32(off, off32, noff, st));  // == the forward's rounded offsets
-  HIP_TRY(dcn::launch_bf16_to_f32(w_off, F32(L.woff32), nwo, st));
+  {
+    dcn::ConvBatch cb;
+    cb.add(off, off32, noff, false);  // == the forward's rounded offsets
+    cb.add(w_off, F32(L.woff32), nwo, false);
+    HIP_TRY(dcn::launch_convert_multi(cb, st));
+  }
   DCN_TRY(fork_aux(h));
   HIP_TRY(dcn::launch_bins(g, off32, base + L.bins, goff32, 0, g.B, h->aux));
   if (!col_valid) {
@@ -569,8 +577,7 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
   const bool exch = h->comm != nullptr;  // sum the fp32 copies over ranks, then round
   if (has_bias) {
     ProfScope ps(h, DCN_K_BWD_BIAS);  // Σ over images and pixels of the bf16 ∂out, in fp32
-    dcn::launch_channel_sum_bf16(gout, g.B, g.O, g.HW, F32(L.gb32), st);
-    if (!exch) HIP_TRY(dcn::launch_f32_to_bf16(F32(L.gb32), gb, (size_t)g.O, st));
+    dcn::launch_channel_sum_bf16(gout, g.B, g.O, g.HW, F32(L.gb32), st, exch ? nullptr : gb);
   }
   bf16_t* goutT = BF(L.goutT);
   const int dwg = dw_groups(g);
@@ -599,8 +606,8 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
       sp.batch = g.B;
       GEMM_TRY(h, sp, col, gout, F32(L.parts));
     }
-    HIP_TRY(dcn::launch_sum_partials(F32(L.parts), nparts, (size_t)g.K * g.O, F32(L.gw32), st));
-    if (!exch) HIP_TRY(dcn::launch_f32_to_bf16(F32(L.gw32), gw, (size_t)g.O * g.K, st));
+    HIP_TRY(dcn::launch_sum_partials(F32(L.parts), nparts, (size_t)g.K * g.O, F32(L.gw32), st,
+                                     exch ? nullptr : gw));
   }
   DCN_TRY(dw_final(h, F32(L.gw32), has_bias ? F32(L.gb32) : nullptr, g, exch ? gw : nullptr,
                    exch && has_bias ? gb : nullptr));
@@ -641,11 +648,17 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
                                         F32(L.wt), gx32, F32(L.gwo32), F32(L.gbo32), F32(L.gxT),
                                         st));
   }
-  if (!dcn::offset_bwd_bf16_ok(g)) HIP_TRY(dcn::launch_f32_to_bf16(gx32, gx, nx, st));
-  if (goff_out) HIP_TRY(dcn::launch_f32_to_bf16(goff32, goff_out, noff, st));
+  // the bf16 results, one launch (the offset-conv parameter grads after the exchange when
+  // there is one)
+  dcn::ConvBatch cb;
+  if (!dcn::offset_bwd_bf16_ok(g)) cb.add(gx32, gx, nx, true);
+  if (goff_out) cb.add(goff32, goff_out, noff, true);
+  if (!exch) {
+    cb.add(F32(L.gwo32), gw_off, nwo, true);
+    cb.add(F32(L.gbo32), gb_off, (size_t)g.J, true);
+  }
+  HIP_TRY(dcn::launch_convert_multi(cb, st));
   if (exch) return grads_final(h, F32(L.gwo32), F32(L.gbo32), g, gw_off, gb_off);
-  HIP_TRY(dcn::launch_f32_to_bf16(F32(L.gwo32), gw_off, nwo, st));
-  HIP_TRY(dcn::launch_f32_to_bf16(F32(L.gbo32), gb_off, (size_t)g.J, st));
   return DCN_OK;
 }
 #undef BF

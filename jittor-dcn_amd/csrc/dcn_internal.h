@@ -123,6 +123,22 @@ hipError_t launch_offset_bwd_finish(const Geo& g, const float* goff, const float
 // dcn_reduce.hip conversions: bf16 <-> f32 (RNE), and the bf16 rounding of a f32 tensor
 // in place (out = bf16(v), v = f32(out)) so later f32 work sees exactly the bf16 value.
 hipError_t launch_bf16_to_f32(const bf16_t* in, float* out, size_t n, hipStream_t s);
+// several bf16 <-> fp32 conversions in one launch (segments with n == 0 are skipped)
+constexpr int kMaxConv = 4;
+struct ConvSeg {
+  const void* in;
+  void* out;
+  size_t n;
+  int to_bf16;  // 1: fp32 -> bf16 (RNE), 0: bf16 -> fp32
+};
+struct ConvBatch {
+  ConvSeg seg[kMaxConv];
+  int n = 0;
+  void add(const void* in, void* out, size_t count, bool to_bf16) {
+    if (count && n < kMaxConv) seg[n++] = ConvSeg{in, out, count, to_bf16 ? 1 : 0};
+  }
+};
+hipError_t launch_convert_multi(const ConvBatch& cb, hipStream_t s);
 hipError_t launch_f32_to_bf16(const float* in, bf16_t* out, size_t n, hipStream_t s);
 hipError_t launch_round_to_bf16(float* v, bf16_t* out, size_t n, hipStream_t s);
 // out_bf[b][o][m] = bf16(out32[b][o][m] + bias[o]) (bias may be null)
@@ -131,7 +147,8 @@ hipError_t launch_bias_to_bf16(const Geo& g, const float* out32, const float* bi
 void launch_channel_sum(const float* in, int B, int Cn, int HW, float* out, hipStream_t s);
 void launch_channel_sum_2l(const float* in, int B, int Cn, int HW, float* part, float* out,
                            hipStream_t s);
-void launch_channel_sum_bf16(const bf16_t* in, int B, int Cn, int HW, float* out, hipStream_t s);
+void launch_channel_sum_bf16(const bf16_t* in, int B, int Cn, int HW, float* out, hipStream_t s,
+                             bf16_t* out_bf = nullptr);
 // in[b][c][p] -> out[b][p][c] and chsum[c] = Σ_{b,p} in[b][c][p] (deterministic); tsum is
 // scratch of xpose_chsum_floats(B, C, P) floats.
 size_t xpose_chsum_floats(int B, int C, int P);
@@ -145,7 +162,8 @@ hipError_t launch_bias_add(const Geo& g, float* out, const float* bias, int b0, 
                            hipStream_t s);
 hipError_t launch_bias_grad(const Geo& g, const float* gout, float* gb, hipStream_t s);
 hipError_t launch_sum_partials(const float* parts, int nparts, size_t n, float* dst,
-                               hipStream_t s);
+                               hipStream_t s,
+                               bf16_t* dst_bf = nullptr);
 
 // dcn_roi_pool.hip: deformable RoI pooling (deform_conv.py:85-241), see include/dcn.h.
 struct RoiGeo {

@@ -1471,6 +1471,8 @@ hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16
   const int n = g.C * KT16;
   hipLaunchKernelGGL(woff_to_ck_bf16, dim3((n + 255) / 256), dim3(256), 0, s2, w_off, wc, g.J, J8,
                      g.C, KK, KT16);
+  // ∂b_off: one block per channel (r02, config 4: the two-level (channel, image) sum that the
+  // fp32 path runs on its side stream measured 0.122 against 0.112 ms for this scope here)
   if (gb_off) launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s2);
   size_t lds_w, lds_x;
   bwd_bf16_lds(g, ms, &lds_w, &lds_x);

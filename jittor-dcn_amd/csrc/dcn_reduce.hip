@@ -11,7 +11,8 @@ namespace dcn {
 // a fixed wave order: deterministic. T: fp32, or bf16 (DCN_BF16's ∂out read directly).
 template <bool VEC, typename T>
 __global__ __launch_bounds__(1024) void channel_sum(const T* __restrict__ in, int B, int Cn,
-                                                    int HW, float* __restrict__ out) {
+                                                    int HW, float* __restrict__ out,
+                                                    bf16_t* __restrict__ out_bf = nullptr) {
   __shared__ float red[1024 / 64];
   const int ch = blockIdx.x, tid = threadIdx.x;
   float s = 0.f;
@@ -39,6 +40,7 @@ __global__ __launch_bounds__(1024) void channel_sum(const T* __restrict__ in, in
     float t = 0.f;
     for (int w = 0; w < 1024 / 64; ++w) t += red[w];
     out[ch] = t;
+    if (out_bf) out_bf[ch] = f2bf(t);
   }
 }
 
@@ -71,27 +73,31 @@ __global__ __launch_bounds__(256) void plane_sum(const float* __restrict__ in, i
   __syncthreads();
   if (tid == 0) part[(size_t)blockIdx.y * gridDim.x + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
+// one wave per channel: lane l sums images l, l+64, ... in order, then a fixed xor tree (a
+// serial 64-image chain per thread took 12 us of dependent loads)
 __global__ __launch_bounds__(64) void fold_images(const float* __restrict__ part, int B, int Cn,
                                                   float* __restrict__ out) {
-  const int ch = blockIdx.x * 64 + threadIdx.x;
-  if (ch >= Cn) return;
+  const int ch = blockIdx.x, l = threadIdx.x;
   float s = 0.f;
-  for (int b = 0; b < B; ++b) s += part[(size_t)b * Cn + ch];
-  out[ch] = s;
+  for (int b = l; b < B; b += 64) s += part[(size_t)b * Cn + ch];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (l == 0) out[ch] = s;
 }
 void launch_channel_sum_2l(const float* in, int B, int Cn, int HW, float* part, float* out,
                            hipStream_t s) {
   if (((uintptr_t)in & 15) != 0) return launch_channel_sum(in, B, Cn, HW, out, s);
   hipLaunchKernelGGL(plane_sum, dim3(Cn, B), dim3(256), 0, s, in, HW, part);
-  hipLaunchKernelGGL(fold_images, dim3((Cn + 63) / 64), dim3(64), 0, s, part, B, Cn, out);
+  hipLaunchKernelGGL(fold_images, dim3(Cn), dim3(64), 0, s, part, B, Cn, out);
 }
 
-void launch_channel_sum_bf16(const bf16_t* in, int B, int Cn, int HW, float* out, hipStream_t s) {
+void launch_channel_sum_bf16(const bf16_t* in, int B, int Cn, int HW, float* out, hipStream_t s,
+                             bf16_t* out_bf) {
   if (HW % 4 == 0 && ((uintptr_t)in & 7) == 0)
-    hipLaunchKernelGGL((channel_sum<true, bf16_t>), dim3(Cn), dim3(1024), 0, s, in, B, Cn, HW, out);
+    hipLaunchKernelGGL((channel_sum<true, bf16_t>), dim3(Cn), dim3(1024), 0, s, in, B, Cn, HW, out,
+                       out_bf);
   else
     hipLaunchKernelGGL((channel_sum<false, bf16_t>), dim3(Cn), dim3(1024), 0, s, in, B, Cn, HW,
-                       out);
+                       out, out_bf);
 }
 
 // ---------------------------------------------------------------------------
@@ -141,20 +147,25 @@ hipError_t launch_bias_grad(const Geo& g, const float* gout, float* gb, hipStrea
   return hipGetLastError();
 }
 
+// dst[i] = Σ_p parts[p][i] in part order; dst_bf (DCN_BF16, optional) = its bf16 rounding,
+// written by the same pass (no separate conversion launch)
 __global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restrict__ parts,
                                                            int nparts, size_t n,
-                                                           float* __restrict__ dst) {
+                                                           float* __restrict__ dst,
+                                                           bf16_t* __restrict__ dst_bf) {
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
     float s = 0.f;
     for (int p = 0; p < nparts; ++p) s += parts[(size_t)p * n + i];
     dst[i] = s;
+    if (dst_bf) dst_bf[i] = f2bf(s);
   }
 }
 
 hipError_t launch_sum_partials(const float* parts, int nparts, size_t n, float* dst,
-                               hipStream_t s) {
+                               hipStream_t s, bf16_t* dst_bf) {
   const unsigned grid = (unsigned)min((n + 255) / 256, (size_t)4096);
-  hipLaunchKernelGGL(sum_partials_kernel, dim3(grid), dim3(256), 0, s, parts, nparts, n, dst);
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(grid), dim3(256), 0, s, parts, nparts, n, dst,
+                     dst_bf);
   return hipGetLastError();
 }
 
@@ -219,6 +230,46 @@ __global__ __launch_bounds__(256) void bias_to_bf16_vec4(const float4* __restric
 static unsigned grid_for(size_t n, size_t per_thread) {
   const size_t b = (n + 256 * per_thread - 1) / (256 * per_thread);
   return (unsigned)(b < 16384 ? (b ? b : 1) : 16384);
+}
+
+// Up to kMaxConv independent conversions in ONE launch (DCN_BF16's small parameter and
+// gradient copies: each was its own 4-6 us launch). Thread quads are numbered across the
+// segments; a quad converts like bf16_to_f32_kernel / f32_to_bf16_kernel (same rounding).
+__global__ __launch_bounds__(256) void convert_multi_kernel(ConvBatch cb) {
+  size_t q0[kMaxConv + 1];
+  q0[0] = 0;
+#pragma unroll
+  for (int k = 0; k < kMaxConv; ++k) q0[k + 1] = q0[k] + (k < cb.n ? (cb.seg[k].n + 3) / 4 : 0);
+  for (size_t q = (size_t)blockIdx.x * 256 + threadIdx.x; q < q0[kMaxConv];
+       q += (size_t)gridDim.x * 256) {
+    int k = 0;
+#pragma unroll
+    for (int t = 1; t < kMaxConv; ++t) k += q >= q0[t] ? 1 : 0;
+    const ConvSeg sg = cb.seg[k];
+    const size_t i = (q - q0[k]) * 4, n = sg.n;
+    if (sg.to_bf16) {
+      const float* in = static_cast<const float*>(sg.in);
+      bf16_t* out = static_cast<bf16_t*>(sg.out);
+      if (i + 4 <= n && (((uintptr_t)(in + i) & 15) | ((uintptr_t)(out + i) & 7)) == 0)
+        st4<false>(out + i, *reinterpret_cast<const float4*>(in + i));
+      else
+        for (size_t e = i; e < n && e < i + 4; ++e) out[e] = f2bf(in[e]);
+    } else {
+      const bf16_t* in = static_cast<const bf16_t*>(sg.in);
+      float* out = static_cast<float*>(sg.out);
+      if (i + 4 <= n && (((uintptr_t)(in + i) & 7) | ((uintptr_t)(out + i) & 15)) == 0)
+        *reinterpret_cast<float4*>(out + i) = ld4(in + i);
+      else
+        for (size_t e = i; e < n && e < i + 4; ++e) out[e] = bf2f(in[e]);
+    }
+  }
+}
+hipError_t launch_convert_multi(const ConvBatch& cb, hipStream_t s) {
+  size_t quads = 0;
+  for (int k = 0; k < cb.n; ++k) quads += (cb.seg[k].n + 3) / 4;
+  if (quads == 0) return hipGetLastError();
+  hipLaunchKernelGGL(convert_multi_kernel, dim3(grid_for(quads * 4, 4)), dim3(256), 0, s, cb);
+  return hipGetLastError();
 }
 
 hipError_t launch_bf16_to_f32(const bf16_t* in, float* out, size_t n, hipStream_t s) {
