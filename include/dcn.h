@@ -315,7 +315,9 @@ int dcn_set_fwd_path(dcn_handle* h, int path);
  *  13  1: fp32 NCHW -> NHWC transposes (x -> xT, ∂out -> ∂outT + ∂b) with 4-byte accesses
  *        instead of the 16-byte form
  *  14  1: bf16 K1 with 4 channels per lane instead of 8
- * Slots 0 and 15 are unused. */
+ *  15  1: fp32 ∂W_off (3x3, J = 18) on the 4-M-tile kernel (12 N-tiles, padding included)
+ *      instead of one M-tile per wave over 10 N-tiles + 2 VALU columns
+ * Slot 0 is unused. */
 
 /* ---- testing ------------------------------------------------------------------ */
 /* One fp32 GEMM through the handle's engine under its current math mode, BLAS

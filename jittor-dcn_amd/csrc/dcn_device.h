@@ -208,6 +208,20 @@ __device__ __forceinline__ void mfma16x4_acc(f32x4& c0, f32x4& c1, f32x4& c2, f3
       : "+a"(c0), "+a"(c1), "+a"(c2), "+a"(c3)
       : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(b));
 }
+// Five 16x16x4 f32 MFMAs sharing the A operand (one M-tile against five N-tiles).
+__device__ __forceinline__ void mfma16x4_a5(f32x4& c0, f32x4& c1, f32x4& c2, f32x4& c3, f32x4& c4,
+                                            float a, float b0, float b1, float b2, float b3,
+                                            float b4) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_mfma_f32_16x16x4_f32 %0, %5, %6, %0\n\t"
+      "v_mfma_f32_16x16x4_f32 %1, %5, %7, %1\n\t"
+      "v_mfma_f32_16x16x4_f32 %2, %5, %8, %2\n\t"
+      "v_mfma_f32_16x16x4_f32 %3, %5, %9, %3\n\t"
+      "v_mfma_f32_16x16x4_f32 %4, %5, %10, %4"
+      : "+a"(c0), "+a"(c1), "+a"(c2), "+a"(c3), "+a"(c4)
+      : "v"(a), "v"(b0), "v"(b1), "v"(b2), "v"(b3), "v"(b4));
+}
 // 12 wait states (8-pass XDL) between the last asm MFMA and any other access to its D.
 __device__ __forceinline__ void mfma_drain(f32x4& c0, f32x4& c1, f32x4& c2, f32x4& c3) {
   asm volatile("s_nop 11" : "+a"(c0), "+a"(c1), "+a"(c2), "+a"(c3));

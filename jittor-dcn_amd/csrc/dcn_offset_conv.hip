@@ -658,6 +658,93 @@ __global__ __launch_bounds__(256) void offset_wgrad_mfma(Geo g, const XT* __rest
   }
 }
 
+// ∂W_off partials with one M-tile (16 channels) per wave over every N-tile: TJ = 160 + NV tap
+// columns (3x3, J = 18: NV = 2) as 10 N-tiles of 16 on the f32 MFMA plus the last NV <= 2
+// columns on the VALU, so the 4 waves carry equal MFMA work and none multiplies padding
+// (offset_wgrad_mfma<3>: 4 M-tiles per wave over 3 of 12 N-tiles = 192 tap columns, 30 of
+// them padding, wave 3 lighter). Lane (n = l&15, q = l>>4): A = xT[pixel 4ks+q][channel
+// cw+n] (fp32, W % 4 == 0, C % 64 == 0); tile T: B = ∂offset at tap column 16T+n of pixel
+// 4ks+q. part[chunk][c][tj] as offset_wgrad_mfma; the same xT register ring and the same
+// zero-operand padding steps.
+__global__ __launch_bounds__(256) void offset_wgrad_mfma_m1(Geo g, const float* __restrict__ xT,
+                                                           const float* __restrict__ goff,
+                                                           float* __restrict__ part, int rowsB,
+                                                           int cpi, int chunk0) {
+  extern __shared__ float S[];
+  const int chunk = chunk0 + blockIdx.x;
+  const int b = chunk / cpi, y0 = (chunk - b * cpi) * rowsB;
+  const int nrows = min(rowsB, g.H - y0);
+  const int SW = g.W + (g.kw - 1) * g.dw;
+  stage_goff(g, goff, b, y0, nrows + (g.kh - 1) * g.dh, SW, S);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n = lane & 15, q = lane >> 4;
+  const int TJ = g.J * g.kh * g.kw, NV = TJ - 160;
+  int bv0[10], vv0[2];
+#pragma unroll
+  for (int t = 0; t < 10; ++t) bv0[t] = q * g.J + g_toff(g, 16 * t + n, SW);
+#pragma unroll
+  for (int r = 0; r < 2; ++r) vv0[r] = q * g.J + g_toff(g, 160 + r, SW);  // 0 past TJ
+  const int cw = blockIdx.y * 64 + 16 * w;
+  f32x4 acc[10];
+#pragma unroll
+  for (int t = 0; t < 10; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float va[2] = {0.f, 0.f};
+  constexpr int kPf = 4;
+  const int nq = g.W / 4, nsteps = nrows * nq;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(xT + ((size_t)b * g.H + y0) * g.W * g.C), 0,
+      (int)((size_t)max(nrows, 1) * g.W * g.C * 4), 0x00020000);
+  const unsigned lane_x = (unsigned)((q * g.C + cw + n) * 4);
+  const int step_x = 16 * g.C, last = (nsteps - 1) * step_x;
+  auto ld = [&](int so) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, lane_x, so, 0));
+  };
+  float ring[kPf];
+  int lo = 0;
+#pragma unroll
+  for (int d = 0; d < kPf; ++d, lo += step_x) ring[d] = ld(min(lo, last));
+  int sb = 0, sx = 0;
+  const int row_skip = (SW - g.W) * g.J;
+  for (int ks0 = 0; ks0 < nsteps; ks0 += kPf) {
+#pragma unroll
+    for (int d = 0; d < kPf; ++d) {
+      const unsigned keep = ks0 + d < nsteps ? 0xffffffffu : 0u;  // wave-uniform
+      const float a = __uint_as_float(__float_as_uint(ring[d]) & keep);
+      float bv[10], vb[2];
+#pragma unroll
+      for (int t = 0; t < 10; ++t) bv[t] = __uint_as_float(__float_as_uint(S[sb + bv0[t]]) & keep);
+#pragma unroll
+      for (int r = 0; r < 2; ++r) vb[r] = __uint_as_float(__float_as_uint(S[sb + vv0[r]]) & keep);
+      sb += 4 * g.J;
+      if (++sx == nq) sx = 0, sb += row_skip;
+      mfma16x4_a5(acc[0], acc[1], acc[2], acc[3], acc[4], a, bv[0], bv[1], bv[2], bv[3], bv[4]);
+      mfma16x4_a5(acc[5], acc[6], acc[7], acc[8], acc[9], a, bv[5], bv[6], bv[7], bv[8], bv[9]);
+      va[0] = fmaf(a, vb[0], va[0]);
+      va[1] = fmaf(a, vb[1], va[1]);
+      ring[d] = ld(min(lo, last));
+      lo += step_x;
+    }
+  }
+  mfma_drain(acc[0], acc[1], acc[2], acc[3]);
+  mfma_drain(acc[4], acc[5], acc[6], acc[7]);
+  mfma_drain(acc[8], acc[9], acc[0], acc[1]);
+  float* pp = part + (size_t)chunk * g.C * TJ;
+  // D: row (channel cw + 4q + r), column (tap column 16t + n)
+#pragma unroll
+  for (int t = 0; t < 10; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pp[(size_t)(cw + 4 * q + r) * TJ + 16 * t + n] = acc[t][r];
+  // the VALU columns: lane (n, q) holds channel cw+n over pixels ≡ q (mod 4); fixed xor tree
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    float v = va[r];
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if (r < NV && q == 0) pp[(size_t)(cw + n) * TJ + 160 + r] = v;
+  }
+}
+
 // ∂w_off[j][c][tap] = Σ_chunk part[chunk][c][j·KK + tap], chunks in order: 64 elements per
 // 1024-thread block, wave w sums chunks ≡ w (mod 16), the 16 wave sums fold in order.
 __global__ __launch_bounds__(1024) void wgrad_mfma_reduce(Geo g, const float* __restrict__ part,
@@ -1886,6 +1973,9 @@ hipError_t launch_offset_bwd_chunk(const Geo& g, const void* xT, bool xT_bf16, c
     if (NT <= 4) w4 ? wg(offset_wgrad_mfma<1, true, bf16_t>, xb) : wg(offset_wgrad_mfma<1, false, bf16_t>, xb);
     else if (NT <= 8) w4 ? wg(offset_wgrad_mfma<2, true, bf16_t>, xb) : wg(offset_wgrad_mfma<2, false, bf16_t>, xb);
     else w4 ? wg(offset_wgrad_mfma<3, true, bf16_t>, xb) : wg(offset_wgrad_mfma<3, false, bf16_t>, xb);
+  } else if (w4 && TJ > 160 && TJ <= 162 && exp_flag(15) != 1) {
+    // (DCN_EXP slot 15 = 1: the 4-M-tile kernel with its padding N-tiles instead)
+    wg(offset_wgrad_mfma_m1, static_cast<const float*>(xT));
   } else {
     const float* xf = static_cast<const float*>(xT);
     if (NT <= 4) w4 ? wg(offset_wgrad_mfma<1, true>, xf) : wg(offset_wgrad_mfma<1, false>, xf);
