@@ -317,7 +317,7 @@ int dcn_set_fwd_path(dcn_handle* h, int path);
  *  14  1: bf16 K1 with 4 channels per lane instead of 8
  *  15  1: fp32 ∂W_off (3x3, J = 18) on the 4-M-tile kernel (12 N-tiles, padding included)
  *      instead of one M-tile per wave over 10 N-tiles + 2 VALU columns
- * Slot 0 is unused. */
+ *   0  1: fp32 ∂W_off (3x3, J = 18) with one row chunk per workgroup instead of two */
 
 /* ---- testing ------------------------------------------------------------------ */
 /* One fp32 GEMM through the handle's engine under its current math mode, BLAS

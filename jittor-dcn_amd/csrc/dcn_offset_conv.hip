@@ -462,6 +462,17 @@ static bool mfma_stage(const Geo& g, MfmaStage* m) {
   m->lds_x = (size_t)tj_pad4(g) * sizeof(int) + (size_t)m->SRx * row_bytes;
   return m->lds_x <= kMfmaLds;
 }
+// fp32 ∂W_off on offset_wgrad_mfma_m1 (3x3, J = 18; W % 4 == 0, C % 64 == 0), and how many row
+// chunks one of its workgroups sums (2: half the partials written and folded; DCN_EXP slot 0
+// = 1 keeps 1). Every other geometry: offset_wgrad_mfma, one partial per chunk.
+static bool wgrad_m1(const Geo& g) {
+  const int TJ = g.J * g.kh * g.kw;
+  return g.dt != DCN_BF16 && g.W % 4 == 0 && g.C % 64 == 0 && TJ > 160 && TJ <= 162 &&
+         exp_flag(15) != 1;
+}
+static int wgrad_cpb(const Geo& g, const MfmaStage& m) {
+  return (wgrad_m1(g) && m.cpi % 2 == 0 && exp_flag(0) != 1) ? 2 : 1;
+}
 static size_t wgrad_mfma_part_floats(const Geo& g, const MfmaStage& m) {
   return (size_t)g.B * m.cpi * g.C * g.J * g.kh * g.kw;
 }
@@ -666,17 +677,15 @@ __global__ __launch_bounds__(256) void offset_wgrad_mfma(Geo g, const XT* __rest
 // cw+n] (fp32, W % 4 == 0, C % 64 == 0); tile T: B = ∂offset at tap column 16T+n of pixel
 // 4ks+q. part[chunk][c][tj] as offset_wgrad_mfma; the same xT register ring and the same
 // zero-operand padding steps.
+// A workgroup sums cpb consecutive row chunks of one image (cpi % cpb == 0) into one partial:
+// part[grp][c][tj], grp = chunk / cpb.
 __global__ __launch_bounds__(256) void offset_wgrad_mfma_m1(Geo g, const float* __restrict__ xT,
                                                            const float* __restrict__ goff,
                                                            float* __restrict__ part, int rowsB,
-                                                           int cpi, int chunk0) {
+                                                           int cpi, int grp0, int cpb) {
   extern __shared__ float S[];
-  const int chunk = chunk0 + blockIdx.x;
-  const int b = chunk / cpi, y0 = (chunk - b * cpi) * rowsB;
-  const int nrows = min(rowsB, g.H - y0);
+  const int grp = grp0 + blockIdx.x;
   const int SW = g.W + (g.kw - 1) * g.dw;
-  stage_goff(g, goff, b, y0, nrows + (g.kh - 1) * g.dh, SW, S);
-  __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int n = lane & 15, q = lane >> 4;
   const int TJ = g.J * g.kh * g.kw, NV = TJ - 160;
@@ -690,46 +699,54 @@ __global__ __launch_bounds__(256) void offset_wgrad_mfma_m1(Geo g, const float* 
 #pragma unroll
   for (int t = 0; t < 10; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   float va[2] = {0.f, 0.f};
-  constexpr int kPf = 4;
-  const int nq = g.W / 4, nsteps = nrows * nq;
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(xT + ((size_t)b * g.H + y0) * g.W * g.C), 0,
-      (int)((size_t)max(nrows, 1) * g.W * g.C * 4), 0x00020000);
-  const unsigned lane_x = (unsigned)((q * g.C + cw + n) * 4);
-  const int step_x = 16 * g.C, last = (nsteps - 1) * step_x;
-  auto ld = [&](int so) {
-    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, lane_x, so, 0));
-  };
-  float ring[kPf];
-  int lo = 0;
+  for (int cc = 0; cc < cpb; ++cc) {
+    const int chunk = grp * cpb + cc;
+    const int b = chunk / cpi, y0 = (chunk - b * cpi) * rowsB;
+    const int nrows = min(rowsB, g.H - y0);
+    if (cc) __syncthreads();  // the previous chunk's LDS reads are done
+    stage_goff(g, goff, b, y0, nrows + (g.kh - 1) * g.dh, SW, S);
+    __syncthreads();
+    constexpr int kPf = 4;
+    const int nq = g.W / 4, nsteps = nrows * nq;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(xT + ((size_t)b * g.H + y0) * g.W * g.C), 0,
+        (int)((size_t)max(nrows, 1) * g.W * g.C * 4), 0x00020000);
+    const unsigned lane_x = (unsigned)((q * g.C + cw + n) * 4);
+    const int step_x = 16 * g.C, last = (nsteps - 1) * step_x;
+    auto ld = [&](int so) {
+      return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, lane_x, so, 0));
+    };
+    float ring[kPf];
+    int lo = 0;
 #pragma unroll
-  for (int d = 0; d < kPf; ++d, lo += step_x) ring[d] = ld(min(lo, last));
-  int sb = 0, sx = 0;
-  const int row_skip = (SW - g.W) * g.J;
-  for (int ks0 = 0; ks0 < nsteps; ks0 += kPf) {
+    for (int d = 0; d < kPf; ++d, lo += step_x) ring[d] = ld(min(lo, last));
+    int sb = 0, sx = 0;
+    const int row_skip = (SW - g.W) * g.J;
+    for (int ks0 = 0; ks0 < nsteps; ks0 += kPf) {
 #pragma unroll
-    for (int d = 0; d < kPf; ++d) {
-      const unsigned keep = ks0 + d < nsteps ? 0xffffffffu : 0u;  // wave-uniform
-      const float a = __uint_as_float(__float_as_uint(ring[d]) & keep);
-      float bv[10], vb[2];
+      for (int d = 0; d < kPf; ++d) {
+        const unsigned keep = ks0 + d < nsteps ? 0xffffffffu : 0u;  // wave-uniform
+        const float a = __uint_as_float(__float_as_uint(ring[d]) & keep);
+        float bv[10], vb[2];
 #pragma unroll
-      for (int t = 0; t < 10; ++t) bv[t] = __uint_as_float(__float_as_uint(S[sb + bv0[t]]) & keep);
+        for (int t = 0; t < 10; ++t) bv[t] = __uint_as_float(__float_as_uint(S[sb + bv0[t]]) & keep);
 #pragma unroll
-      for (int r = 0; r < 2; ++r) vb[r] = __uint_as_float(__float_as_uint(S[sb + vv0[r]]) & keep);
-      sb += 4 * g.J;
-      if (++sx == nq) sx = 0, sb += row_skip;
-      mfma16x4_a5(acc[0], acc[1], acc[2], acc[3], acc[4], a, bv[0], bv[1], bv[2], bv[3], bv[4]);
-      mfma16x4_a5(acc[5], acc[6], acc[7], acc[8], acc[9], a, bv[5], bv[6], bv[7], bv[8], bv[9]);
-      va[0] = fmaf(a, vb[0], va[0]);
-      va[1] = fmaf(a, vb[1], va[1]);
-      ring[d] = ld(min(lo, last));
-      lo += step_x;
+        for (int r = 0; r < 2; ++r) vb[r] = __uint_as_float(__float_as_uint(S[sb + vv0[r]]) & keep);
+        sb += 4 * g.J;
+        if (++sx == nq) sx = 0, sb += row_skip;
+        mfma16x4_a5(acc[0], acc[1], acc[2], acc[3], acc[4], a, bv[0], bv[1], bv[2], bv[3], bv[4]);
+        mfma16x4_a5(acc[5], acc[6], acc[7], acc[8], acc[9], a, bv[5], bv[6], bv[7], bv[8], bv[9]);
+        va[0] = fmaf(a, vb[0], va[0]);
+        va[1] = fmaf(a, vb[1], va[1]);
+        ring[d] = ld(min(lo, last));
+        lo += step_x;
+      }
     }
-  }
+  }  // chunks
   mfma_drain(acc[0], acc[1], acc[2], acc[3]);
   mfma_drain(acc[4], acc[5], acc[6], acc[7]);
   mfma_drain(acc[8], acc[9], acc[0], acc[1]);
-  float* pp = part + (size_t)chunk * g.C * TJ;
+  float* pp = part + (size_t)grp * g.C * TJ;
   // D: row (channel cw + 4q + r), column (tap column 16t + n)
 #pragma unroll
   for (int t = 0; t < 10; ++t)
@@ -1973,9 +1990,12 @@ hipError_t launch_offset_bwd_chunk(const Geo& g, const void* xT, bool xT_bf16, c
     if (NT <= 4) w4 ? wg(offset_wgrad_mfma<1, true, bf16_t>, xb) : wg(offset_wgrad_mfma<1, false, bf16_t>, xb);
     else if (NT <= 8) w4 ? wg(offset_wgrad_mfma<2, true, bf16_t>, xb) : wg(offset_wgrad_mfma<2, false, bf16_t>, xb);
     else w4 ? wg(offset_wgrad_mfma<3, true, bf16_t>, xb) : wg(offset_wgrad_mfma<3, false, bf16_t>, xb);
-  } else if (w4 && TJ > 160 && TJ <= 162 && exp_flag(15) != 1) {
+  } else if (wgrad_m1(g)) {
     // (DCN_EXP slot 15 = 1: the 4-M-tile kernel with its padding N-tiles instead)
-    wg(offset_wgrad_mfma_m1, static_cast<const float*>(xT));
+    const int cpb = wgrad_cpb(g, ms);
+    hipLaunchKernelGGL(offset_wgrad_mfma_m1, dim3(nb * ms.cpi / cpb, g.C / 64), dim3(256),
+                       ms.lds_w, s, g, static_cast<const float*>(xT), goff, goffT, ms.rowsB,
+                       ms.cpi, b0 * ms.cpi / cpb, cpb);
   } else {
     const float* xf = static_cast<const float*>(xT);
     if (NT <= 4) w4 ? wg(offset_wgrad_mfma<1, true>, xf) : wg(offset_wgrad_mfma<1, false>, xf);
@@ -1993,7 +2013,7 @@ hipError_t launch_offset_bwd_finish(const Geo& g, const float* goff, const float
   if (!mfma_stage(g, &ms)) return hipErrorInvalidValue;
   const long E = (long)g.C * g.J * g.kh * g.kw;
   hipLaunchKernelGGL(wgrad_mfma_reduce, dim3((unsigned)((E + 63) / 64)), dim3(1024), 0, s, g,
-                     goffT, g.B * ms.cpi, gw_off);
+                     goffT, g.B * ms.cpi / wgrad_cpb(g, ms), gw_off);
   if (gb_off) launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
   return hipGetLastError();
 }
