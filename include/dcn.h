@@ -253,12 +253,17 @@ int dcn_allreduce_grads(dcn_handle* h, dcn_comm* c, void* grads, size_t count, i
  * overlapped with the ∂columns GEMM, col2im and the offset-conv backward; grad_w_off and
  * grad_b_off are all-reduced at the end; the handle's stream waits for both before any
  * later work. For DCN_BF16 the sums run over the fp32 working copies (one bf16 rounding
- * of the summed value). Every rank must run the same sequence of dcn_backward calls. */
+ * of the summed value). Every rank must run the same sequence of dcn_backward calls.
+ * Lifetime: the communicator remembers the handles attached to it; dcn_comm_destroy waits
+ * for their in-flight exchanges and detaches them, and dcn_destroy detaches its handle, so
+ * either may be destroyed first. */
 int dcn_set_comm(dcn_handle* h, dcn_comm* c);
 /* For callers with their own collectives (e.g. torch.distributed): when `hip_stream` is not
  * NULL, each later dcn_backward makes that stream wait (hipStreamWaitEvent) until grad_w
  * and grad_b are final, before the ∂columns GEMM even starts, so a collective enqueued on
- * it right after dcn_backward returns overlaps the rest of the backward. NULL disables. */
+ * it right after dcn_backward returns overlaps the rest of the backward. NULL disables.
+ * Lifetime: the library keeps the raw stream; the caller detaches it (NULL) before
+ * destroying that stream. */
 int dcn_set_grad_stream(dcn_handle* h, void* hip_stream);
 
 /* ---- GEMM arithmetic ------------------------------------------------------------ */
@@ -291,33 +296,11 @@ typedef enum { DCN_FWD_AUTO = 0, DCN_FWD_UNFUSED = 1, DCN_FWD_FUSED = 2 } dcn_fw
 int dcn_set_fwd_path(dcn_handle* h, int path);
 
 /* ---- development A/B knobs ------------------------------------------------------ *
- * Env DCN_EXP="v0,v1,..." (read once per process; unset = all 0 = the measured defaults)
- * switches between implementations of the same math for speed experiments; results agree
- * to fp32 rounding (only summation orders change). Each alternative is measured in
- * DESIGN.md §4. Slots:
- *   1  1: fp32 ∂b_off as one 1024-thread block per offset channel instead of the
- *        two-level (channel, image) sum
- *   2  1: fp32 K5 as two kernels (offgrad_cl + dx_gather_cl) instead of col2im_tile
- *   4  1: offset conv forward on the per-pixel VALU kernel instead of the 2-px row kernel
- *   3  1: fp32 offset conv forward on the VALU kernel with the x transpose beside it
- *        instead of the f32-MFMA kernel that writes xT itself; 2 / 3: that kernel with
- *        2 rows x 2 pixel tiles per wave / 4 rows per workgroup
- *   5  1 / 2: split-bf16 GEMM form EARLY / LATE (default: picked per shape)
- *   6  1: offset conv backward on the VALU kernels instead of the MFMA ones
- *   7  n > 0: output rows per wave of the VALU ∂w_off kernel (default 4)
- *   8  1: fused forward workgroup shape 0 (4 waves x 2 per CU) instead of shape 1
- *   9  n > 0: bf16/fp32 ∂W as n grouped GEMMs; n < 0: one GEMM per image
- *  10  1: bf16 offset conv forward on the register-direct MFMA kernel instead of the
- *        LDS-windowed row kernel
- *  11  n > 0: bf16 ∂W_off kernel sums n row chunks per workgroup (default 2)
- *  12  1: K5 on 4-row input tiles (5 waves) instead of 7-row tiles (8 waves);
- *      2: bf16 K5 with 2 ∂col rows in flight per wave instead of 3
- *  13  1: fp32 NCHW -> NHWC transposes (x -> xT, ∂out -> ∂outT + ∂b) with 4-byte accesses
- *        instead of the 16-byte form
- *  14  1: bf16 K1 with 4 channels per lane instead of 8
- *  15  1: fp32 ∂W_off (3x3, J = 18) on the 4-M-tile kernel (12 N-tiles, padding included)
- *      instead of one M-tile per wave over 10 N-tiles + 2 VALU columns
- *   0  1: fp32 ∂W_off (3x3, J = 18) with one row chunk per workgroup instead of two */
+ * Env DCN_EXP="v0,v1,..." (read once per process) is the hook for speed experiments
+ * during development: a candidate kernel is put behind exp_flag(i), A/B-measured against
+ * the default, and then either made the default or deleted. No slot selects anything in
+ * this build: every alternative measured slower was removed (DESIGN.md §4 keeps the
+ * measurements), so the shipped path is the one the parity tests run. */
 
 /* ---- testing ------------------------------------------------------------------ */
 /* One fp32 GEMM through the handle's engine under its current math mode, BLAS

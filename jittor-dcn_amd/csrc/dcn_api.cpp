@@ -137,8 +137,13 @@ WsLayout ws_layout(const Geo& g, bool bwd) {
     // DCN_BF16 forward copies, at the same offsets in the forward-only and the
     // forward+backward layouts: a backward with DCN_BWD_COL_IN_WS reads what the forward
     // (which always uses the forward-only layout) wrote
-    L.x32 = take((size_t)g.B * g.C * g.HWi * f);
-    L.xT32 = take((size_t)g.B * g.C * g.HWi * f);  // fp32 channels-last x (VALU fallbacks)
+    // fp32 copies of x only for the fallback offset-conv kernels (the MFMA paths read the
+    // bf16 x / xT directly): NCHW when either direction falls back, channels-last for the
+    // VALU backward. Depends on the geometry alone, so both layouts agree.
+    const bool fb_fwd = !dcn::offset_fwd_mfma_bf16_ok(g), fb_bwd = !dcn::offset_bwd_bf16_ok(g);
+    const size_t xb = (size_t)g.B * g.C * g.HWi * f;
+    L.x32 = take(fb_fwd || fb_bwd ? xb : 0);
+    L.xT32 = take(fb_bwd ? xb : 0);
     L.wb16 = take(std::max(dcn::offset_fwd_bf16_wb_elems(g), dcn::offset_bwd_bf16_wc_elems(g)) *
                   sizeof(dcn::bf16_t));
     L.woff32 = take((size_t)g.J * g.C * g.N * f);
@@ -158,7 +163,8 @@ WsLayout ws_layout(const Geo& g, bool bwd) {
     L.bins = take(dcn::bins_ws_bytes(g, g.B));
   }
   if (g.dt == DCN_BF16 && bwd) {
-    L.gx32 = take((size_t)g.B * g.C * g.HWi * f);
+    // fp32 ∂x only where the offset-conv backward does not write the bf16 ∂x itself
+    L.gx32 = take(dcn::offset_bwd_bf16_ok(g) ? 0 : (size_t)g.B * g.C * g.HWi * f);
     L.gw32 = take((size_t)g.O * g.K * f);
     L.gb32 = take((size_t)g.O * f);
     L.gwo32 = take((size_t)g.J * g.C * g.N * f);
@@ -267,6 +273,11 @@ int join_aux(dcn_handle* h) {
   return DCN_OK;
 }
 
+extern "C" __attribute__((visibility("hidden"))) void dcn_internal_handle_drop_comm(dcn_handle* h);
+extern "C" __attribute__((visibility("hidden"))) void dcn_internal_comm_attach(dcn_comm* c,
+                                                                             dcn_handle* h);
+extern "C" __attribute__((visibility("hidden"))) void dcn_internal_comm_detach(dcn_comm* c,
+                                                                             dcn_handle* h);
 extern "C" __attribute__((visibility("hidden"))) int dcn_internal_allreduce_n(
     dcn_comm* c, int n, void* const* bufs, const size_t* counts, int dtype, void* st);
 
@@ -366,12 +377,8 @@ int core_forward(dcn_handle* h, const Geo& g, const float* x, const float* off, 
 // The offset-conv backward, when core_backward runs it interleaved with col2im.
 // ∂W as dwg grouped NT GEMMs over B/dwg images each, or one NN GEMM per image (0). r01
 // (tools/dw_ab.sh): bf16 config 4 ∂W 0.178 ms per image -> 0.130 ms in 16 groups (step 1.10 ->
-// 1.02 ms); fp32 config 3 unchanged at 1.65 ms, so fp32 stays per image. DCN_EXP slot 9
-// overrides: n > 0 groups, n < 0 per image.
+// 1.02 ms); fp32 config 3 unchanged at 1.65 ms, so fp32 stays per image.
 int dw_groups(const Geo& g) {
-  const int n = dcn::exp_flag(9);
-  if (n < 0) return 0;
-  if (n > 0) return (n < g.B && g.B % n == 0) ? n : 0;
   return (g.dt == DCN_BF16 && g.B > 16 && g.B % 16 == 0) ? 16 : 0;
 }
 
@@ -736,6 +743,7 @@ int dcn_destroy(dcn_handle* h) {
   if (!h) return DCN_OK;
   (void)hipSetDevice(h->device);
   (void)hipStreamSynchronize(h->stream);
+  if (h->comm) dcn_internal_handle_drop_comm(h);
   for (auto& v : h->ev)
     for (hipEvent_t e : v) (void)hipEventDestroy(e);
   if (h->ws) (void)hipFree(h->ws);
@@ -976,11 +984,8 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
     // ∂b_off = Σ ∂offset (18 channels: a latency-bound reduction) on the side stream, beside
     // the offset-conv ∂W / ∂x kernels
     DCN_TRY(fork_aux(h));
-    // (two-level over (channel, image) blocks; DCN_EXP slot 1 = 1: one block per channel)
-    if (dcn::exp_flag(1) == 1)
-      dcn::launch_channel_sum(goff, g.B, g.J, g.HW, grad_b_off, h->aux);
-    else
-      dcn::launch_channel_sum_2l(goff, g.B, g.J, g.HW, F(L.part), grad_b_off, h->aux);
+    // two-level over (channel, image) blocks (one block per channel held 18 CUs for 0.11 ms)
+    dcn::launch_channel_sum_2l(goff, g.B, g.J, g.HW, F(L.part), grad_b_off, h->aux);
     HIP_TRY(dcn::launch_offset_conv_bwd(g, x, F(L.xT), w_off, goff, F(L.goffT), F(L.wt), grad_x,
                                         grad_w_off, nullptr,
                                         dcn::get_force_generic() ? nullptr : F(L.gxT), h->stream));
@@ -1351,6 +1356,15 @@ int dcn_prof_reset(dcn_handle* h) {
 }
 
 // Internal hooks for dcn_comm.cpp (not in dcn.h).
+// Detach the handle's communicator after its last exchange has finished (dcn_comm_destroy,
+// dcn_destroy): the stream the exchange runs on is drained first.
+__attribute__((visibility("hidden"))) void dcn_internal_handle_drop_comm(dcn_handle* h) {
+  if (!h || !h->comm) return;
+  (void)hipSetDevice(h->device);
+  if (h->comm_stream) (void)hipStreamSynchronize(h->comm_stream);
+  dcn_internal_comm_detach(h->comm, h);
+  h->comm = nullptr;
+}
 __attribute__((visibility("hidden"))) int dcn_internal_fail(int code, const char* msg) {
   return fail(code, msg);
 }
@@ -1383,8 +1397,12 @@ int dcn_set_math(dcn_handle* h, int math) {
 
 int dcn_set_comm(dcn_handle* h, dcn_comm* c) {
   DCN_TRY(set_device(h));
-  if (h->comm && h->comm != c) HIP_TRY(hipStreamSynchronize(h->comm_stream));
+  if (h->comm && h->comm != c) {
+    HIP_TRY(hipStreamSynchronize(h->comm_stream));
+    dcn_internal_comm_detach(h->comm, h);
+  }
   h->comm = c;
+  dcn_internal_comm_attach(c, h);
   return DCN_OK;
 }
 

@@ -10,8 +10,10 @@
 // holds an RCCL (e.g. torch's) reuses that copy instead of loading a second one.
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "dcn_internal.h"
 
@@ -96,7 +98,22 @@ int rccl_fail(Rccl* r, const char* what, int rc) {
 struct dcn_comm {
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = 0;
+  // handles this communicator is attached to (dcn_set_comm): dcn_comm_destroy detaches
+  // them first, so no handle keeps a dangling pointer or races an in-flight exchange
+  std::vector<dcn_handle*> users;
 };
+
+extern "C" __attribute__((visibility("hidden"))) void dcn_internal_handle_drop_comm(dcn_handle* h);
+
+extern "C" __attribute__((visibility("hidden"))) void dcn_internal_comm_attach(dcn_comm* c,
+                                                                             dcn_handle* h) {
+  if (c && std::find(c->users.begin(), c->users.end(), h) == c->users.end())
+    c->users.push_back(h);
+}
+extern "C" __attribute__((visibility("hidden"))) void dcn_internal_comm_detach(dcn_comm* c,
+                                                                             dcn_handle* h) {
+  if (c) c->users.erase(std::remove(c->users.begin(), c->users.end(), h), c->users.end());
+}
 
 extern "C" {
 
@@ -139,6 +156,8 @@ int dcn_comm_init(dcn_handle* h, int nranks, int rank, const void* id, dcn_comm*
 
 int dcn_comm_destroy(dcn_comm* c) {
   if (!c) return DCN_OK;
+  // waits for each attached handle's exchange stream, then clears its pointer
+  while (!c->users.empty()) dcn_internal_handle_drop_comm(c->users.back());
   std::string err;
   Rccl* r = rccl(&err);
   if (r && c->comm) r->destroy(c->comm);

@@ -308,22 +308,17 @@ hipError_t launch_fused_fwd(const Geo& g, const float* xT, const float* off, con
   const int nblk = (int)((P + kFBlk - 1) / kFBlk);
   const int OT = g.O % 256 == 0 ? 256 : 128;
   const int tiles_o = g.O / OT;
-  // shape 1 measured faster at config 3 (2.49 against 2.91 ms); DCN_EXP slot 8 = 1 picks 0
-  const int cfg = exp_flag(8) == 1 ? 0 : 1;
-  const int wgcu = cfg == 0 ? FCfg<0>::WGCU : FCfg<1>::WGCU;
-  const int want = g_fused_wg > 0 ? g_fused_wg : std::max(1, wgcu * cus / tiles_o);
+  // shape 1 (FCfg<1>) measured faster at config 3: 2.49 against 2.91 ms for shape 0
+  constexpr int cfg = 1;
+  const int want = g_fused_wg > 0 ? g_fused_wg : std::max(1, FCfg<cfg>::WGCU * cus / tiles_o);
   const dim3 grid(std::max(1, std::min(nblk, want)), tiles_o);
-#define DCN_FUSED_LAUNCH(OT_, CFG_)                                                          \
-  hipLaunchKernelGGL((fwd_fused<OT_, CFG_>), grid, dim3(FCfg<CFG_>::T), 0, s, g, xT, off, Wf, \
+#define DCN_FUSED_LAUNCH(OT_)                                                                \
+  hipLaunchKernelGGL((fwd_fused<OT_, cfg>), grid, dim3(FCfg<cfg>::T), 0, s, g, xT, off, Wf,   \
                      bias, out, colT, nblk)
-  if (OT == 256 && cfg == 0)
-    DCN_FUSED_LAUNCH(256, 0);
-  else if (OT == 256)
-    DCN_FUSED_LAUNCH(256, 1);
-  else if (cfg == 0)
-    DCN_FUSED_LAUNCH(128, 0);
+  if (OT == 256)
+    DCN_FUSED_LAUNCH(256);
   else
-    DCN_FUSED_LAUNCH(128, 1);
+    DCN_FUSED_LAUNCH(128);
 #undef DCN_FUSED_LAUNCH
   return hipGetLastError();
 }

@@ -350,9 +350,7 @@ hipError_t launch_gemm_split(int math, const GemmSpec& s, const float* A, const 
   const double a_el = (double)s.m * s.k * (s.sa ? s.batch : 1);
   const double b_el = (double)s.n * s.k * (s.sb ? s.batch : 1);
   a.n_fast = a_el >= b_el;
-  // form: 0 EARLY, 1 LATE (A/B knob DCN_EXP slot 5 = form + 1)
-  const int knob = exp_flag(5);
-  if (knob == 1 || knob == 2) form = knob - 1;
+  // form: 0 EARLY, 1 LATE (picked per shape by the caller)
   const bool a_kc = s.ta, b_kc = !s.tb;
   switch (math) {
     case 3: return launch_p<3>(a, a_kc, b_kc, form, st);

@@ -134,8 +134,14 @@ struct ConvSeg {
 struct ConvBatch {
   ConvSeg seg[kMaxConv];
   int n = 0;
+  bool overflow = false;  // more than kMaxConv segments: launch_convert_multi refuses the batch
   void add(const void* in, void* out, size_t count, bool to_bf16) {
-    if (count && n < kMaxConv) seg[n++] = ConvSeg{in, out, count, to_bf16 ? 1 : 0};
+    if (!count) return;
+    if (n == kMaxConv) {
+      overflow = true;
+      return;
+    }
+    seg[n++] = ConvSeg{in, out, count, to_bf16 ? 1 : 0};
   }
 };
 hipError_t launch_convert_multi(const ConvBatch& cb, hipStream_t s);

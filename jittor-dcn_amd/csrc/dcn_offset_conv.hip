@@ -200,7 +200,7 @@ struct WgradGrid {
   unsigned nbx, ny, nz;
   int cper;  // channels per wave (64 lanes x VEC)
 };
-static int wgrad_rpw() { return exp_flag(7) ? exp_flag(7) : kWgradRpw; }
+static int wgrad_rpw() { return kWgradRpw; }
 static WgradGrid wgrad_grid(const Geo& g, int rpw) {
   const long waves = ((long)g.B * g.Ho + rpw - 1) / rpw;
   WgradGrid w;
@@ -463,15 +463,15 @@ static bool mfma_stage(const Geo& g, MfmaStage* m) {
   return m->lds_x <= kMfmaLds;
 }
 // fp32 ∂W_off on offset_wgrad_mfma_m1 (3x3, J = 18; W % 4 == 0, C % 64 == 0), and how many row
-// chunks one of its workgroups sums (2: half the partials written and folded; DCN_EXP slot 0
-// = 1 keeps 1). Every other geometry: offset_wgrad_mfma, one partial per chunk.
+// chunks one of its workgroups sums (2: half the partials written and folded; one per
+// workgroup measured 0.449 against 0.435 ms). Every other geometry:
+// offset_wgrad_mfma, one partial per chunk.
 static bool wgrad_m1(const Geo& g) {
   const int TJ = g.J * g.kh * g.kw;
-  return g.dt != DCN_BF16 && g.W % 4 == 0 && g.C % 64 == 0 && TJ > 160 && TJ <= 162 &&
-         exp_flag(15) != 1;
+  return g.dt != DCN_BF16 && g.W % 4 == 0 && g.C % 64 == 0 && TJ > 160 && TJ <= 162;
 }
 static int wgrad_cpb(const Geo& g, const MfmaStage& m) {
-  return (wgrad_m1(g) && m.cpi % 2 == 0 && exp_flag(0) != 1) ? 2 : 1;
+  return (wgrad_m1(g) && m.cpi % 2 == 0) ? 2 : 1;
 }
 static size_t wgrad_mfma_part_floats(const Geo& g, const MfmaStage& m) {
   return (size_t)g.B * m.cpi * g.C * g.J * g.kh * g.kw;
@@ -1147,7 +1147,7 @@ hipError_t launch_offset_conv_fwd_bf16(const Geo& g, const bf16_t* xT, const bf1
                      g.C, Cp, KK);
   const int tiles = (g.HW + 31) / 32, spt = Cp / 64;  // 16-channel steps per tap and wave
   int SWc = 0;
-  const size_t lds = exp_flag(10) ? 0 : fwd_bf16_row_lds(g, &SWc);
+  const size_t lds = fwd_bf16_row_lds(g, &SWc);
   if (lds) {
     const int tpr = (g.Wo + 31) / 32;
     dim3 grid(tpr * g.Ho, 1, g.B);
@@ -1581,7 +1581,7 @@ hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16
   size_t lds_w, lds_x;
   bwd_bf16_lds(g, ms, &lds_w, &lds_x);
   // chunks per workgroup (config 4: 1 -> 48 + 11 us, 2 -> 42 + 7, 4 -> 53 + 6 for ∂W_off + fold)
-  const int cpb = exp_flag(11) > 0 ? exp_flag(11) : 2;
+  const int cpb = 2;
   const int nblk = (g.B * ms.cpi + cpb - 1) / cpb;
   hipLaunchKernelGGL(offset_wgrad_bf16, dim3(nblk, g.C / 64), dim3(256), lds_w, s, g, x, goff,
                      part, ms.rowsB, ms.cpi, cpb);
@@ -1877,8 +1877,7 @@ offset_conv_fwd_mfma_xt(Geo g, const float* __restrict__ x, const float* __restr
 bool offset_fwd_mfma_xt_ok(const Geo& g) {
   return g.dt == DCN_F32 && g.kh == 3 && g.kw == 3 && g.sh == 1 && g.sw == 1 && g.dh == 1 &&
          g.dw == 1 && g.ph == 1 && g.pw == 1 && g.Ho == g.H && g.Wo == g.W &&
-         g.W + 2 <= kXtRWmax && g.W % 4 == 0 && g.C % 16 == 0 && g.J >= 1 && g.J <= 18 &&
-         exp_flag(3) != 1;
+         g.W + 2 <= kXtRWmax && g.W % 4 == 0 && g.C % 16 == 0 && g.J >= 1 && g.J <= 18;
 }
 
 // off and xT (channels-last x) from x in one pass; wf: offset_conv_wt_floats(g) scratch
@@ -1893,10 +1892,7 @@ hipError_t launch_offset_conv_fwd_xt(const Geo& g, const float* x, const float* 
       hipLaunchKernelGGL(kern, dim3((g.H + rows - 1) / rows, 1, g.B), dim3(nt), 0, s, g, x, wf,
                          b_off, off, xT);
     };
-    const int e = exp_flag(3);
-    if (e == 2) go(offset_conv_fwd_mfma_xt<2, 2>, 2, 256);
-    else if (e == 3) go(offset_conv_fwd_mfma_xt<4, 2>, 4, 512);
-    else go(offset_conv_fwd_mfma_xt<2, 1>, 2, 512);
+    go(offset_conv_fwd_mfma_xt<2, 1>, 2, 512);
   }
   return hipGetLastError();
 }
@@ -1928,7 +1924,7 @@ hipError_t launch_offset_conv_fwd(const Geo& g, const float* x, const float* w_o
   const int n = pad_j(g.J) * g.C * KK;
   hipLaunchKernelGGL(woff_to_ctj, dim3((n + 255) / 256), dim3(256), 0, s, w_off, wt, g.J,
                      pad_j(g.J), g.C, KK);
-  if (g.sw == 1 && g.dw == 1 && g.kh == 3 && g.kw == 3 && !exp_flag(4)) {
+  if (g.sw == 1 && g.dw == 1 && g.kh == 3 && g.kw == 3) {
     auto go = [&](auto kern, int npx) {
       const int gpr = (g.Wo + npx - 1) / npx;
       const long T = (long)g.B * g.Ho * gpr;
@@ -1959,7 +1955,7 @@ bool offset_bwd_chunkable(const Geo& g) {
   MfmaStage ms;
   const int KK = g.kh * g.kw;
   return (KK == 1 || KK == 4 || KK == 6 || KK == 9) && mfma_stage(g, &ms) &&
-         !get_force_generic() && !exp_flag(6);
+         !get_force_generic();
 }
 
 hipError_t launch_offset_bwd_prep(const Geo& g, const float* w_off, float* wt2, hipStream_t s) {
@@ -1991,7 +1987,6 @@ hipError_t launch_offset_bwd_chunk(const Geo& g, const void* xT, bool xT_bf16, c
     else if (NT <= 8) w4 ? wg(offset_wgrad_mfma<2, true, bf16_t>, xb) : wg(offset_wgrad_mfma<2, false, bf16_t>, xb);
     else w4 ? wg(offset_wgrad_mfma<3, true, bf16_t>, xb) : wg(offset_wgrad_mfma<3, false, bf16_t>, xb);
   } else if (wgrad_m1(g)) {
-    // (DCN_EXP slot 15 = 1: the 4-M-tile kernel with its padding N-tiles instead)
     const int cpb = wgrad_cpb(g, ms);
     hipLaunchKernelGGL(offset_wgrad_mfma_m1, dim3(nb * ms.cpi / cpb, g.C / 64), dim3(256),
                        ms.lds_w, s, g, static_cast<const float*>(xT), goff, goffT, ms.rowsB,

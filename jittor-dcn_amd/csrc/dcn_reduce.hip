@@ -292,6 +292,7 @@ __global__ __launch_bounds__(256) void convert_multi_kernel(ConvBatch cb) {
   }
 }
 hipError_t launch_convert_multi(const ConvBatch& cb, hipStream_t s) {
+  if (cb.overflow) return hipErrorInvalidValue;  // a dropped conversion would be a silent bug
   size_t quads = 0;
   for (int k = 0; k < cb.n; ++k) quads += (cb.seg[k].n + 3) / 4;
   if (quads == 0) return hipGetLastError();
@@ -455,7 +456,7 @@ __global__ __launch_bounds__(64) void tile_sum_to_channels(const float* __restri
 
 // the plain fp32 NCHW -> NHWC transpose in the 16-byte form; false when it does not apply
 bool launch_xpose_f4(const float* in, float* out, int B, int C, int P, hipStream_t s) {
-  if (!xpose_f4_ok(in, out, C, P) || exp_flag(13)) return false;
+  if (!xpose_f4_ok(in, out, C, P)) return false;
   dim3 grid(xpose_blocks_x(P), C / 64, B);
   hipLaunchKernelGGL(xpose_f4<false>, grid, dim3(256), 0, s, in, out, nullptr, C, P);
   return true;
@@ -467,7 +468,7 @@ hipError_t launch_xpose_chsum(const float* in, float* out, float* tsum, float* c
                               int C, int P, hipStream_t s, hipStream_t s_sum,
                               hipEvent_t ev) {
   dim3 grid(xpose_blocks_x(P), (C + 63) / 64, B);
-  if (xpose_f4_ok(in, out, C, P) && !exp_flag(13))
+  if (xpose_f4_ok(in, out, C, P))
     hipLaunchKernelGGL(xpose_f4<true>, grid, dim3(256), 0, s, in, out, tsum, C, P);
   else
     hipLaunchKernelGGL(xpose_chsum, grid, dim3(256), 0, s, in, out, tsum, C, P);

@@ -1156,7 +1156,7 @@ hipError_t launch_im2col(const Geo& g, const float* x, const float* xT, const fl
 }
 
 static bool k5_fused(const Geo& g) {
-  return g.G == 1 && g.C % 4 == 0 && g.C <= 256 && (g.dt == DCN_BF16 || exp_flag(2) == 0);
+  return g.G == 1 && g.C % 4 == 0 && g.C <= 256;
 }
 
 // Pointers into the bins workspace (bins_ws_bytes layout).
@@ -1242,22 +1242,16 @@ static void launch_k5_fused(const Geo& g, const XT* xT, const BinsWs& P, const G
   // rows measured slower (r02, config 4: 0.192 against 0.187 ms; 95 VGPRs, 5 waves/SIMD)
   // bf16 rows stay raw (8 B per lane) until consumed, so 3 rows in flight fit the 6-waves-per-
   // SIMD budget (80 VGPRs): config 4 0.189 (U = 2, converted at load) -> 0.162 (U = 2 raw) ->
-  // 0.154 ms (U = 3 raw); U = 4 spills at 6 waves and runs 0.178 at 5. DCN_EXP slot 12 = 2
-  // keeps U = 2. fp32 rows (16 B per lane) with U = 3 spill 32 B at 6 waves: 0.67 -> 0.88 ms.
+  // 0.154 ms (U = 3 raw); U = 4 spills at 6 waves and runs 0.178 at 5. fp32 rows (16 B per lane) with U = 3 spill 32 B at 6 waves: 0.67 -> 0.88 ms.
   // Tile rows (kTR; kTR + 1 waves per workgroup): 4 -> 7 (r02) cuts the bin rows read twice
   // (a tile re-reads the bin row it shares with the tile below: 5/4 -> 8/7 of the ∂col rows)
   // at the same 24 waves per CU (3 workgroups of 8, 40 KB of window each). Config 3 fp32 /
   // config 4 bf16: kTR 4 0.667 / 0.152 ms, 5 0.651 / 0.163, 6 0.630 / 0.151, 7 0.568 / 0.129,
-  // 8 (2 workgroups per CU) 0.658 / 0.167, 11 0.585 / 0.137. DCN_EXP slot 12 = 1 keeps kTR 4.
-  const int e = exp_flag(12);
-  if constexpr (sizeof(GT) == 2) {
-    if (e == 1) return launch_c2i<3, 4, 6, 4>(g, xT, P, gcolT, gxT, goff, b0, nb, s);
-    if (e == 2) return launch_c2i<2, 4, 6, 7>(g, xT, P, gcolT, gxT, goff, b0, nb, s);
+  // 8 (2 workgroups per CU) 0.658 / 0.167, 11 0.585 / 0.137.
+  if constexpr (sizeof(GT) == 2)
     return launch_c2i<3, 4, 6, 7>(g, xT, P, gcolT, gxT, goff, b0, nb, s);
-  } else {
-    if (e == 1) return launch_c2i<2, 4, 6, 4>(g, xT, P, gcolT, gxT, goff, b0, nb, s);
+  else
     return launch_c2i<2, 4, 6, 7>(g, xT, P, gcolT, gxT, goff, b0, nb, s);
-  }
 }
 
 hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, const float* off,
@@ -1321,15 +1315,9 @@ hipError_t launch_im2col_bf16(const Geo& g, const bf16_t* xT, const float* off, 
     hipLaunchKernelGGL(kern, dim3(th_n * tw_n, 1, nb), dim3(256), 0, s, g, xT, off, colT, b0,
                        tw_n);
   };
-  const int v = exp_flag(14);
-  if (g.C % 8 == 0 && g.C > 128 && v != 1) {
-    if (v == 2) go(im2col_lds_b8<8, 4, 1, 256>, 8, 4);
-    else if (v == 3) go(im2col_lds_b8<4, 8, 1, 256>, 4, 8);
-    else if (v == 4) go(im2col_lds_b8<8, 8, 1, 256>, 8, 8);
-    else if (v == 5) go(im2col_lds_b8<4, 4, 2, 256>, 4, 4);
-    else if (v == 6) go(im2col_lds_b8<4, 4, 1, 256, false>, 4, 4);
-    else go(im2col_lds_b8<4, 4, 1, 256>, 4, 4);
-  } else if (g.C <= 32)
+  if (g.C % 8 == 0 && g.C > 128)
+    go(im2col_lds_b8<4, 4, 1, 256>, 4, 4);
+  else if (g.C <= 32)
     go(im2col_lds<8, 8, 2, 32, true, bf16_t, bf16_t>, 8, 8);
   else if (g.C <= 64)
     go(im2col_lds<8, 8, 2, 64, true, bf16_t, bf16_t>, 8, 8);

@@ -74,7 +74,6 @@ class HostFwdCtx:
 def dcn_forward_numpy(x, w_off, b_off, w, b, stride, padding, handle=None, return_ctx=False):
     """out, off = DeformConv2d.execute on host arrays (one libdcn call). With return_ctx,
     also a HostFwdCtx for dcn_backward_numpy(ctx=...)."""
-    h = handle or rt.default_handle()
     x, w_off, b_off, w = _f32(x), _f32(w_off), _f32(b_off), _f32(w)
     b = None if b is None else _f32(b)
     B, C, H, W = x.shape
@@ -83,8 +82,11 @@ def dcn_forward_numpy(x, w_off, b_off, w, b, stride, padding, handle=None, retur
         raise ValueError(f"input has {C} channels, weight expects {Cw}")
     if B == 0:  # empty batch: empty outputs, as the reference's ops give (no launch)
         Ho, Wo = rt.out_shape(rt.make_desc(1, C, H, W, O, (kh, kw), stride, padding))
-        return (np.empty((0, O, Ho, Wo), np.float32),
-                np.empty((0, w_off.shape[0], Ho, Wo), np.float32))
+        out = np.empty((0, O, Ho, Wo), np.float32)
+        off = np.empty((0, w_off.shape[0], Ho, Wo), np.float32)
+        # no forward state to reuse: dcn_backward_numpy takes ctx=None (and B == 0 there too)
+        return (out, off, None) if return_ctx else (out, off)
+    h = handle or rt.default_handle()  # after the empty-batch case: it launches nothing
     desc = rt.make_desc(B, C, H, W, O, (kh, kw), stride, padding, bias=b is not None)
     Ho, Wo = rt.out_shape(desc)
     out = hostmem.empty((B, O, Ho, Wo))
@@ -102,7 +104,6 @@ def dcn_backward_numpy(x, off, w_off, w, has_bias, grad_out, stride, padding, ha
     """Grads of DeformConv2d.execute (dict keyed like the state dict, plus 'x', 'offset').
     ctx: the forward's HostFwdCtx; when nothing else ran on the handle since, x / off /
     weights are not uploaded again and the forward's columns are reused."""
-    h = handle or (ctx.handle if ctx is not None else rt.default_handle())
     x, off, w_off, w, grad_out = map(_f32, (x, off, w_off, w, grad_out))
     B, C, H, W = x.shape
     O, _, kh, kw = w.shape
@@ -114,6 +115,7 @@ def dcn_backward_numpy(x, off, w_off, w, has_bias, grad_out, stride, padding, ha
         if has_bias:
             g["bias"] = np.zeros(O, np.float32)
         return g
+    h = handle or (ctx.handle if ctx is not None else rt.default_handle())
     desc = rt.make_desc(B, C, H, W, O, (kh, kw), stride, padding, bias=has_bias)
     g = {"x": hostmem.empty_like(x), "weight": hostmem.empty_like(w),
          "offset_conv.weight": hostmem.empty_like(w_off),

@@ -30,7 +30,9 @@ class HostPool:
     def __init__(self, keep=_KEEP):
         self.keep = keep
         self._free: dict[int, list[np.ndarray]] = {}
-        self._lock = threading.Lock()
+        # re-entrant: _release runs from a weakref finalizer, which cyclic GC may trigger on
+        # this thread while it already holds the lock (inside empty() or _release itself)
+        self._lock = threading.RLock()
 
     def empty(self, shape, dtype=np.float32) -> np.ndarray:
         dtype = np.dtype(dtype)

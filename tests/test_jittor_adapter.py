@@ -103,3 +103,16 @@ def test_jittor_adapter_on_libdcn(jdc, bias):
     assert_close(grads[0].numpy(), rg["x"], what="jt adapter ∂x")
     for n, gv in zip(names[1:], grads[1:]):
         assert_close_reduction(gv.numpy(), rg[n], what=f"jt adapter ∂{n}")
+
+
+def test_jittor_adapter_empty_batch(jdc):
+    """An empty batch through the jt.Function: execute unpacks the forward's
+    (out, off, ctx) and grad returns zero parameter grads, with no launch."""
+    jt, mod = jdc
+    m = mod.DeformConv2d(4, 6, 3, 1, 1)
+    out = m(jt.array(np.zeros((0, 4, 8, 8), np.float32)))
+    assert out.shape == (0, 6, 8, 8)
+    grads = jt.Function.last.backward(jt.array(np.zeros((0, 6, 8, 8), np.float32)))
+    assert grads[0].shape == (0, 4, 8, 8)
+    for gv in grads[1:5]:
+        assert not gv.numpy().any()

@@ -8,7 +8,7 @@ import pytest
 
 import deform_conv
 import dcn_runtime as rt
-from deform_conv import DeformConv2d
+from deform_conv import DeformConv2d, dcn_backward_numpy, dcn_forward_numpy
 
 
 def test_import_line_matches_reference():
@@ -69,3 +69,24 @@ def test_execute_without_gpu_fails_loudly():
     m = DeformConv2d(2, 3)
     with pytest.raises(RuntimeError):
         m(np.zeros((1, 2, 8, 8), np.float32))
+
+
+def test_empty_batch_through_the_module():
+    """B == 0: execute + backward through the module give empty outputs and zero
+    parameter grads without a launch (so without a device), as the reference's ops do on an
+    empty batch; the forward-reuse context is None and the backward accepts it."""
+    m = DeformConv2d(3, 5, 3, 2, 1)
+    x = np.zeros((0, 3, 9, 7), np.float32)
+    out = m(x)
+    assert out.shape == (0, 5, 5, 4) and out.dtype == np.float32
+    gx = m.backward(np.zeros_like(out))
+    assert gx.shape == x.shape
+    for name, p in m.named_parameters():
+        assert p.grad.shape == p.shape and not p.grad.any(), name
+    # the functional form, with and without the context
+    o2, off, ctx = dcn_forward_numpy(x, m.offset_conv.weight, m.offset_conv.bias, m.weight, None,
+                                     (2, 2), (1, 1), return_ctx=True)
+    assert ctx is None and o2.shape == (0, 5, 5, 4) and off.shape == (0, 18, 5, 4)
+    g = dcn_backward_numpy(x, off, m.offset_conv.weight, m.weight, False, o2, (2, 2), (1, 1),
+                           ctx=ctx)
+    assert "bias" not in g and g["offset"].shape == off.shape
