@@ -10,8 +10,12 @@ Samples per step per GPU = B·Ho·Wo·kh·kw = 1,806,336.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-One process per GPU; batch shards are independent (weak scaling); value = all
-ranks' samples / max-over-ranks time. Rank 0 prints one JSON line. torch is
+One process per GPU; batch shards are independent. Default: weak scaling (B=64 images per
+GPU, the driver's per-N `value`); `--global-batch G` splits a fixed batch of G images over
+the N ranks instead ("scaling": "strong"; SURVEY §8(e) asks for both curves), and the
+default multi-GPU run also times the fixed global batch 512 and reports it under
+`strong_scaling`. value = all ranks' samples / max-over-ranks time. Rank 0 prints one JSON
+line. torch is
 plumbing only (HBM buffers, the stream handle, torch.distributed/RCCL); every
 kernel of the step is libdcn's (hand-written gfx950 HIP + rocBLAS).
 """
@@ -52,6 +56,18 @@ def k1_bytes(B, C, H, W, N, Ho, Wo, elem=4, J=None):
     read x + read offsets (J = 2·N·deform_groups channels) + write columns."""
     J = 2 * N if J is None else J
     return elem * (B * C * H * W + B * J * Ho * Wo + B * Ho * Wo * N * C)
+
+
+def shard_sizes(global_batch, world):
+    """Images per rank when a fixed global batch is split over `world` ranks: as even as
+    possible, the first global_batch % world ranks one image more (every rank >= 1)."""
+    if global_batch < world:
+        raise ValueError(f"global batch {global_batch} < {world} ranks")
+    q, r = divmod(global_batch, world)
+    return [q + (1 if i < r else 0) for i in range(world)]
+
+
+STRONG_GLOBAL_BATCH = 512  # SURVEY §8(e) / BASELINE config 4: N=512 over 8 GPUs
 
 
 def host_cpus():
@@ -238,6 +254,12 @@ def main():
     ap.add_argument("--dry", action="store_true",
                     help="launcher check without a GPU: ranks join a gloo group, sum their "
                          "rank ids and rank 0 prints the world it saw (CPU tests)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="strong scaling: split this many images over the N ranks (0: weak "
+                         "scaling, the config's B per GPU)")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="skip the secondary fixed-global-batch (512) measurement that "
+                         "multi-GPU weak runs of configs 3 and 4 add under strong_scaling")
     ap.add_argument("--exchange", action="store_true",
                     help="run the gradient exchange even at N=1 (a 1-rank RCCL group), to "
                          "exercise the overlapped all-reduce path on one GPU")
@@ -253,7 +275,7 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if args.dry:
-        return dry_run(world, rank)
+        return dry_run(world, rank, args.global_batch)
 
     # stdout carries exactly one JSON line: whatever the libraries print there (RCCL's
     # version banner at communicator init, ...) goes to stderr instead
@@ -278,13 +300,17 @@ def main():
 
     cfg = CONFIGS[args.config]
     B, C, O_, H, W, k, s, p = (cfg[n] for n in ("B", "C", "O", "H", "W", "k", "s", "p"))
+    strong = args.global_batch > 0
+    if strong:  # fixed global batch split over the ranks (SURVEY §8(e) strong scaling)
+        B = shard_sizes(args.global_batch, world)[rank]
     bf16 = cfg["dtype"] == "bf16"
     tdt = torch.bfloat16 if bf16 else torch.float32
     N = k * k
     dil, G = cfg.get("dil", 1), cfg.get("G", 1)
     fwd_only = cfg.get("fwd_only", False)
-    desc = rt.make_desc(B, C, H, W, O_, (k, k), (s, s), (p, p), (dil, dil), G,
-                        dtype=rt.DCN_BF16 if bf16 else rt.DCN_F32)
+    mk_desc = lambda nb: rt.make_desc(nb, C, H, W, O_, (k, k), (s, s), (p, p), (dil, dil), G,
+                                      dtype=rt.DCN_BF16 if bf16 else rt.DCN_F32)
+    desc = mk_desc(B)
     Ho, Wo = rt.out_shape(desc)
     J = 2 * N * G
 
@@ -296,20 +322,11 @@ def main():
     b_off = (torch.rand(J, device=dev, generator=g) - 0.5).to(tdt)
     w = (torch.randn(O_, C, k, k, device=dev, generator=g) * float(np.sqrt(2.0 / (C * N)))).to(tdt)
     b = (torch.randn(O_, device=dev, generator=g) * 0.1).to(tdt)
-    g.manual_seed(1000 + rank)
-    x = torch.randn(B, C, H, W, device=dev, generator=g).to(tdt)
-    gout = torch.randn(B, O_, Ho, Wo, device=dev, generator=g).to(tdt)
-    out = torch.empty(B, O_, Ho, Wo, device=dev, dtype=tdt)
-    off = torch.empty(B, J, Ho, Wo, device=dev, dtype=tdt)
-    gx = torch.empty_like(x)
     # all parameter grads packed in ONE buffer -> one all-reduce per step (dcn_dp)
     gbuf = dcn_dp.GradBuffer(dcn_dp.param_shapes(C, O_, k, k, deform_groups=G),
                              lambda n: torch.empty(n, device=dev, dtype=tdt))
     gflat = gbuf.flat
     gw, gb, gwo, gbo = (gbuf[n] for n in dcn_dp.PARAM_ORDER)
-    goff = torch.empty_like(off)
-    wsb = rt.workspace_bytes(desc, True)
-    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
 
     h = rt.Handle(local_rank)
     stream = torch.cuda.current_stream(dev)
@@ -343,20 +360,55 @@ def main():
             dcn_dp.allreduce_torch(t32)
             t.copy_(t32)
 
-    def step():
-        rt.check(L.dcn_forward(h.h, desc, P(x), P(w_off), P(b_off), P(w), P(b), P(out), P(off),
-                               P(ws), wsb), "dcn_forward")
-        if fwd_only:
-            return
-        rt.check(L.dcn_backward(h.h, desc, P(x), P(off), P(w_off), P(w), P(gout), P(gx), P(gw),
-                                P(gb), P(gwo), P(gbo), P(goff), P(ws), wsb, rt.DCN_BWD_COL_IN_WS),
-                 "dcn_backward")
-        if gs is not None:
-            with torch.cuda.stream(gs):
-                reduce_fp32(gflat[:n_dw])  # starts once ∂W/∂b are final (dcn_set_grad_stream)
-            reduce_fp32(gflat[n_dw:])      # ∂W_off/∂b_off after the whole backward
-            stream.wait_stream(gs)
+    def make_step(nb, seed):
+        """One DeformConv2d fwd + bwd (+ the gradient exchange) over a resident shard of
+        nb images; returns the step and the buffers it keeps alive."""
+        d = mk_desc(nb)
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(seed)
+        x = torch.randn(nb, C, H, W, device=dev, generator=gen).to(tdt)
+        gout = torch.randn(nb, O_, Ho, Wo, device=dev, generator=gen).to(tdt)
+        out = torch.empty(nb, O_, Ho, Wo, device=dev, dtype=tdt)
+        off = torch.empty(nb, J, Ho, Wo, device=dev, dtype=tdt)
+        gx = torch.empty_like(x)
+        goff = torch.empty_like(off)
+        wsb = rt.workspace_bytes(d, True)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
 
+        def step():
+            rt.check(L.dcn_forward(h.h, d, P(x), P(w_off), P(b_off), P(w), P(b), P(out), P(off),
+                                   P(ws), wsb), "dcn_forward")
+            if fwd_only:
+                return
+            rt.check(L.dcn_backward(h.h, d, P(x), P(off), P(w_off), P(w), P(gout), P(gx), P(gw),
+                                    P(gb), P(gwo), P(gbo), P(goff), P(ws), wsb,
+                                    rt.DCN_BWD_COL_IN_WS), "dcn_backward")
+            if gs is not None:
+                with torch.cuda.stream(gs):
+                    reduce_fp32(gflat[:n_dw])  # starts once ∂W/∂b are final (dcn_set_grad_stream)
+                reduce_fp32(gflat[n_dw:])      # ∂W_off/∂b_off after the whole backward
+                stream.wait_stream(gs)
+        return step, (x, gout, out, off, gx, goff, ws)
+
+    def timed(run, steps):
+        """Barrier + synchronize on both sides of exactly `steps` steps; max over ranks."""
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            run()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el_ = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el_], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el_ = float(t.item())
+        return el_
+
+    step, bufs = make_step(B, 1000 + rank)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -381,19 +433,7 @@ def main():
             h.set_stream(stream.cuda_stream)
             graph_note = f"graph capture failed ({type(e).__name__}: {e}); eager step timed"
             torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = timed(run, args.steps)
 
     # per-kernel durations: a second, separate pass of the same steps with HIP events
     # around every libdcn launch on `stream` (kept out of the timed region above)
@@ -439,8 +479,34 @@ def main():
     k1_b = k1_bytes(B, C, H, W, N, Ho, Wo, elem=2 if bf16 else 4, J=J)
     k1_name = K1_KERNEL if (G == 1 and C % 4 == 0) else "dcn::im2col_cl"
 
-    samples = B * Ho * Wo * N * world * args.steps
+    gbatch = args.global_batch if strong else B * world
+    samples = gbatch * Ho * Wo * N * args.steps
     value = samples / el / 1e9
+    # the other scaling curve: a weak run of configs 3 / 4 also times the
+    # fixed global batch of 512 images split over the same ranks (at N = 8 that is the weak
+    # shard again); reported beside `value`, never as it
+    strong_res = None
+    if (not strong and not args.no_strong and args.config in (3, 4) and not fwd_only
+            and not args.graph):
+        h.prof_enable(0)  # no per-kernel events in this timed region
+        del step, bufs, run
+        torch.cuda.synchronize(dev)
+        torch.cuda.empty_cache()
+        shards = shard_sizes(STRONG_GLOBAL_BATCH, world)
+        step2, bufs2 = make_step(shards[rank], 2000 + rank)
+        for _ in range(2):
+            step2()
+        st_steps = max(1, min(args.steps, 10))
+        el2 = timed(step2, st_steps)
+        strong_res = {
+            "scaling": "strong", "global_batch": STRONG_GLOBAL_BATCH, "shards": shards,
+            "steps": st_steps, "ms_per_step": round(el2 / st_steps * 1e3, 4),
+            "value": round(STRONG_GLOBAL_BATCH * Ho * Wo * N * st_steps / el2 / 1e9, 5),
+            "unit": "Gsamples/s",
+            "note": "fixed global batch of 512 images split over the ranks, timed like value "
+                    "(barrier + synchronize, max over ranks); `value` is the weak curve"}
+        del step2, bufs2
+        torch.cuda.empty_cache()
     if rank == 0:
         achieved = k1_b / (k1_ms * 1e-3) / 1e9 if k1_ms else None
         # the committed PMC summary covers the config-3 (fp32) and config-4 (bf16) K1 only
@@ -457,7 +523,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": cfg["dtype"],
             "gemm_math": MATH_NAMES[args.math] if not bf16 else "bf16 MFMA (fp32 accumulate)",
@@ -466,7 +532,9 @@ def main():
                                    f"p{p} dil{dil} G{G} {cfg['dtype']} DeformConv2d "
                                    + ("fwd only" if fwd_only else
                                       "fwd+bwd (+RCCL grad all-reduce if N>1)"),
-                       "global_batch": B * world, "B_per_gpu": B, "C": C, "O": O_, "H": H, "W": W,
+                       "global_batch": gbatch,
+                       "B_per_gpu": (shard_sizes(args.global_batch, world) if strong else B),
+                       "C": C, "O": O_, "H": H, "W": W,
                        "kernel": k, "stride": s, "padding": p,
                        "parallelism": f"dp{world} (batch-sharded, replicated params)",
                        "grad_allreduce": (f"{args.comm} (overlapped with the backward, fp32 sums)"
@@ -488,6 +556,7 @@ def main():
             "rooflines_other": other_rooflines(kernel_ms, B, C, O_, H, W, N, Ho, Wo, J, bf16,
                                                fwd_only),
             "alt": alt,
+            "strong_scaling": strong_res,
             "cpu_baseline": None,
             "cpu_baseline_other": None,
         }
@@ -584,22 +653,30 @@ def spawn_ranks(n):
     return max((abs(rc) for rc in rcs), default=0)
 
 
-def dry_run(world, rank):
-    """--dry: the launch contract without a GPU (gloo on CPU)."""
+def dry_run(world, rank, global_batch=0):
+    """--dry: the launch contract without a GPU (gloo on CPU): the ranks join one group and
+    rank 0 reports the world it saw and, per rank, the images of its shard (the config's B
+    per GPU, or its share of --global-batch), gathered from the ranks themselves."""
     import torch
     import torch.distributed as dist
+    mine = shard_sizes(global_batch, world)[rank] if global_batch else CONFIGS[3]["B"]
     if world > 1:
         dist.init_process_group("gloo")
         t = torch.tensor([float(rank)])
         dist.all_reduce(t)
         seen = int(t.item())
+        got = [torch.zeros(1) for _ in range(world)]
+        dist.all_gather(got, torch.tensor([float(mine)]))
+        shards = [int(v.item()) for v in got]
         dist.barrier()
         dist.destroy_process_group()
     else:
-        seen = 0
+        seen, shards = 0, [mine]
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "dry": True,
-                          "rank_id_sum": seen, "pid": os.getpid()}), flush=True)
+                          "rank_id_sum": seen, "pid": os.getpid(),
+                          "scaling": "strong" if global_batch else "weak",
+                          "global_batch": sum(shards), "shards": shards}), flush=True)
 
 
 def other_rooflines(kernel_ms, B, C, O_, H, W, N, Ho, Wo, J, bf16, fwd_only):

@@ -15,13 +15,15 @@
 // ∂x without atomics: LDS float atomics (ds_add_f32) measured ~0.3 lanes/clk/CU on
 // MI355X and global float atomics cap at ~1.3 TB/s, both far too slow for the
 // 4·B·HW·N·C scatter. Instead each sample is binned by its top-left corner
-// (counting sort per image: int atomics on 28k samples/image), each sample's place in
-// its bin is its rank by sample index, and each input pixel gathers the ∂col rows of the
+// (a stable sort per image by bin, sample index breaking ties: K5b below), and each input
+// pixel gathers the ∂col rows of the
 // four bins whose 2x2 footprint covers it — a fixed summation order, so ∂x is bitwise
 // reproducible.
 #include <climits>
 #include <cstdlib>
 #include <type_traits>
+
+#include <rocprim/block/block_radix_sort.hpp>
 
 #include "dcn_device.h"
 
@@ -524,82 +526,182 @@ __global__ __launch_bounds__(256) void offgrad_cl(Geo g, LaneMap L, const float*
 
 // ---------------------------------------------------------------------------
 // K5b: sample bins. Bin of a valid sample = its top-left corner (r0, c0) in
-// [-1, H-1] x [-1, W-1] -> (r0+1)*(W+1) + (c0+1); NB = (H+1)*(W+1) bins per
-// (image, group). rec[s] = {bin, fr, fc}.
+// [-1, H-1] x [-1, W-1] -> (r0+1)*(W+1) + (c0+1); NB = (H+1)*(W+1) bins per segment
+// (image, group). Within a bin the samples are ordered by sample index s = m*N + n (that
+// order fixes K5's summation order, so ∂x and ∂offset are bitwise reproducible).
+//
+// Three kernels, no atomics (r03; r02's count / scan / fill / rank took ~0.98 ms per
+// config-3 step on the side stream, 0.60 of it in the rank loop):
+//   bins_chunk_sort  a segment's samples in chunks of kBinChunk: each chunk's bins are
+//                    computed from the offsets and sorted in LDS (rocprim block radix sort,
+//                    stable, so equal bins keep ascending s); the chunk's sorted list and
+//                    its per-bin run lengths H[seg][bin][chunk] are written;
+//   bins_scan_table  one workgroup per segment: exclusive scan of H in (bin, chunk) order
+//                    = every (bin, chunk) run's first position in the segment's bin order;
+//                    start[bin] = the bin's first position;
+//   bins_emit        each chunk places its sorted samples at base + rank in run: the packed
+//                    records of the fused K5 (brec) or the sorted sample lists (slist).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void bins_count(Geo g, const float* __restrict__ off,
-                                                  int* __restrict__ cnt, float4* __restrict__ rec,
-                                                  int b0, int nb) {
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  const int NS = g.HW * g.N;
-  const long total = (long)nb * g.G * NS;
-  if (idx >= total) return;
-  const int s = (int)(idx % NS);
-  const int bg = (int)(idx / NS);  // bl*G + gi
-  const int gi = bg % g.G, bl = bg / g.G;
-  const Tap t = sample_tap(g, off, b0 + bl, gi, s % g.N, s / g.N);
-  const int NB = (g.H + 1) * (g.W + 1);
-  int bin = -1;
-  if (t.ok) {
-    bin = (t.r0 + 1) * (g.W + 1) + (t.c0 + 1);
-    atomicAdd(cnt + (size_t)bg * NB + bin, 1);
-  }
-  rec[idx] = make_float4(__int_as_float(bin), t.fr, t.fc, 0.f);
+constexpr int kBinT = 256, kBinIPT = 8, kBinChunk = kBinT * kBinIPT;
+constexpr int kBinLBits = 11;  // sample index within a chunk (< 2048) in a packed entry
+static_assert(kBinChunk == 1 << kBinLBits, "packed entry layout");
+
+// H row length: NB bins plus the sentinel NB (whose start is the end of the last bin), padded
+// to a multiple of 4 for the 16-B accesses of bins_scan_table
+__host__ __device__ __forceinline__ int bins_nbp(int NB) { return (NB + 1 + 3) / 4 * 4; }
+
+__device__ __forceinline__ unsigned sample_bin(const Geo& g, const float* __restrict__ off, int b,
+                                               int gi, int s, int NB, Tap* tp) {
+  const Tap t = sample_tap(g, off, b, gi, s % g.N, s / g.N);
+  if (tp) *tp = t;
+  return t.ok ? (unsigned)((t.r0 + 1) * (g.W + 1) + (t.c0 + 1)) : (unsigned)NB;
 }
 
-// Exclusive scan of the NB counts of one (image, group); start has NB+1 entries.
-__global__ __launch_bounds__(1024) void bins_scan(int NB, const int* __restrict__ cnt,
-                                                  int* __restrict__ start,
-                                                  int* __restrict__ cursor) {
-  __shared__ int wsum[16];
-  const int bg = blockIdx.x, tid = threadIdx.x;
-  const int* c = cnt + (size_t)bg * NB;
-  int* st = start + (size_t)bg * (NB + 1);
-  int* cu = cursor + (size_t)bg * NB;
-  const int per = (NB + 1023) / 1024;
-  const int lo = min(tid * per, NB), hi = min(lo + per, NB);
-  int local = 0;
-  for (int i = lo; i < hi; ++i) local += c[i];
-  // inclusive scan of `local` across the block
-  int v = local;
-  const int lane = tid & 63, wv = tid >> 6;
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(v, o);
-    if (lane >= o) v += t;
-  }
-  if (lane == 63) wsum[wv] = v;
-  __syncthreads();
-  if (tid == 0) {
-    int acc = 0;
-    for (int i = 0; i < 16; ++i) {
-      const int t = wsum[i];
-      wsum[i] = acc;
-      acc += t;
+__global__ __launch_bounds__(kBinT) void bins_chunk_sort(Geo g, const float* __restrict__ off,
+                                                         int b0, int nch, int NB, unsigned kbits,
+                                                         int* __restrict__ H,
+                                                         unsigned* __restrict__ sorted,
+                                                         float4* __restrict__ rec) {
+  using Sort = rocprim::block_radix_sort<unsigned, kBinT, kBinIPT, unsigned short>;
+  __shared__ typename Sort::storage_type sst;
+  __shared__ unsigned skey[kBinChunk];
+  const int tid = threadIdx.x, ch = blockIdx.x, bg = blockIdx.y;
+  const int NS = g.HW * g.N, gi = bg % g.G, b = b0 + bg / g.G;
+  unsigned key[kBinIPT];
+  unsigned short val[kBinIPT];
+#pragma unroll
+  for (int u = 0; u < kBinIPT; ++u) {
+    const int l = tid * kBinIPT + u, s = ch * kBinChunk + l;
+    val[u] = (unsigned short)l;
+    if (s < NS) {
+      Tap t;
+      key[u] = sample_bin(g, off, b, gi, s, NB, &t);
+      if (rec)  // dx_gather_cl's per-sample records (the unfused K5 only)
+        rec[(size_t)bg * NS + s] = make_float4(__int_as_float(t.ok ? (int)key[u] : -1), t.fr, t.fc, 0.f);
+    } else {
+      key[u] = (unsigned)NB + 1;  // past the end: after every bin and the invalid samples
     }
   }
-  __syncthreads();
-  int run = v - local + wsum[wv];
-  for (int i = lo; i < hi; ++i) {
-    st[i] = run;
-    cu[i] = 0;
-    run += c[i];
+  Sort().sort(key, val, sst, 0, kbits);  // blocked result: thread t holds ranks t*IPT + u
+  unsigned* out = sorted + ((size_t)bg * nch + ch) * kBinChunk;
+#pragma unroll
+  for (int u = 0; u < kBinIPT; ++u) {
+    skey[tid * kBinIPT + u] = key[u];
+    out[tid * kBinIPT + u] = (key[u] << kBinLBits) | val[u];
   }
-  if (tid == 1023) st[NB] = run;
+  __syncthreads();
+  // run lengths: the thread holding a run's first entry counts it (runs are short)
+  int* Hb = H + ((size_t)bg * nch + ch) * bins_nbp(NB);
+#pragma unroll
+  for (int u = 0; u < kBinIPT; ++u) {
+    const int i = tid * kBinIPT + u;
+    const unsigned k = key[u];
+    if (k < (unsigned)NB && (i == 0 || skey[i - 1] != k)) {
+      int c = 1;
+      while (i + c < kBinChunk && skey[i + c] == k) ++c;
+      Hb[k] = c;
+    }
+  }
 }
 
-__global__ __launch_bounds__(256) void bins_fill(Geo g, const float4* __restrict__ rec,
-                                                 const int* __restrict__ start,
-                                                 int* __restrict__ cursor, int* __restrict__ list,
-                                                 int nb) {
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  const int NS = g.HW * g.N;
-  if (idx >= (long)nb * g.G * NS) return;
-  const int bin = __float_as_int(rec[idx].x);
-  if (bin < 0) return;
-  const int bg = (int)(idx / NS);
-  const int NB = (g.H + 1) * (g.W + 1);
-  const int slot = atomicAdd(cursor + (size_t)bg * NB + bin, 1);
-  list[(size_t)bg * NS + start[(size_t)bg * (NB + 1) + bin] + slot] = (int)(idx % NS);
+// One workgroup per segment: the (bin, chunk) runs in bin-major order get their first
+// positions in the segment's bin order. H is chunk-major ([chunk][bin], bins padded to a
+// multiple of 4), so thread t owns bins 4t..4t+3 and every access is a coalesced 16-B one:
+// pass 1 sums each bin over the chunks, a block scan over the bins gives start[bin], pass 2
+// replaces H[c][bin] by start[bin] + the runs of the earlier chunks. Bins beyond 4096 are
+// handled in rounds, carrying the running total.
+__global__ __launch_bounds__(1024) void bins_scan_table(int NB, int nch, int* __restrict__ H,
+                                                        int* __restrict__ start) {
+  __shared__ int wsum[17];  // exclusive wave prefixes, then the block total
+  const int bg = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int NBp = bins_nbp(NB);
+  int* Hs = H + (size_t)bg * nch * NBp;
+  int* st = start + (size_t)bg * (NB + 1);
+  int carry = 0;
+  for (int b0 = 0; b0 < NBp; b0 += 4096) {
+    const int bb = b0 + 4 * tid;
+    const bool act = bb < NBp;
+    int4 tot = make_int4(0, 0, 0, 0);
+    if (act)
+      for (int c = 0; c < nch; ++c) {
+        const int4 v = *reinterpret_cast<const int4*>(Hs + (size_t)c * NBp + bb);
+        tot.x += v.x; tot.y += v.y; tot.z += v.z; tot.w += v.w;
+      }
+    const int local = tot.x + tot.y + tot.z + tot.w;
+    int v = local;  // inclusive scan over the block
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(v, o);
+      if (lane >= o) v += t;
+    }
+    if (lane == 63) wsum[wv] = v;
+    __syncthreads();
+    if (tid == 0) {
+      int acc = 0;
+      for (int i = 0; i < 16; ++i) {
+        const int t = wsum[i];
+        wsum[i] = acc;
+        acc += t;
+      }
+      wsum[16] = acc;
+    }
+    __syncthreads();
+    const int e = carry + v - local + wsum[wv];
+    carry += wsum[16];
+    int run[4] = {e, e + tot.x, e + tot.x + tot.y, e + tot.x + tot.y + tot.z};
+    if (act) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (bb + i <= NB) st[bb + i] = run[i];
+      for (int c = 0; c < nch; ++c) {
+        int4* p = reinterpret_cast<int4*>(Hs + (size_t)c * NBp + bb);
+        const int4 hv = *p;
+        *p = make_int4(run[0], run[1], run[2], run[3]);
+        run[0] += hv.x; run[1] += hv.y; run[2] += hv.z; run[3] += hv.w;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Places each chunk's sorted samples: position = base[bin][chunk] + rank within the run.
+// brec (fused K5): {∂colT row offset m*K + n*C, fr, fc, ∂offset index n*HW + m}; else
+// slist (dx_gather_cl): the sample index.
+__global__ __launch_bounds__(kBinT) void bins_emit(Geo g, const float* __restrict__ off, int b0,
+                                                   int nch, int NB, const int* __restrict__ H,
+                                                   const unsigned* __restrict__ sorted,
+                                                   int4* __restrict__ brec,
+                                                   int* __restrict__ slist) {
+  __shared__ unsigned skey[kBinChunk];
+  const int tid = threadIdx.x, ch = blockIdx.x, bg = blockIdx.y;
+  const int NS = g.HW * g.N, gi = bg % g.G, b = b0 + bg / g.G;
+  const unsigned* in = sorted + ((size_t)bg * nch + ch) * kBinChunk;
+  unsigned e[kBinIPT];
+#pragma unroll
+  for (int u = 0; u < kBinIPT; ++u) {
+    e[u] = in[tid * kBinIPT + u];
+    skey[tid * kBinIPT + u] = e[u] >> kBinLBits;
+  }
+  __syncthreads();
+  const int* Hb = H + ((size_t)bg * nch + ch) * bins_nbp(NB);
+#pragma unroll
+  for (int u = 0; u < kBinIPT; ++u) {
+    const int i = tid * kBinIPT + u;
+    const unsigned k = e[u] >> kBinLBits;
+    if (k >= (unsigned)NB) continue;  // invalid sample or chunk padding (sorted last)
+    int j = i;
+    while (j > 0 && skey[j - 1] == k) --j;
+    const size_t pos = (size_t)bg * NS + Hb[k] + (i - j);
+    const int s = ch * kBinChunk + (int)(e[u] & (kBinChunk - 1));
+    if (brec) {
+      Tap t;
+      sample_bin(g, off, b, gi, s, NB, &t);
+      const int m = s / g.N, n = s - m * g.N;
+      brec[pos] = make_int4(m * g.K + n * g.C, __float_as_int(t.fr), __float_as_int(t.fc),
+                            n * g.HW + m);
+    } else {
+      slist[pos] = s;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -783,37 +885,6 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
       if (Q0 + j < g.W)
         *reinterpret_cast<float4*>(gxT + (((size_t)b * g.H + r) * g.W + Q0 + j) * g.C + c) =
             add4(dn[j], lds[(w * kTQ + j) * 64 + lane]);
-  }
-}
-
-// Binned samples as contiguous records for the fused K5 kernels, in bin order:
-// {∂colT row offset m*K + n*C, fr, fc, ∂offset index n*HW + m}. One thread per sample,
-// in sample order: its place in its bin is the number of the bin's samples with a smaller
-// index (the bin lists are filled in atomic order, so this is what fixes the order; the
-// rank needs only independent loads of the bin's ~N entries, no sort).
-__global__ __launch_bounds__(256) void bins_rank(Geo g, int nbg, const float4* __restrict__ rec,
-                                                 const int* __restrict__ start,
-                                                 const int* __restrict__ list,
-                                                 int4* __restrict__ brec, int* __restrict__ slist) {
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  const int NS = g.HW * g.N, NB = (g.H + 1) * (g.W + 1);
-  if (idx >= (long)nbg * NS) return;
-  const int bg = (int)(idx / NS), s = (int)(idx - (long)bg * NS);
-  const float4 R = rec[idx];
-  const int bin = __float_as_int(R.x);
-  if (bin < 0) return;
-  const int* stb = start + (size_t)bg * (NB + 1);
-  const int lo = stb[bin], hi = stb[bin + 1];
-  const int* l = list + (size_t)bg * NS;
-  int rank = 0;
-  for (int j = lo; j < hi; ++j) rank += l[j] < s;
-  const size_t pos = (size_t)bg * NS + lo + rank;
-  if (brec) {
-    const int m = s / g.N, n = s - m * g.N;
-    brec[pos] = make_int4(m * g.K + n * g.C, __float_as_int(R.y), __float_as_int(R.z),
-                          n * g.HW + m);
-  } else {
-    slist[pos] = s;
   }
 }
 
@@ -1101,19 +1172,21 @@ __global__ __launch_bounds__(256) void col2im_generic(Geo g, const float* __rest
 // ---------------------------------------------------------------------------
 static bool can_vec4(const Geo& g) { return g.C % 4 == 0 && g.Cg % 4 == 0; }
 
+static int bins_nch(const Geo& g) { return (g.HW * g.N + kBinChunk - 1) / kBinChunk; }
+static bool k5_fused(const Geo& g);
+
+// Bins workspace: start[seg][NB+1] | H[seg][NB][nch] | sorted[seg][nch][kBinChunk] |
+// rec[seg][NS] (unfused K5 only) | brec[seg][NS] (int4; slist, int, for the unfused K5).
 size_t bins_ws_bytes(const Geo& g, int nb) {
   const size_t NB = (size_t)(g.H + 1) * (g.W + 1), NS = (size_t)g.HW * g.N;
-  const size_t groups = (size_t)nb * g.G;
-  size_t b = 0;
-  b += groups * NB * 4;        // cnt
-  b += groups * (NB + 1) * 4;  // start
-  b += groups * NB * 4;        // cursor
-  b = (b + 15) / 16 * 16;
-  b += groups * NS * 16;       // rec
-  b += groups * NS * 4;        // list
-  b = (b + 15) / 16 * 16;
-  b += groups * NS * 16;       // packed records (col2im_tile)
-  return (b + 255) / 256 * 256;
+  const size_t seg = (size_t)nb * g.G, nch = bins_nch(g);
+  auto al = [](size_t v) { return (v + 255) / 256 * 256; };
+  size_t b = al(seg * (NB + 1) * 4);
+  b += al(seg * nch * bins_nbp((int)NB) * 4);
+  b += al(seg * nch * kBinChunk * 4);
+  if (!k5_fused(g)) b += al(seg * NS * 16);
+  b += al(seg * NS * 16);
+  return b;
 }
 
 hipError_t launch_im2col(const Geo& g, const float* x, const float* xT, const float* off,
@@ -1161,46 +1234,50 @@ static bool k5_fused(const Geo& g) {
 
 // Pointers into the bins workspace (bins_ws_bytes layout).
 struct BinsWs {
-  int *cnt, *start, *cursor, *list, *slist;
+  int *start, *H, *slist;
+  unsigned* sorted;
   float4* rec;
   int4* brec;
 };
 static BinsWs bins_ptrs(const Geo& g, void* bins_ws, int nb) {
-  const int NB = (g.H + 1) * (g.W + 1), NS = g.HW * g.N;
-  const size_t groups = (size_t)nb * g.G;
+  const size_t NB = (size_t)(g.H + 1) * (g.W + 1), NS = (size_t)g.HW * g.N;
+  const size_t seg = (size_t)nb * g.G, nch = bins_nch(g);
+  auto al = [](size_t v) { return (v + 255) / 256 * 256; };
   char* w = static_cast<char*>(bins_ws);
   BinsWs P;
-  P.cnt = reinterpret_cast<int*>(w);
-  P.start = P.cnt + groups * NB;
-  P.cursor = P.start + groups * (NB + 1);
-  size_t o = (size_t)((char*)(P.cursor + groups * NB) - w);
-  o = (o + 15) / 16 * 16;
-  P.rec = reinterpret_cast<float4*>(w + o);
-  P.list = reinterpret_cast<int*>(P.rec + groups * NS);
-  const size_t lend = (size_t)((char*)(P.list + groups * NS) - w);
-  P.brec = reinterpret_cast<int4*>(w + (lend + 15) / 16 * 16);
-  P.slist = reinterpret_cast<int*>(P.brec);  // sorted lists (non-fused K5) share that region
+  P.start = reinterpret_cast<int*>(w);
+  w += al(seg * (NB + 1) * 4);
+  P.H = reinterpret_cast<int*>(w);
+  w += al(seg * nch * bins_nbp((int)NB) * 4);
+  P.sorted = reinterpret_cast<unsigned*>(w);
+  w += al(seg * nch * kBinChunk * 4);
+  P.rec = nullptr;
+  if (!k5_fused(g)) {
+    P.rec = reinterpret_cast<float4*>(w);
+    w += al(seg * NS * 16);
+  }
+  P.brec = reinterpret_cast<int4*>(w);
+  P.slist = reinterpret_cast<int*>(w);  // sorted lists (unfused K5) share that region
   return P;
 }
 
 hipError_t launch_bins(const Geo& g, const float* off, void* bins_ws, float* goff, int b0, int nb,
                        hipStream_t s) {
   if (nb <= 0 || g_force_generic) return hipSuccess;
-  const int NB = (g.H + 1) * (g.W + 1), NS = g.HW * g.N;
-  const size_t groups = (size_t)nb * g.G;
+  const int NB = (g.H + 1) * (g.W + 1), nch = bins_nch(g);
+  // packed entries hold the bin above kBinLBits bits; keys go up to NB + 1
+  if ((unsigned long long)(NB + 2) >= (1ull << (32 - kBinLBits))) return hipErrorInvalidValue;
+  const unsigned kbits = 32 - __builtin_clz((unsigned)NB + 1);
+  const size_t seg = (size_t)nb * g.G;
   const BinsWs P = bins_ptrs(g, bins_ws, nb);
-  hipError_t e = hipMemsetAsync(P.cnt, 0, groups * NB * sizeof(int), s);
-  if (e != hipSuccess) return e;
-  const long total = (long)groups * NS;
-  const unsigned gs = (unsigned)((total + 255) / 256);
-  hipLaunchKernelGGL(bins_count, dim3(gs), dim3(256), 0, s, g, off, P.cnt, P.rec, b0, nb);
-  hipLaunchKernelGGL(bins_scan, dim3((unsigned)groups), dim3(1024), 0, s, NB, P.cnt, P.start,
-                     P.cursor);
-  hipLaunchKernelGGL(bins_fill, dim3(gs), dim3(256), 0, s, g, P.rec, P.start, P.cursor, P.list, nb);
-  // bin order fixed by rank (r01: an insertion sort per bin took 0.83 ms beside the GEMMs):
-  // packed records for the fused K5 kernels, else a sorted list for dx_gather_cl
   const bool fused = k5_fused(g);
-  hipLaunchKernelGGL(bins_rank, dim3(gs), dim3(256), 0, s, g, (int)groups, P.rec, P.start, P.list,
+  hipError_t e = hipMemsetAsync(P.H, 0, seg * nch * bins_nbp(NB) * sizeof(int), s);
+  if (e != hipSuccess) return e;
+  const dim3 grid(nch, (unsigned)seg);
+  hipLaunchKernelGGL(bins_chunk_sort, grid, dim3(kBinT), 0, s, g, off, b0, nch, NB, kbits, P.H,
+                     P.sorted, fused ? nullptr : P.rec);
+  hipLaunchKernelGGL(bins_scan_table, dim3((unsigned)seg), dim3(1024), 0, s, NB, nch, P.H, P.start);
+  hipLaunchKernelGGL(bins_emit, grid, dim3(kBinT), 0, s, g, off, b0, nch, NB, P.H, P.sorted,
                      fused ? P.brec : nullptr, P.slist);
   if (fused) {
     // samples in no bin (every corner outside the image) have ∂offset 0

@@ -192,6 +192,37 @@ int dcnref_forward(const dcnref_desc* d, const float* x, const float* w_off, con
   return 0;
 }
 
+/* deform_conv.py:59-80 only: the sampling + GEMM + bias from GIVEN offsets (the device's),
+ * so a test can compare a device forward without the knife edges of a re-derived offset
+ * (used for the bf16 path, whose offsets are rounded to bf16 before sampling). */
+int dcnref_forward_from_offsets(const dcnref_desc* d, const float* x, const float* off,
+                                const float* w, const float* b, float* out) {
+  geo_t g;
+  if (geo(d, &g)) return -1;
+  float* col = (float*)malloc((size_t)g.K * g.HW * sizeof(float));
+  if (!col) return -2;
+  for (int bi = 0; bi < d->B; ++bi) {
+    const float* xb = x + (size_t)bi * d->C * g.HWi;
+    im2col_img(d, &g, xb, off + (size_t)bi * g.J * g.HW, col);
+    float* ob = out + (size_t)bi * d->O * g.HW;
+#pragma omp parallel for schedule(static)
+    for (int o = 0; o < d->O; ++o) {
+      float* dst = ob + (size_t)o * g.HW;
+      for (int m = 0; m < g.HW; ++m) dst[m] = 0.f;
+      const float* wr = w + (size_t)o * g.K;
+      for (int k = 0; k < g.K; ++k) {
+        float wv = wr[k];
+        const float* cr = col + (size_t)k * g.HW;
+        for (int m = 0; m < g.HW; ++m) dst[m] = fmaf(wv, cr[m], dst[m]);
+      }
+      if (d->has_bias)
+        for (int m = 0; m < g.HW; ++m) dst[m] += b[o];
+    }
+  }
+  free(col);
+  return 0;
+}
+
 int dcnref_backward(const dcnref_desc* d, const float* x, const float* off, const float* w_off,
                     const float* w, const float* gout, float* gx, float* gw, float* gb,
                     float* gw_off, float* gb_off, float* goff_out) {

@@ -55,6 +55,7 @@ def lib():
         D = ctypes.POINTER(RefDesc)
         L.dcnref_forward.argtypes = [D, P, P, P, P, P, P, P]
         L.dcnref_backward.argtypes = [D, P, P, P, P, P, P, P, P, P, P, P]
+        L.dcnref_forward_from_offsets.argtypes = [D, P, P, P, P, P]
         L.dcnref_out_shape.argtypes = [D, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         L.dcnref_num_threads.restype = ctypes.c_int
         L.dcnref_set_threads.argtypes = [ctypes.c_int]
@@ -104,6 +105,19 @@ def forward(desc, x, w_off, b_off, w, b):
     if rc:
         raise RuntimeError(f"dcnref_forward failed ({rc})")
     return out, off
+
+
+def forward_from_offsets(desc, x, off, w, b):
+    """out from GIVEN offsets (deform_conv.py:59-80 without the offset conv)."""
+    Ho, Wo = out_shape(desc)
+    out = np.empty((desc.B, desc.O, Ho, Wo), np.float32)
+    f = lambda a: None if a is None else np.ascontiguousarray(a, np.float32)
+    x, off, w, b = map(f, (x, off, w, b))
+    rc = lib().dcnref_forward_from_offsets(ctypes.byref(desc), _p(x), _p(off), _p(w), _p(b),
+                                           _p(out))
+    if rc:
+        raise RuntimeError(f"dcnref_forward_from_offsets failed ({rc})")
+    return out
 
 
 def backward(desc, x, off, w_off, w, grad_out):

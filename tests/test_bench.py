@@ -88,3 +88,28 @@ def test_host_cpus_reports_model_and_count(bench):
     assert 1 <= threads <= info["host_threads"]
     assert threads <= info["affinity_threads"]
     assert "cpu_model" in info
+
+
+def test_shard_sizes_split_a_fixed_global_batch(bench):
+    """SURVEY §8(e) strong scaling: the fixed global batch of 512 over 1/2/4/8 GPUs."""
+    for n, want in ((1, [512]), (2, [256] * 2), (4, [128] * 4), (8, [64] * 8)):
+        assert bench.shard_sizes(512, n) == want
+    assert bench.shard_sizes(10, 4) == [3, 3, 2, 2]  # ragged: the first ranks take one more
+    with pytest.raises(ValueError):
+        bench.shard_sizes(3, 4)
+
+
+@pytest.mark.parametrize("n", [1, 2, 4, 8])
+def test_dry_strong_scaling_shards_per_rank(n):
+    """`bench.py --gpus N --global-batch 512 --dry`: every rank computes its own shard and
+    rank 0 reports what the ranks gathered (gloo on CPU): 512 images in all, 512/N each."""
+    rc, line, err = _run_bench("--gpus", str(n), "--global-batch", "512", "--dry", timeout=300)
+    assert rc == 0, err
+    assert line["scaling"] == "strong" and line["n_gpus"] == n
+    assert line["shards"] == [512 // n] * n and line["global_batch"] == 512
+
+
+def test_dry_weak_scaling_shards_per_rank():
+    rc, line, err = _run_bench("--gpus", "2", "--dry")
+    assert rc == 0, err
+    assert line["scaling"] == "weak" and line["shards"] == [64, 64]

@@ -3,8 +3,8 @@ operands inside, fp32 coordinates, accumulation and reductions.
 
 Oracle: the fp32/f64 restatement run on the bf16-rounded inputs, its sampling conditioned
 on the device's own bf16 offsets (knife edges, see test_gpu_parity). Tolerance (SURVEY
-§8(d): 1e-4 is unattainable in bf16, ≈1e-2 relative): every tensor must satisfy
-max|Δ| / max|ref| ≤ BF16_TOL."""
+§8(d): 1e-4 is unattainable in bf16, ≈1e-2 relative): elementwise, every element of every
+tensor within BF16_ATOL·rms(ref) + BF16_RTOL·|ref| (assert_bf16_close)."""
 from __future__ import annotations
 
 import ctypes
@@ -18,6 +18,14 @@ import ref_lib as R
 
 pytestmark = pytest.mark.gpu
 BF16_TOL = 1e-2  # measured r01: 2-4e-3 (about one bf16 ulp) on every tensor
+# Elementwise bf16 bound: |Δ| <= BF16_ATOL·rms(ref) + BF16_RTOL·|ref|
+# for EVERY element, so a localised wrong element (a corrupted column row, a wrong pixel)
+# fails even when the tensor's max-norm error stays small. rtol = 4 bf16 ulps (2^-6): the
+# device rounds its inputs' products, columns and result to bf16 (a half ulp, 2^-9, each);
+# atol scales with the tensor's RMS because the column roundings accumulate over K-long
+# sums whose result can cancel to near zero (an absolute, not relative, error there).
+BF16_RTOL = 2.0 ** -6
+BF16_ATOL = 2.0 ** -5
 
 
 def to_bf16(a):
@@ -28,6 +36,23 @@ def to_bf16(a):
 
 def from_bf16(b):
     return (np.asarray(b, np.uint16).astype(np.uint32) << 16).view(np.float32)
+
+
+def assert_bf16_close(a, ref, what):
+    """Elementwise: |Δ| <= BF16_ATOL·rms(ref) + BF16_RTOL·|ref| (see BF16_RTOL)."""
+    a = np.asarray(a, np.float64)
+    r = np.asarray(ref, np.float64)
+    assert a.shape == r.shape, f"{what}: shape {a.shape} vs {r.shape}"
+    rms = float(np.sqrt(np.mean(r * r))) if r.size else 0.0
+    lim = BF16_ATOL * max(rms, 1e-30) + BF16_RTOL * np.abs(r)
+    d = np.abs(a - r)
+    bad = ~(d <= lim)
+    if bad.any():
+        i = np.unravel_index(np.argmax(d / lim), a.shape)
+        raise AssertionError(f"{what}: {int(bad.sum())} / {a.size} elements past the bf16 bound; "
+                             f"worst at {i}: got {a[i]!r} want {r[i]!r} (|Δ|/bound "
+                             f"{float(d[i] / lim[i]):.2f}, rms {rms:.3e})")
+    return float(np.max(d / lim)) if a.size else 0.0
 
 
 def rel_err(a, ref):
@@ -150,11 +175,9 @@ def test_bf16_forward_backward_vs_oracle(gpu_handle, case):
     ro, _, cache = O.forward(v["x"], v["w_off"], v["b_off"], v["w"], v["b"], s, (1, 1),
                              offsets=off)  # condition on the device's bf16 offsets
     rg = O.backward(cache, v["grad_out"])
-    errs = {"out": rel_err(out, ro)}
+    assert_bf16_close(out, ro, "out")
     for k in ("x", "weight", "bias", "offset_conv.weight", "offset_conv.bias", "offset"):
-        errs[k] = rel_err(g[k], rg[k])
-    bad = {k: e for k, e in errs.items() if not e <= BF16_TOL}
-    assert not bad, f"bf16 relative errors {errs}"
+        assert_bf16_close(g[k], rg[k], k)
 
 
 def test_bf16_config4_full_size_every_tensor(gpu_handle):
@@ -170,11 +193,31 @@ def test_bf16_config4_full_size_every_tensor(gpu_handle):
     desc = R.make_desc((64, 256, 28, 28), v["w"].shape, (1, 1), (1, 1))
     ro, roff = R.forward(desc, v["x"], v["w_off"], v["b_off"], v["w"], v["b"])
     rg = R.backward(desc, v["x"], off, v["w_off"], v["w"], v["grad_out"])
-    errs = {"out": rel_err(out, ro), "offset_values": rel_err(off, roff)}
+    # out: elementwise against the oracle sampling at the device's own (bf16-rounded)
+    # offsets; against the oracle's fp32 offsets (~4e-3 px apart) only in max-norm, since
+    # a sample moved by the offset rounding legitimately changes single elements by more
+    # than a bf16 ulp (r03: one of 12.8M elements by 0.034·rms)
+    ro_dev = R.forward_from_offsets(desc, v["x"], off, v["w"], v["b"])
+    worst = {"out": assert_bf16_close(out, ro_dev, "out"),
+             "offset_values": assert_bf16_close(off, roff, "offset values")}
+    assert rel_err(out, ro) <= BF16_TOL, "out vs the oracle's own offsets (max-norm)"
     for k in ("x", "offset", "weight", "bias", "offset_conv.weight", "offset_conv.bias"):
-        errs[k] = rel_err(g[k], rg[k])
-    bad = {k: e for k, e in errs.items() if not e <= BF16_TOL}
-    assert not bad, f"bf16 relative errors {errs}"
+        worst[k] = assert_bf16_close(g[k], rg[k], k)
+    print("config 4 worst |Δ|/bound per tensor:", {k: round(v_, 3) for k, v_ in worst.items()})
+
+
+def test_bf16_config4_full_size_bitwise_reproducible(gpu_handle):
+    """BASELINE config 4 per GPU at full size, forward + backward twice in one process: every
+    output bit for bit equal (the removed fused forward differed run to run
+    here; the shipped schedule has no float atomics and fixed summation orders)."""
+    bits, _, s = _case(12, B=64, C=256, O_=256, H=28, W=28, off_scale=1.5)
+    r1 = _device(gpu_handle, bits, s)
+    r2 = _device(gpu_handle, bits, s)
+    np.testing.assert_array_equal(r1[0].view(np.uint32), r2[0].view(np.uint32), err_msg="out")
+    np.testing.assert_array_equal(r1[1].view(np.uint32), r2[1].view(np.uint32), err_msg="off")
+    for k in r1[2]:
+        np.testing.assert_array_equal(r1[2][k].view(np.uint32), r2[2][k].view(np.uint32),
+                                      err_msg=k)
 
 
 @pytest.mark.parametrize("k,pad,C,H,W", [((1, 3), (0, 1), 24, 13, 11), ((3, 1), (1, 0), 24, 13, 11),
@@ -190,11 +233,9 @@ def test_bf16_nonsquare_kernels_vs_oracle(gpu_handle, k, pad, C, H, W):
     ro, _, cache = O.forward(v["x"], v["w_off"], v["b_off"], v["w"], v["b"], s, pad,
                              offsets=off)
     rg = O.backward(cache, v["grad_out"])
-    errs = {"out": rel_err(out, ro)}
+    assert_bf16_close(out, ro, "out")
     for name in ("x", "weight", "bias", "offset_conv.weight", "offset_conv.bias", "offset"):
-        errs[name] = rel_err(g[name], rg[name])
-    bad = {n: e for n, e in errs.items() if not e <= BF16_TOL}
-    assert not bad, f"bf16 relative errors {errs}"
+        assert_bf16_close(g[name], rg[name], name)
 
 
 def test_bf16_backward_with_attached_comm_single_rank(gpu_handle):

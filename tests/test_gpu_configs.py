@@ -112,6 +112,19 @@ def test_config3_full_batch_every_tensor_vs_c_oracle(gpu_handle):
     _check_all(out, off, g, ro, roff, rg, "config3")
 
 
+def test_config3_full_size_bitwise_reproducible(gpu_handle):
+    """Config 3 at full size, forward + backward twice in one process: every output bit for
+    bit equal (no float atomics; bins ordered by sample index; fixed-order partial sums)."""
+    c = _rand_case(62, B=64, C=256, O_=256, H=56, W=56, off_scale=1.5)
+    r1 = _device_fwd_bwd(gpu_handle, c)
+    r2 = _device_fwd_bwd(gpu_handle, c)
+    np.testing.assert_array_equal(r1[0].view(np.uint32), r2[0].view(np.uint32), err_msg="out")
+    np.testing.assert_array_equal(r1[1].view(np.uint32), r2[1].view(np.uint32), err_msg="off")
+    for k in r1[2]:
+        np.testing.assert_array_equal(r1[2][k].view(np.uint32), r2[2][k].view(np.uint32),
+                                      err_msg=k)
+
+
 # ---- config 5: B=64, C=O=512, 14x14, k3 s2 p1, dilation 2, deform_groups 4 ----------------
 
 def test_config5_full_batch_every_tensor_vs_c_oracle(gpu_handle):

@@ -10,6 +10,6 @@ for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VA
            "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_BUSY_CYCLES SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_SCA SQ_INSTS_VMEM" \
            ${EXTRA_SETS}; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $set --kernel-trace -d gpurun_out/pmcg_$i -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --math ${MATH:-6} > gpurun_out/pmcg_$i.log 2>&1 || { echo "pass $i failed"; tail -3 gpurun_out/pmcg_$i.log; }
+  timeout -s KILL 120 rocprofv3 --pmc $set --kernel-trace -d gpurun_out/pmcg_$i -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-strong --math ${MATH:-6} > gpurun_out/pmcg_$i.log 2>&1 || { echo "pass $i failed"; tail -3 gpurun_out/pmcg_$i.log; }
 done
 echo done

@@ -5,4 +5,4 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 [ -n "$2" ] && export DCN_EXP="$2"
-timeout -k 10 420 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$1 -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/prof_$1.log 2>&1 && echo "prof done"
+timeout -k 10 420 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$1 -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-strong > gpurun_out/prof_$1.log 2>&1 && echo "prof done"
