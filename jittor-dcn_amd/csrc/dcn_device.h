@@ -193,38 +193,26 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// Four 16x16x4 f32 MFMAs sharing the B operand, accumulators pinned in place ("+a": the
-// compiler's own MFMA code rotated loop-carried accumulators through AGPR copies). Wait
-// states (cdna_hip_programming.md §5.7 item 2): s_nop 1 for the just-written A/B VGPRs;
-// an accumulate chain D -> C needs none; mfma_drain() before anything else reads D.
+// Four 16x16x4 f32 MFMAs sharing the B operand / five sharing the A operand. Builtins, not
+// inline asm (r03): an asm MFMA is opaque to hipcc, which then neither pads the wait states
+// between it and the compiler's own accesses of its AGPRs / source VGPRs nor counts them
+// (cdna_hip_programming.md §5.7); r01-r02 shipped them as asm with hand-placed s_nops and
+// "+a" accumulators, which the register allocator could still copy between asm statements.
 __device__ __forceinline__ void mfma16x4_acc(f32x4& c0, f32x4& c1, f32x4& c2, f32x4& c3, float a0,
                                              float a1, float a2, float a3, float b) {
-  asm volatile(
-      "s_nop 1\n\t"
-      "v_mfma_f32_16x16x4_f32 %0, %4, %8, %0\n\t"
-      "v_mfma_f32_16x16x4_f32 %1, %5, %8, %1\n\t"
-      "v_mfma_f32_16x16x4_f32 %2, %6, %8, %2\n\t"
-      "v_mfma_f32_16x16x4_f32 %3, %7, %8, %3"
-      : "+a"(c0), "+a"(c1), "+a"(c2), "+a"(c3)
-      : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(b));
+  c0 = mfma16(a0, b, c0);
+  c1 = mfma16(a1, b, c1);
+  c2 = mfma16(a2, b, c2);
+  c3 = mfma16(a3, b, c3);
 }
-// Five 16x16x4 f32 MFMAs sharing the A operand (one M-tile against five N-tiles).
 __device__ __forceinline__ void mfma16x4_a5(f32x4& c0, f32x4& c1, f32x4& c2, f32x4& c3, f32x4& c4,
                                             float a, float b0, float b1, float b2, float b3,
                                             float b4) {
-  asm volatile(
-      "s_nop 1\n\t"
-      "v_mfma_f32_16x16x4_f32 %0, %5, %6, %0\n\t"
-      "v_mfma_f32_16x16x4_f32 %1, %5, %7, %1\n\t"
-      "v_mfma_f32_16x16x4_f32 %2, %5, %8, %2\n\t"
-      "v_mfma_f32_16x16x4_f32 %3, %5, %9, %3\n\t"
-      "v_mfma_f32_16x16x4_f32 %4, %5, %10, %4"
-      : "+a"(c0), "+a"(c1), "+a"(c2), "+a"(c3), "+a"(c4)
-      : "v"(a), "v"(b0), "v"(b1), "v"(b2), "v"(b3), "v"(b4));
-}
-// 12 wait states (8-pass XDL) between the last asm MFMA and any other access to its D.
-__device__ __forceinline__ void mfma_drain(f32x4& c0, f32x4& c1, f32x4& c2, f32x4& c3) {
-  asm volatile("s_nop 11" : "+a"(c0), "+a"(c1), "+a"(c2), "+a"(c3));
+  c0 = mfma16(a, b0, c0);
+  c1 = mfma16(a, b1, c1);
+  c2 = mfma16(a, b2, c2);
+  c3 = mfma16(a, b3, c3);
+  c4 = mfma16(a, b4, c4);
 }
 
 // Row of D[row][col] held in register r by lane half hi, for 32x32 MFMA tiles.

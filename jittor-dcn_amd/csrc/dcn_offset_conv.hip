@@ -652,8 +652,6 @@ __global__ __launch_bounds__(256) void offset_wgrad_mfma(Geo g, const XT* __rest
       }
     }
   }
-#pragma unroll
-  for (int u = 0; u < NTW; ++u) mfma_drain(acc[0][u], acc[1][u], acc[2][u], acc[3][u]);
   float* pp = part + (size_t)chunk * g.C * TJ;
 #pragma unroll
   for (int u = 0; u < NTW; ++u) {
@@ -743,9 +741,6 @@ __global__ __launch_bounds__(256) void offset_wgrad_mfma_m1(Geo g, const float* 
       }
     }
   }  // chunks
-  mfma_drain(acc[0], acc[1], acc[2], acc[3]);
-  mfma_drain(acc[4], acc[5], acc[6], acc[7]);
-  mfma_drain(acc[8], acc[9], acc[0], acc[1]);
   float* pp = part + (size_t)grp * g.C * TJ;
   // D: row (channel cw + 4q + r), column (tap column 16t + n)
 #pragma unroll
@@ -861,8 +856,6 @@ __global__ __launch_bounds__(256, 4) void offset_dgrad_mfma(Geo g, const float* 
       lda(ks + kPf, ra[d]);
     }
   }
-#pragma unroll
-  for (int u = 0; u < 4; ++u) mfma_drain(acc[0][u], acc[1][u], acc[2][u], acc[3][u]);
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int pl = 16 * u + n;

@@ -534,20 +534,22 @@ __global__ __launch_bounds__(256) void offgrad_cl(Geo g, LaneMap L, const float*
 // config-3 step on the side stream, 0.60 of it in the rank loop):
 //   bins_chunk_sort  a segment's samples in chunks of kBinChunk: each chunk's bins are
 //                    computed from the offsets and sorted in LDS (rocprim block radix sort,
-//                    stable, so equal bins keep ascending s); the chunk's sorted list and
-//                    its per-bin run lengths H[seg][bin][chunk] are written;
-//   bins_scan_table  one workgroup per segment: exclusive scan of H in (bin, chunk) order
-//                    = every (bin, chunk) run's first position in the segment's bin order;
-//                    start[bin] = the bin's first position;
-//   bins_emit        each chunk places its sorted samples at base + rank in run: the packed
-//                    records of the fused K5 (brec) or the sorted sample lists (slist).
+//                    stable, so equal bins keep ascending s); the chunk's sorted entries
+//                    {bin, index, fr, fc} are written, and per bin present its run length
+//                    H[seg][chunk][bin] and run start R[seg][chunk][bin];
+//   bins_scan_table  one workgroup per segment: H becomes each (chunk, bin) run's first
+//                    position in the segment's bin order (bin-major, chunk-minor), start[bin]
+//                    each bin's first position; every access a coalesced 16-B one;
+//   bins_emit        one thread per bin copies the bin's runs, chunk by chunk, to its output
+//                    range: the packed records of the fused K5 (brec) or the sorted sample
+//                    lists (slist), written in output order.
 // ---------------------------------------------------------------------------
-constexpr int kBinT = 256, kBinIPT = 8, kBinChunk = kBinT * kBinIPT;
-constexpr int kBinLBits = 11;  // sample index within a chunk (< 2048) in a packed entry
+constexpr int kBinT = 256, kBinIPT = 16, kBinChunk = kBinT * kBinIPT;
+constexpr int kBinLBits = 12;  // sample index within a chunk (< 4096) in a packed entry
 static_assert(kBinChunk == 1 << kBinLBits, "packed entry layout");
 
-// H row length: NB bins plus the sentinel NB (whose start is the end of the last bin), padded
-// to a multiple of 4 for the 16-B accesses of bins_scan_table
+// H / R row length: NB bins plus the sentinel NB (whose start is the end of the last bin),
+// padded to a multiple of 4 for the 16-B accesses of bins_scan_table
 __host__ __device__ __forceinline__ int bins_nbp(int NB) { return (NB + 1 + 3) / 4 * 4; }
 
 __device__ __forceinline__ unsigned sample_bin(const Geo& g, const float* __restrict__ off, int b,
@@ -559,12 +561,13 @@ __device__ __forceinline__ unsigned sample_bin(const Geo& g, const float* __rest
 
 __global__ __launch_bounds__(kBinT) void bins_chunk_sort(Geo g, const float* __restrict__ off,
                                                          int b0, int nch, int NB, unsigned kbits,
-                                                         int* __restrict__ H,
-                                                         unsigned* __restrict__ sorted,
+                                                         int* __restrict__ H, int* __restrict__ R,
+                                                         uint4* __restrict__ sorted,
                                                          float4* __restrict__ rec) {
   using Sort = rocprim::block_radix_sort<unsigned, kBinT, kBinIPT, unsigned short>;
   __shared__ typename Sort::storage_type sst;
   __shared__ unsigned skey[kBinChunk];
+  __shared__ float2 frfc[kBinChunk];
   const int tid = threadIdx.x, ch = blockIdx.x, bg = blockIdx.y;
   const int NS = g.HW * g.N, gi = bg % g.G, b = b0 + bg / g.G;
   unsigned key[kBinIPT];
@@ -573,25 +576,28 @@ __global__ __launch_bounds__(kBinT) void bins_chunk_sort(Geo g, const float* __r
   for (int u = 0; u < kBinIPT; ++u) {
     const int l = tid * kBinIPT + u, s = ch * kBinChunk + l;
     val[u] = (unsigned short)l;
-    if (s < NS) {
-      Tap t;
-      key[u] = sample_bin(g, off, b, gi, s, NB, &t);
-      if (rec)  // dx_gather_cl's per-sample records (the unfused K5 only)
-        rec[(size_t)bg * NS + s] = make_float4(__int_as_float(t.ok ? (int)key[u] : -1), t.fr, t.fc, 0.f);
-    } else {
-      key[u] = (unsigned)NB + 1;  // past the end: after every bin and the invalid samples
-    }
+    Tap t;
+    t.ok = false;
+    t.fr = t.fc = 0.f;
+    key[u] = s < NS ? sample_bin(g, off, b, gi, s, NB, &t)
+                    : (unsigned)NB + 1;  // past the end: after every bin and the invalid samples
+    frfc[l] = make_float2(t.fr, t.fc);
+    if (rec && s < NS)  // dx_gather_cl's per-sample records (the unfused K5 only)
+      rec[(size_t)bg * NS + s] = make_float4(__int_as_float(t.ok ? (int)key[u] : -1), t.fr, t.fc, 0.f);
   }
   Sort().sort(key, val, sst, 0, kbits);  // blocked result: thread t holds ranks t*IPT + u
-  unsigned* out = sorted + ((size_t)bg * nch + ch) * kBinChunk;
+  uint4* out = sorted + ((size_t)bg * nch + ch) * kBinChunk;
+#pragma unroll
+  for (int u = 0; u < kBinIPT; ++u) skey[tid * kBinIPT + u] = key[u];
+  __syncthreads();  // skey complete; frfc was complete before the sort's own barriers
 #pragma unroll
   for (int u = 0; u < kBinIPT; ++u) {
-    skey[tid * kBinIPT + u] = key[u];
-    out[tid * kBinIPT + u] = (key[u] << kBinLBits) | val[u];
+    const float2 f = frfc[val[u]];
+    out[tid * kBinIPT + u] =
+        make_uint4((key[u] << kBinLBits) | val[u], __float_as_uint(f.x), __float_as_uint(f.y), 0u);
   }
-  __syncthreads();
-  // run lengths: the thread holding a run's first entry counts it (runs are short)
-  int* Hb = H + ((size_t)bg * nch + ch) * bins_nbp(NB);
+  // run lengths and starts: the thread holding a run's first entry counts it (runs are short)
+  const size_t row = ((size_t)bg * nch + ch) * bins_nbp(NB);
 #pragma unroll
   for (int u = 0; u < kBinIPT; ++u) {
     const int i = tid * kBinIPT + u;
@@ -599,12 +605,13 @@ __global__ __launch_bounds__(kBinT) void bins_chunk_sort(Geo g, const float* __r
     if (k < (unsigned)NB && (i == 0 || skey[i - 1] != k)) {
       int c = 1;
       while (i + c < kBinChunk && skey[i + c] == k) ++c;
-      Hb[k] = c;
+      H[row + k] = c;
+      R[row + k] = i;
     }
   }
 }
 
-// One workgroup per segment: the (bin, chunk) runs in bin-major order get their first
+// One workgroup per segment: the (chunk, bin) runs in bin-major order get their first
 // positions in the segment's bin order. H is chunk-major ([chunk][bin], bins padded to a
 // multiple of 4), so thread t owns bins 4t..4t+3 and every access is a coalesced 16-B one:
 // pass 1 sums each bin over the chunks, a block scan over the bins gives start[bin], pass 2
@@ -622,11 +629,13 @@ __global__ __launch_bounds__(1024) void bins_scan_table(int NB, int nch, int* __
     const int bb = b0 + 4 * tid;
     const bool act = bb < NBp;
     int4 tot = make_int4(0, 0, 0, 0);
-    if (act)
+    if (act) {
+#pragma unroll 8
       for (int c = 0; c < nch; ++c) {
         const int4 v = *reinterpret_cast<const int4*>(Hs + (size_t)c * NBp + bb);
         tot.x += v.x; tot.y += v.y; tot.z += v.z; tot.w += v.w;
       }
+    }
     const int local = tot.x + tot.y + tot.z + tot.w;
     int v = local;  // inclusive scan over the block
     for (int o = 1; o < 64; o <<= 1) {
@@ -652,6 +661,7 @@ __global__ __launch_bounds__(1024) void bins_scan_table(int NB, int nch, int* __
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         if (bb + i <= NB) st[bb + i] = run[i];
+#pragma unroll 8
       for (int c = 0; c < nch; ++c) {
         int4* p = reinterpret_cast<int4*>(Hs + (size_t)c * NBp + bb);
         const int4 hv = *p;
@@ -663,44 +673,60 @@ __global__ __launch_bounds__(1024) void bins_scan_table(int NB, int nch, int* __
   }
 }
 
-// Places each chunk's sorted samples: position = base[bin][chunk] + rank within the run.
+// One thread per bin: its runs (chunk by chunk, each already in ascending s) go to the bin's
+// output range in order; a run's length is the next chunk's first position minus its own.
 // brec (fused K5): {∂colT row offset m*K + n*C, fr, fc, ∂offset index n*HW + m}; else
 // slist (dx_gather_cl): the sample index.
-__global__ __launch_bounds__(kBinT) void bins_emit(Geo g, const float* __restrict__ off, int b0,
-                                                   int nch, int NB, const int* __restrict__ H,
-                                                   const unsigned* __restrict__ sorted,
-                                                   int4* __restrict__ brec,
-                                                   int* __restrict__ slist) {
-  __shared__ unsigned skey[kBinChunk];
-  const int tid = threadIdx.x, ch = blockIdx.x, bg = blockIdx.y;
-  const int NS = g.HW * g.N, gi = bg % g.G, b = b0 + bg / g.G;
-  const unsigned* in = sorted + ((size_t)bg * nch + ch) * kBinChunk;
-  unsigned e[kBinIPT];
-#pragma unroll
-  for (int u = 0; u < kBinIPT; ++u) {
-    e[u] = in[tid * kBinIPT + u];
-    skey[tid * kBinIPT + u] = e[u] >> kBinLBits;
-  }
-  __syncthreads();
-  const int* Hb = H + ((size_t)bg * nch + ch) * bins_nbp(NB);
-#pragma unroll
-  for (int u = 0; u < kBinIPT; ++u) {
-    const int i = tid * kBinIPT + u;
-    const unsigned k = e[u] >> kBinLBits;
-    if (k >= (unsigned)NB) continue;  // invalid sample or chunk padding (sorted last)
-    int j = i;
-    while (j > 0 && skey[j - 1] == k) --j;
-    const size_t pos = (size_t)bg * NS + Hb[k] + (i - j);
-    const int s = ch * kBinChunk + (int)(e[u] & (kBinChunk - 1));
-    if (brec) {
-      Tap t;
-      sample_bin(g, off, b, gi, s, NB, &t);
-      const int m = s / g.N, n = s - m * g.N;
-      brec[pos] = make_int4(m * g.K + n * g.C, __float_as_int(t.fr), __float_as_int(t.fc),
-                            n * g.HW + m);
-    } else {
-      slist[pos] = s;
+__global__ __launch_bounds__(256) void bins_emit(Geo g, int nch, int NB,
+                                                 const int* __restrict__ H,
+                                                 const int* __restrict__ R,
+                                                 const int* __restrict__ start,
+                                                 const uint4* __restrict__ sorted,
+                                                 int4* __restrict__ brec,
+                                                 int* __restrict__ slist) {
+  const int bin = blockIdx.x * 256 + threadIdx.x, bg = blockIdx.y;
+  if (bin >= NB) return;
+  const int NS = g.HW * g.N, NBp = bins_nbp(NB);
+  const int* Hs = H + (size_t)bg * nch * NBp + bin;
+  const int* Rs = R + (size_t)bg * nch * NBp + bin;
+  const uint4* so = sorted + (size_t)bg * nch * kBinChunk;
+  const int* stb = start + (size_t)bg * (NB + 1);
+  auto copy_run = [&](int c, int pos, int n, int r) {
+    const uint4* src = so + (size_t)c * kBinChunk + r;
+    for (int j = 0; j < n; ++j) {
+      const uint4 e = src[j];
+      const int s = c * kBinChunk + (int)(e.x & (kBinChunk - 1));
+      const size_t o = (size_t)bg * NS + pos + j;
+      if (brec) {
+        const int m = s / g.N, tap = s - m * g.N;
+        brec[o] = make_int4(m * g.K + tap * g.C, (int)e.y, (int)e.z, tap * g.HW + m);
+      } else {
+        slist[o] = s;
+      }
     }
+  };
+  constexpr int kPre = 8;  // chunks whose run positions / starts are loaded up front
+  if (nch <= kPre) {
+    int hb[kPre + 1], rr[kPre];
+#pragma unroll
+    for (int c = 0; c < kPre; ++c) {
+      hb[c] = c < nch ? Hs[(size_t)c * NBp] : 0;
+      rr[c] = c < nch ? Rs[(size_t)c * NBp] : 0;
+    }
+    hb[kPre] = stb[bin + 1];
+#pragma unroll
+    for (int c = 0; c < kPre; ++c) {
+      if (c >= nch) break;
+      const int next = c + 1 < nch ? hb[c + 1] : hb[kPre];
+      if (next > hb[c]) copy_run(c, hb[c], next - hb[c], rr[c]);
+    }
+    return;
+  }
+  int pos = Hs[0];
+  for (int c = 0; c < nch; ++c) {
+    const int next = c + 1 < nch ? Hs[(size_t)(c + 1) * NBp] : stb[bin + 1];
+    if (next > pos) copy_run(c, pos, next - pos, Rs[(size_t)c * NBp]);
+    pos = next;
   }
 }
 
@@ -1175,15 +1201,16 @@ static bool can_vec4(const Geo& g) { return g.C % 4 == 0 && g.Cg % 4 == 0; }
 static int bins_nch(const Geo& g) { return (g.HW * g.N + kBinChunk - 1) / kBinChunk; }
 static bool k5_fused(const Geo& g);
 
-// Bins workspace: start[seg][NB+1] | H[seg][NB][nch] | sorted[seg][nch][kBinChunk] |
-// rec[seg][NS] (unfused K5 only) | brec[seg][NS] (int4; slist, int, for the unfused K5).
+// Bins workspace: start[seg][NB+1] | H[seg][nch][NBp] | R[seg][nch][NBp] |
+// sorted[seg][nch][kBinChunk] (16 B) | rec[seg][NS] (unfused K5 only) | brec[seg][NS] (int4;
+// slist, int, for the unfused K5).
 size_t bins_ws_bytes(const Geo& g, int nb) {
   const size_t NB = (size_t)(g.H + 1) * (g.W + 1), NS = (size_t)g.HW * g.N;
   const size_t seg = (size_t)nb * g.G, nch = bins_nch(g);
   auto al = [](size_t v) { return (v + 255) / 256 * 256; };
   size_t b = al(seg * (NB + 1) * 4);
-  b += al(seg * nch * bins_nbp((int)NB) * 4);
-  b += al(seg * nch * kBinChunk * 4);
+  b += 2 * al(seg * nch * bins_nbp((int)NB) * 4);
+  b += al(seg * nch * kBinChunk * 16);
   if (!k5_fused(g)) b += al(seg * NS * 16);
   b += al(seg * NS * 16);
   return b;
@@ -1234,8 +1261,8 @@ static bool k5_fused(const Geo& g) {
 
 // Pointers into the bins workspace (bins_ws_bytes layout).
 struct BinsWs {
-  int *start, *H, *slist;
-  unsigned* sorted;
+  int *start, *H, *R, *slist;
+  uint4* sorted;
   float4* rec;
   int4* brec;
 };
@@ -1249,8 +1276,10 @@ static BinsWs bins_ptrs(const Geo& g, void* bins_ws, int nb) {
   w += al(seg * (NB + 1) * 4);
   P.H = reinterpret_cast<int*>(w);
   w += al(seg * nch * bins_nbp((int)NB) * 4);
-  P.sorted = reinterpret_cast<unsigned*>(w);
-  w += al(seg * nch * kBinChunk * 4);
+  P.R = reinterpret_cast<int*>(w);
+  w += al(seg * nch * bins_nbp((int)NB) * 4);
+  P.sorted = reinterpret_cast<uint4*>(w);
+  w += al(seg * nch * kBinChunk * 16);
   P.rec = nullptr;
   if (!k5_fused(g)) {
     P.rec = reinterpret_cast<float4*>(w);
@@ -1271,14 +1300,14 @@ hipError_t launch_bins(const Geo& g, const float* off, void* bins_ws, float* gof
   const size_t seg = (size_t)nb * g.G;
   const BinsWs P = bins_ptrs(g, bins_ws, nb);
   const bool fused = k5_fused(g);
+  // H must start at 0 (only the bins present in a chunk are written); R needs no init
   hipError_t e = hipMemsetAsync(P.H, 0, seg * nch * bins_nbp(NB) * sizeof(int), s);
   if (e != hipSuccess) return e;
-  const dim3 grid(nch, (unsigned)seg);
-  hipLaunchKernelGGL(bins_chunk_sort, grid, dim3(kBinT), 0, s, g, off, b0, nch, NB, kbits, P.H,
-                     P.sorted, fused ? nullptr : P.rec);
+  hipLaunchKernelGGL(bins_chunk_sort, dim3(nch, (unsigned)seg), dim3(kBinT), 0, s, g, off, b0, nch,
+                     NB, kbits, P.H, P.R, P.sorted, fused ? nullptr : P.rec);
   hipLaunchKernelGGL(bins_scan_table, dim3((unsigned)seg), dim3(1024), 0, s, NB, nch, P.H, P.start);
-  hipLaunchKernelGGL(bins_emit, grid, dim3(kBinT), 0, s, g, off, b0, nch, NB, P.H, P.sorted,
-                     fused ? P.brec : nullptr, P.slist);
+  hipLaunchKernelGGL(bins_emit, dim3((NB + 255) / 256, (unsigned)seg), dim3(256), 0, s, g, nch, NB,
+                     P.H, P.R, P.start, P.sorted, fused ? P.brec : nullptr, P.slist);
   if (fused) {
     // samples in no bin (every corner outside the image) have ∂offset 0
     e = hipMemsetAsync(goff + (size_t)b0 * g.J * g.HW, 0, (size_t)nb * g.J * g.HW * sizeof(float),
