@@ -390,7 +390,7 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
   // main stream runs the ∂W / ∂col GEMMs
   DCN_TRY(fork_aux(h));
   // (r02 A/B: the bins serialised before K5 instead: step 7.06 against 7.00-7.02 ms)
-  HIP_TRY(dcn::launch_bins(g, off, bins, goff, 0, g.B, dcn::exp_flag(0) == 1 ? h->stream : h->aux));
+  HIP_TRY(dcn::launch_bins(g, off, bins, goff, 0, g.B, h->aux));
   if (!col_valid) {
     {
       ProfScope ps(h, DCN_K_XPOSE);
@@ -573,7 +573,7 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
   }
   DCN_TRY(fork_aux(h));
   HIP_TRY(dcn::launch_bins(g, off32, base + L.bins, goff32, 0, g.B,
-                           dcn::exp_flag(0) == 1 ? h->stream : h->aux));
+                           h->aux));
   if (!col_valid) {
     {
       ProfScope ps(h, DCN_K_XPOSE);
