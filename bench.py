@@ -596,26 +596,31 @@ def host_path_rate(cfg, config, steps=4):
     w = (rng.standard_normal((O_, C, k, k)) * np.sqrt(2 / (C * N))).astype(np.float32)
     b = (rng.standard_normal(O_) * 0.1).astype(np.float32)
     h = rt.Handle(0)
+    st = rt.HostState(h)  # what a DeformConv2d module holds (deform_conv.py host_state)
     Ho, Wo = rt.out_shape(rt.make_desc(B, C, H, W, O_, (k, k), (s, s), (p, p)))
     gout = rng.standard_normal((B, O_, Ho, Wo), dtype=np.float32)
     fwd_only = cfg.get("fwd_only", False)
 
     def step():
-        out, off, ctx = dcn_forward_numpy(x, wo, bo, w, b, (s, s), (p, p), handle=h,
+        out, off, ctx = dcn_forward_numpy(x, wo, bo, w, b, (s, s), (p, p), state=st,
                                           return_ctx=True)
         if not fwd_only:
-            dcn_backward_numpy(x, off, wo, w, True, gout, (s, s), (p, p), handle=h, ctx=ctx)
+            dcn_backward_numpy(x, off, wo, w, True, gout, (s, s), (p, p), ctx=ctx,
+                               offset_grad=False)
 
     step()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     el = (time.perf_counter() - t0) / steps
+    st.close()
     h.close()
     moved = (x.nbytes + gout.nbytes * (0 if fwd_only else 1) + B * O_ * Ho * Wo * 4
              + B * 2 * N * Ho * Wo * 4 + (0 if fwd_only else x.nbytes))
-    return {"what": "host-pointer API (NumPy arrays in, NumPy arrays out): dcn_forward_host"
-                    + ("" if fwd_only else " + dcn_backward_host_ex(DCN_HOST_REUSE_FWD)"),
+    return {"what": "host-pointer API (NumPy arrays in, NumPy arrays out) on a module's host "
+                    "state: dcn_forward_host_s"
+                    + ("" if fwd_only else " + dcn_backward_host_s(DCN_HOST_REUSE_FWD)")
+                    + ", image-chunk transfer pipeline (auto chunks)",
             "config": f"config{config}", "steps": steps, "ms_per_step": round(el * 1e3, 3),
             "value": round(B * Ho * Wo * N / el / 1e9, 5), "unit": "Gsamples/s",
             "pcie_bytes_per_step": int(moved),

@@ -36,8 +36,8 @@
 extern "C" {
 #endif
 
-#define DCN_ABI_VERSION 3 /* 2: dcn_allreduce_grads takes a dtype; dcn_set_comm, dcn_set_grad_stream;
-                             3: dcn_backward_host_ex */
+#define DCN_ABI_VERSION 4 /* 2: dcn_allreduce_grads takes a dtype; dcn_set_comm, dcn_set_grad_stream;
+                             3: dcn_backward_host_ex; 4: dcn_host_state */
 
 typedef enum {
   DCN_OK = 0,
@@ -147,9 +147,17 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x,
 
 /* Host-pointer variants (NumPy / Jittor-CPU callers, the reference caller's path:
  * train.py:408-414 through the module). Synchronous. Device copies of the tensors are
- * kept on the handle between calls (no per-call allocation); transfers run straight from /
- * to the caller's memory (env DCN_HOST_STAGING=1: through a pinned ring with host copy
- * threads instead, which pays for destinations whose pages were never touched). */
+ * kept between calls (no per-call allocation); transfers run straight from / to the
+ * caller's memory (env DCN_HOST_STAGING=1: through a pinned ring with host copy threads
+ * instead, which pays for destinations whose pages were never touched).
+ *
+ * The batch is cut into image chunks whose transfers run beside the kernels (the upload
+ * of chunk i+1 and the download of chunk i-1 while chunk i computes). fp32 only: about
+ * 24 MB of x per chunk, at most 16 chunks (dcn_host_state_set_chunks); bf16 and a handle
+ * with a communicator use one chunk. With several chunks the parameter gradients are
+ * the chunk partials summed in chunk order (deterministic; not bitwise the one-chunk
+ * sums). The dcn_*_host calls below use the handle's own host state; a network of
+ * several modules on one handle gives each module its own (dcn_host_state_create). */
 int dcn_forward_host(dcn_handle* h, const dcn_desc* d, const float* x,
                      const float* w_off, const float* b_off, const float* w,
                      const float* b, float* out, float* off);
@@ -170,6 +178,29 @@ int dcn_backward_host_ex(dcn_handle* h, const dcn_desc* d, const float* x,
                          const float* grad_out, float* grad_x, float* grad_w,
                          float* grad_b, float* grad_w_off, float* grad_b_off,
                          float* grad_off_out, int flags);
+
+/* Per-module host state (ABI 4). One per DeformConv2d module (train.py:304-318 stacks
+ * four on one handle): the device copies of that module's x / offsets / weights and its
+ * own workspace, which keeps the forward's columns. A dcn_backward_host_s with
+ * DCN_HOST_REUSE_FWD given the arrays of the state's last forward reuses them, whatever
+ * other states ran on the handle in between (DCN_ERR_INVALID for other arrays; `off` may
+ * then be NULL if the forward was given NULL). States belong to their handle:
+ * dcn_destroy frees their device memory, after which only dcn_host_state_destroy accepts
+ * them. The handle-level dcn_*_host calls use a state of the handle's own. */
+typedef struct dcn_host_state dcn_host_state;
+int dcn_host_state_create(dcn_handle* h, dcn_host_state** out);
+int dcn_host_state_destroy(dcn_host_state* s);
+/* image chunks of the transfer pipeline: 0 = auto (the default), else min(chunks, B, 16);
+ * fp32 only (bf16 and a communicator: always 1). */
+int dcn_host_state_set_chunks(dcn_host_state* s, int chunks);
+int dcn_forward_host_s(dcn_host_state* s, const dcn_desc* d, const float* x,
+                       const float* w_off, const float* b_off, const float* w,
+                       const float* b, float* out, float* off);
+int dcn_backward_host_s(dcn_host_state* s, const dcn_desc* d, const float* x,
+                        const float* off, const float* w_off, const float* w,
+                        const float* grad_out, float* grad_x, float* grad_w,
+                        float* grad_b, float* grad_w_off, float* grad_b_off,
+                        float* grad_off_out, int flags);
 
 /* ---- deformable RoI pooling -------------------------------- *
  * DeformRoIPool (deform_conv.py:85-159) and DeformPSRoIPool (:162-241), fp32.

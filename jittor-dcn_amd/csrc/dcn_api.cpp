@@ -194,19 +194,19 @@ struct dcn_handle {
   hipStream_t comm_stream = nullptr;
   hipStream_t grad_stream = nullptr;  // caller's stream to release at ∂W/∂b-final
   hipEvent_t dw_main = nullptr, dw_aux = nullptr, end_ev = nullptr, comm_done = nullptr;
-  // handle-owned workspace (host-pointer API) and scratch (standalone kernel API)
-  void* ws = nullptr;
-  size_t ws_bytes = 0;
-  // host-pointer API: persistent device copies of the caller's tensors (grow-only, one
-  // per role), the pinned staging ring, and what the last dcn_forward_host left on the
-  // device for a dcn_backward_host_ex(DCN_HOST_REUSE_FWD)
+  // host-pointer API: device copies of the tensors no module state keeps (outputs and
+  // gradients, grow-only, one per role), the pinned staging ring, the per-module states
+  // (dcn_host_state, hs0 = the one dcn_forward_host / dcn_backward_host[_ex] use), and the
+  // copy streams + events of the image-chunk transfer pipeline
   void* hbuf[16] = {nullptr};
   size_t hbuf_bytes[16] = {0};
   dcn::HostStage* stage = nullptr;
   int staging = -1;  // DCN_HOST_STAGING, read at the first host transfer
-  bool hfwd_valid = false;
-  dcn_desc hfwd_desc{};
-  const void *hfwd_x = nullptr, *hfwd_wo = nullptr, *hfwd_w = nullptr, *hfwd_off = nullptr;
+  dcn_host_state* hs0 = nullptr;
+  std::vector<dcn_host_state*> states;
+  hipStream_t cin = nullptr, cout = nullptr;
+  std::vector<hipEvent_t> hev;  // [2*i] chunk i uploaded, [2*i+1] chunk i computed
+  // scratch of the standalone kernel API
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
   // profiling: events per kernel class
@@ -214,6 +214,28 @@ struct dcn_handle {
   std::vector<hipEvent_t> ev[DCN_K_COUNT];  // pairs: [2*i] start, [2*i+1] stop
   int prof_n[DCN_K_COUNT] = {0};
 };
+
+enum StateRole { SB_X, SB_OFF, SB_WO, SB_W, SB_COUNT };
+
+// One module's device state for the host-pointer API (include/dcn.h dcn_host_state): its
+// x / offsets / weights, its workspace (one slice per image chunk, each holding that
+// chunk's columns for the backward) and what its last forward was given.
+struct dcn_host_state {
+  dcn_handle* h = nullptr;  // null once the handle is destroyed
+  void* dev[SB_COUNT] = {nullptr};
+  size_t dev_bytes[SB_COUNT] = {0};
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  int chunks = 0;  // dcn_host_state_set_chunks; 0 = auto
+  bool valid = false;
+  int plan_n = 1;  // image chunks of the last forward
+  dcn_desc desc{};
+  const void *x = nullptr, *wo = nullptr, *w = nullptr, *off = nullptr;
+};
+
+namespace {
+void state_free(dcn_host_state* s);
+}  // namespace
 
 namespace dcn {
 int exp_flag(int i) {
@@ -747,10 +769,21 @@ int dcn_destroy(dcn_handle* h) {
   if (h->comm) dcn_internal_handle_drop_comm(h);
   for (auto& v : h->ev)
     for (hipEvent_t e : v) (void)hipEventDestroy(e);
-  if (h->ws) (void)hipFree(h->ws);
   if (h->scratch) (void)hipFree(h->scratch);
   for (void* p : h->hbuf)
     if (p) (void)hipFree(p);
+  // the caller's states stay valid objects that only dcn_host_state_destroy accepts
+  for (dcn_host_state* s : h->states) {
+    state_free(s);
+    s->h = nullptr;
+  }
+  if (h->hs0) {
+    state_free(h->hs0);
+    delete h->hs0;
+  }
+  for (hipEvent_t e : h->hev) (void)hipEventDestroy(e);
+  for (hipStream_t s : {h->cin, h->cout})
+    if (s) (void)hipStreamDestroy(s);
   delete h->stage;
   if (h->aux) (void)hipStreamSynchronize(h->aux);
   dcn::gemm_engine_destroy(h->gemm);
@@ -1018,47 +1051,63 @@ struct DevBufs {
 };
 
 enum HostRole {
-  HB_X, HB_WO, HB_BO, HB_W, HB_B, HB_OUT, HB_OFF,
-  HB_GO, HB_GX, HB_GW, HB_GB, HB_GWO, HB_GBO, HB_GOFF, HB_COUNT
+  HB_BO, HB_B, HB_OUT, HB_GO, HB_GX, HB_GPAR, HB_PART, HB_GOFF, HB_COUNT
 };
 
-int host_buf(dcn_handle* h, int role, size_t bytes, float** p) {
+int grow(dcn_handle* h, void** p, size_t* have, size_t bytes) {
   bytes = bytes ? bytes : 4;
-  if (h->hbuf_bytes[role] < bytes) {
-    if (h->hbuf[role]) {
-      HIP_TRY(hipStreamSynchronize(h->stream));
-      HIP_TRY(hipFree(h->hbuf[role]));
-    }
-    h->hbuf[role] = nullptr;
-    h->hbuf_bytes[role] = 0;
-    HIP_TRY(hipMalloc(&h->hbuf[role], bytes));
-    h->hbuf_bytes[role] = bytes;
+  if (*have >= bytes) return DCN_OK;
+  if (*p) {
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hipFree(*p));
   }
-  *p = static_cast<float*>(h->hbuf[role]);
+  *p = nullptr;
+  *have = 0;
+  HIP_TRY(hipMalloc(p, bytes));
+  *have = bytes;
   return DCN_OK;
 }
 
-int ensure_ws(dcn_handle* h, size_t bytes) {
-  if (h->ws_bytes >= bytes) return DCN_OK;
-  h->hfwd_valid = false;  // the forward's columns go with the old workspace
-  if (h->ws) {
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    HIP_TRY(hipFree(h->ws));
-  }
-  h->ws = nullptr;
-  h->ws_bytes = 0;
-  HIP_TRY(hipMalloc(&h->ws, bytes));
-  h->ws_bytes = bytes;
+int host_buf(dcn_handle* h, int role, size_t bytes, char** p) {
+  DCN_TRY(grow(h, &h->hbuf[role], &h->hbuf_bytes[role], bytes));
+  *p = static_cast<char*>(h->hbuf[role]);
   return DCN_OK;
+}
+}  // namespace
+
+namespace {
+void state_free(dcn_host_state* s) {
+  for (void*& p : s->dev) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+  }
+  if (s->ws) (void)hipFree(s->ws);
+  s->ws = nullptr;
+  s->ws_bytes = 0;
+  s->valid = false;
+}
+
+int state_buf(dcn_host_state* s, int role, size_t bytes, char** p) {
+  DCN_TRY(grow(s->h, &s->dev[role], &s->dev_bytes[role], bytes));
+  *p = static_cast<char*>(s->dev[role]);
+  return DCN_OK;
+}
+
+int state_ws(dcn_host_state* s, size_t bytes) {
+  if (s->ws_bytes < bytes) s->valid = false;  // the forward's columns go with the old workspace
+  return grow(s->h, &s->ws, &s->ws_bytes, bytes);
 }
 
 // Transfers go straight from / to the caller's pageable memory by default: on the MI355X
 // box that runs at 54 GB/s both ways when the host pages are resident (tools/pcie_probe.py;
 // pinned: 57 GB/s), and the Python shim hands out recycled, resident output arrays
-// (hostmem.py). DCN_HOST_STAGING=1 routes them through the pinned ring and copy threads
-// instead (DCN_HOST_THREADS, default 8; DCN_HOST_CHUNK_MB, default 32): that pays only for
-// destinations never touched before (page faults: 8.9 GB/s direct, 16 GB/s with 16
-// threads).
+// (hostmem.py). A pageable copy blocks the calling thread until it is done, and an upload
+// and a download do not run at the same time even pinned (tools/pcie_overlap.py: 205 MB
+// each way, 3.6 ms alone, 7.3 ms together), while kernels queued before a copy keep running
+// beside it (a 6.1 ms GEMM + both copies: 7.4 ms). DCN_HOST_STAGING=1 routes the copies
+// through the pinned ring and copy threads instead (DCN_HOST_THREADS, default 8;
+// DCN_HOST_CHUNK_MB, default 32): that pays only for destinations never touched before
+// (page faults: 8.9 GB/s direct, 16 GB/s with 16 threads).
 bool staging_on(dcn_handle* h) {
   if (h->staging < 0) {  // read once per handle, at its first host transfer
     const char* e = std::getenv("DCN_HOST_STAGING");
@@ -1084,124 +1133,321 @@ int get_stage(dcn_handle* h, dcn::HostStage** st) {
   return DCN_OK;
 }
 
-int h2d(dcn_handle* h, float* dst, const float* src, size_t bytes) {
+int h2d(dcn_handle* h, hipStream_t s, void* dst, const void* src, size_t bytes) {
+  if (!bytes) return DCN_OK;
   if (!staging_on(h)) {
-    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
     return DCN_OK;
   }
   dcn::HostStage* st;
   DCN_TRY(get_stage(h, &st));
-  HIP_TRY(st->h2d(dst, src, bytes, h->stream));
+  HIP_TRY(st->h2d(dst, src, bytes, s));
   return DCN_OK;
 }
-int d2h(dcn_handle* h, float* dst, const float* src, size_t bytes) {
+int d2h(dcn_handle* h, hipStream_t s, void* dst, const void* src, size_t bytes) {
+  if (!bytes) return DCN_OK;
   if (!staging_on(h)) {
-    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
     return DCN_OK;
   }
   dcn::HostStage* st;
   DCN_TRY(get_stage(h, &st));
-  HIP_TRY(st->d2h(dst, src, bytes, h->stream));
+  HIP_TRY(st->d2h(dst, src, bytes, s));
   return DCN_OK;
 }
 
-int backward_host(dcn_handle* h, const dcn_desc* d, const float* x, const float* off,
+// ---- the image-chunk transfer pipeline -----------------------------------------
+// The batch is cut into n image chunks. Chunk i's upload runs on the copy-in stream, its
+// kernels on the handle's stream once that upload is done (event), its download on the
+// copy-out stream once the kernels are done, so the kernels of chunk i run beside the
+// copies of chunks i-1 and i+1: the step costs about the transfers alone plus one chunk's
+// kernels, instead of transfers + kernels. Each chunk has its own workspace slice, which
+// keeps that chunk's columns from the forward for the backward.
+constexpr int kMaxHostChunks = 16;
+constexpr size_t kHostChunkBytes = size_t(24) << 20;  // auto: about this much x per chunk
+
+struct ChunkPlan {
+  int n = 1;
+  int b0[kMaxHostChunks + 1] = {0};
+  size_t ws_off[kMaxHostChunks + 1] = {0};  // workspace slice of chunk i
+  dcn_desc d[kMaxHostChunks];               // the chunk's descriptor (B = its images)
+};
+
+int chunk_count(const dcn_host_state* s, const Geo& g) {
+  // bf16 parameter gradients would be summed over chunks in bf16 and a communicator would
+  // all-reduce every chunk: both keep one chunk
+  if (g.dt != DCN_F32 || s->h->comm) return 1;
+  int n = s->chunks;
+  if (n <= 0) {
+    const size_t xb = (size_t)g.B * g.C * g.HWi * sizeof(float);
+    n = (int)((xb + kHostChunkBytes - 1) / kHostChunkBytes);
+  }
+  return std::max(1, std::min(std::min(n, kMaxHostChunks), g.B));
+}
+
+int make_plan(const dcn_desc* d, const Geo& g, int n, ChunkPlan* P) {
+  P->n = n;
+  size_t off = 0;
+  for (int i = 0; i < n; ++i) {
+    P->b0[i] = (int)((long)g.B * i / n);
+    P->d[i] = *d;
+    P->d[i].B = (int)((long)g.B * (i + 1) / n) - P->b0[i];
+    Geo gi;
+    DCN_TRY(make_geo(&P->d[i], &gi));
+    P->ws_off[i] = off;
+    off += (ws_layout(gi, true).total + 255) & ~size_t(255);
+  }
+  P->b0[n] = g.B;
+  P->ws_off[n] = off;
+  return DCN_OK;
+}
+
+int pipeline_init(dcn_handle* h) {
+  if (!h->cin) HIP_TRY(hipStreamCreateWithFlags(&h->cin, hipStreamNonBlocking));
+  if (!h->cout) HIP_TRY(hipStreamCreateWithFlags(&h->cout, hipStreamNonBlocking));
+  while (h->hev.size() < 2 * kMaxHostChunks) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    h->hev.push_back(e);
+  }
+  return DCN_OK;
+}
+
+// every exit of a pipelined call (errors included) leaves no copy in flight on the
+// caller's memory
+struct PipelineDrain {
+  dcn_handle* h;
+  ~PipelineDrain() {
+    for (hipStream_t s : {h->cin, h->cout, h->stream}) (void)hipStreamSynchronize(s);
+  }
+};
+
+// stream `s` waits for event slot k, recorded on stream `from`
+int hop(dcn_handle* h, int k, hipStream_t from, hipStream_t s) {
+  HIP_TRY(hipEventRecord(h->hev[k], from));
+  HIP_TRY(hipStreamWaitEvent(s, h->hev[k], 0));
+  return DCN_OK;
+}
+
+int check_state(dcn_host_state* s) {
+  if (!s) return fail(DCN_ERR_INVALID, "null host state");
+  if (!s->h) return fail(DCN_ERR_INVALID, "host state of a destroyed handle");
+  return set_device(s->h);
+}
+
+int forward_host(dcn_host_state* s, const dcn_desc* d, const float* x, const float* w_off,
+                 const float* b_off, const float* w, const float* b, float* out, float* off) {
+  DCN_TRY(check_state(s));
+  dcn_handle* h = s->h;
+  Geo g;
+  DCN_TRY(make_geo(d, &g));
+  if (!out) return fail(DCN_ERR_INVALID, "dcn_forward_host: out is required");
+  s->valid = false;
+  const size_t es = elem_bytes(g);
+  const size_t xi = (size_t)g.C * g.HWi * es, oi = (size_t)g.O * g.HW * es;  // per image
+  const size_t fi = (size_t)g.J * g.HW * es, nwo = (size_t)g.J * g.C * g.N * es;
+  const size_t nw = (size_t)g.O * g.K * es;
+  ChunkPlan P;
+  DCN_TRY(make_plan(d, g, chunk_count(s, g), &P));
+  char *dx, *doff, *dwo, *dw, *dbo, *db_ = nullptr, *dout;
+  DCN_TRY(state_buf(s, SB_X, g.B * xi, &dx));
+  DCN_TRY(state_buf(s, SB_OFF, g.B * fi, &doff));
+  DCN_TRY(state_buf(s, SB_WO, nwo, &dwo));
+  DCN_TRY(state_buf(s, SB_W, nw, &dw));
+  DCN_TRY(host_buf(h, HB_BO, g.J * es, &dbo));
+  if (d->has_bias) DCN_TRY(host_buf(h, HB_B, g.O * es, &db_));
+  DCN_TRY(host_buf(h, HB_OUT, g.B * oi, &dout));
+  DCN_TRY(state_ws(s, P.ws_off[P.n]));
+  DCN_TRY(pipeline_init(h));
+  PipelineDrain drain{h};
+  DCN_TRY(h2d(h, h->stream, dwo, w_off, nwo));
+  DCN_TRY(h2d(h, h->stream, dbo, b_off, g.J * es));
+  DCN_TRY(h2d(h, h->stream, dw, w, nw));
+  if (d->has_bias) DCN_TRY(h2d(h, h->stream, db_, b, g.O * es));
+  auto download = [&](int i) -> int {
+    const size_t b0 = P.b0[i], nb = P.d[i].B;
+    DCN_TRY(hop(h, 2 * i + 1, h->stream, h->cout));
+    DCN_TRY(d2h(h, h->cout, (char*)out + b0 * oi, dout + b0 * oi, nb * oi));
+    if (off) DCN_TRY(d2h(h, h->cout, (char*)off + b0 * fi, doff + b0 * fi, nb * fi));
+    return DCN_OK;
+  };
+  for (int i = 0; i < P.n; ++i) {
+    const size_t b0 = P.b0[i], nb = P.d[i].B;
+    DCN_TRY(h2d(h, h->cin, dx + b0 * xi, (const char*)x + b0 * xi, nb * xi));
+    DCN_TRY(hop(h, 2 * i, h->cin, h->stream));
+    DCN_TRY(dcn_forward(h, &P.d[i], (float*)(dx + b0 * xi), (float*)dwo, (float*)dbo,
+                        (float*)dw, (float*)db_, (float*)(dout + b0 * oi),
+                        (float*)(doff + b0 * fi), (char*)s->ws + P.ws_off[i],
+                        P.ws_off[i + 1] - P.ws_off[i]));
+    if (i > 0) DCN_TRY(download(i - 1));
+  }
+  DCN_TRY(download(P.n - 1));
+  HIP_TRY(hipStreamSynchronize(h->cout));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  s->valid = true;
+  s->plan_n = P.n;
+  s->desc = *d;
+  s->x = x, s->wo = w_off, s->w = w, s->off = off;
+  return DCN_OK;
+}
+
+int backward_host(dcn_host_state* s, const dcn_desc* d, const float* x, const float* off,
                   const float* w_off, const float* w, const float* grad_out, float* grad_x,
                   float* grad_w, float* grad_b, float* grad_w_off, float* grad_b_off,
                   float* grad_off_out, int flags) {
+  DCN_TRY(check_state(s));
+  dcn_handle* h = s->h;
   Geo g;
   DCN_TRY(make_geo(d, &g));
-  DCN_TRY(set_device(h));
   const bool reuse = (flags & DCN_HOST_REUSE_FWD) != 0;
   if (reuse) {
-    if (!h->hfwd_valid || std::memcmp(&h->hfwd_desc, d, sizeof(dcn_desc)) != 0 ||
-        h->hfwd_x != x || h->hfwd_wo != w_off || h->hfwd_w != w || h->hfwd_off != off)
+    if (!s->valid || std::memcmp(&s->desc, d, sizeof(dcn_desc)) != 0 || s->x != x ||
+        s->wo != w_off || s->w != w || s->off != off)
       return fail(DCN_ERR_INVALID,
                   "DCN_HOST_REUSE_FWD: not the descriptor and x / off / w_off / w arrays of the "
-                  "last dcn_forward_host on this handle");
+                  "last forward on this host state");
+  } else if (!off) {
+    return fail(DCN_ERR_INVALID, "dcn_backward_host: off is required without DCN_HOST_REUSE_FWD");
   }
-  const size_t nx = (size_t)g.B * g.C * g.HWi, nwo = (size_t)g.J * g.C * g.N, nw = (size_t)g.O * g.K;
-  const size_t nout = (size_t)g.B * g.O * g.HW, noff = (size_t)g.B * g.J * g.HW;
   const size_t es = elem_bytes(g);
-  float *dx, *doff, *dwo, *dw, *dgo, *dgx, *dgw, *dgb = nullptr, *dgwo, *dgbo, *dgoff;
-  DCN_TRY(host_buf(h, HB_X, nx * es, &dx));
-  DCN_TRY(host_buf(h, HB_OFF, noff * es, &doff));
-  DCN_TRY(host_buf(h, HB_WO, nwo * es, &dwo));
-  DCN_TRY(host_buf(h, HB_W, nw * es, &dw));
-  DCN_TRY(host_buf(h, HB_GO, nout * es, &dgo));
-  DCN_TRY(host_buf(h, HB_GX, nx * es, &dgx));
-  DCN_TRY(host_buf(h, HB_GW, nw * es, &dgw));
-  if (d->has_bias) DCN_TRY(host_buf(h, HB_GB, (size_t)g.O * es, &dgb));
-  DCN_TRY(host_buf(h, HB_GWO, nwo * es, &dgwo));
-  DCN_TRY(host_buf(h, HB_GBO, (size_t)g.J * es, &dgbo));
-  DCN_TRY(host_buf(h, HB_GOFF, noff * es, &dgoff));
-  DCN_TRY(ensure_ws(h, ws_layout(g, true).total));
-  if (!reuse) {
-    h->hfwd_valid = false;  // the workspace columns are about to be rebuilt from these inputs
-    DCN_TRY(h2d(h, dx, x, nx * es));
-    DCN_TRY(h2d(h, doff, off, noff * es));
-    DCN_TRY(h2d(h, dwo, w_off, nwo * es));
-    DCN_TRY(h2d(h, dw, w, nw * es));
-  }
-  DCN_TRY(h2d(h, dgo, grad_out, nout * es));
-  DCN_TRY(dcn_backward(h, d, dx, doff, dwo, dw, dgo, dgx, dgw, dgb, dgwo, dgbo, dgoff, h->ws,
-                       h->ws_bytes, reuse ? DCN_BWD_COL_IN_WS : 0));
+  const size_t xi = (size_t)g.C * g.HWi * es, oi = (size_t)g.O * g.HW * es;
+  const size_t fi = (size_t)g.J * g.HW * es;
+  // ∂W, ∂b, ∂W_off, ∂b_off packed in one block (16-B aligned parts): the per-chunk partials
+  // of a pipelined backward are summed in chunk order with one launch
+  auto up4 = [](size_t n) { return (n + 3) & ~size_t(3); };
+  const size_t nw = (size_t)g.O * g.K, nwo = (size_t)g.J * g.C * g.N;
+  const size_t p_gw = 0, p_gb = up4(nw), p_gwo = p_gb + up4(g.O), p_gbo = p_gwo + up4(nwo);
+  const size_t npar = p_gbo + up4(g.J);
+  ChunkPlan P;
+  DCN_TRY(make_plan(d, g, reuse ? s->plan_n : chunk_count(s, g), &P));
+  char *dx, *doff, *dwo, *dw, *dgo, *dgx, *dgoff = nullptr, *gpar, *part = nullptr;
+  DCN_TRY(state_buf(s, SB_X, g.B * xi, &dx));
+  DCN_TRY(state_buf(s, SB_OFF, g.B * fi, &doff));
+  DCN_TRY(state_buf(s, SB_WO, nwo * es, &dwo));
+  DCN_TRY(state_buf(s, SB_W, nw * es, &dw));
+  DCN_TRY(host_buf(h, HB_GO, g.B * oi, &dgo));
+  DCN_TRY(host_buf(h, HB_GX, g.B * xi, &dgx));
+  if (grad_off_out) DCN_TRY(host_buf(h, HB_GOFF, g.B * fi, &dgoff));
+  DCN_TRY(host_buf(h, HB_GPAR, npar * es, &gpar));
+  if (P.n > 1) DCN_TRY(host_buf(h, HB_PART, P.n * npar * sizeof(float), &part));
+  if (!reuse) DCN_TRY(state_ws(s, P.ws_off[P.n]));
+  DCN_TRY(pipeline_init(h));
+  PipelineDrain drain{h};
   // the backward overwrites the columns with ∂columns: a second reuse needs a new forward
-  h->hfwd_valid = false;
-  DCN_TRY(d2h(h, grad_x, dgx, nx * es));
-  DCN_TRY(d2h(h, grad_w, dgw, nw * es));
-  if (d->has_bias) DCN_TRY(d2h(h, grad_b, dgb, g.O * es));
-  DCN_TRY(d2h(h, grad_w_off, dgwo, nwo * es));
-  DCN_TRY(d2h(h, grad_b_off, dgbo, g.J * es));
-  if (grad_off_out) DCN_TRY(d2h(h, grad_off_out, dgoff, noff * es));
+  s->valid = false;
+  if (!reuse) {
+    DCN_TRY(h2d(h, h->stream, dwo, w_off, nwo * es));
+    DCN_TRY(h2d(h, h->stream, dw, w, nw * es));
+  }
+  auto download = [&](int i) -> int {
+    const size_t b0 = P.b0[i], nb = P.d[i].B;
+    DCN_TRY(hop(h, 2 * i + 1, h->stream, h->cout));
+    DCN_TRY(d2h(h, h->cout, (char*)grad_x + b0 * xi, dgx + b0 * xi, nb * xi));
+    if (grad_off_out)
+      DCN_TRY(d2h(h, h->cout, (char*)grad_off_out + b0 * fi, dgoff + b0 * fi, nb * fi));
+    return DCN_OK;
+  };
+  for (int i = 0; i < P.n; ++i) {
+    const size_t b0 = P.b0[i], nb = P.d[i].B;
+    if (!reuse) {
+      DCN_TRY(h2d(h, h->cin, dx + b0 * xi, (const char*)x + b0 * xi, nb * xi));
+      DCN_TRY(h2d(h, h->cin, doff + b0 * fi, (const char*)off + b0 * fi, nb * fi));
+    }
+    DCN_TRY(h2d(h, h->cin, dgo + b0 * oi, (const char*)grad_out + b0 * oi, nb * oi));
+    DCN_TRY(hop(h, 2 * i, h->cin, h->stream));
+    char* pp = P.n > 1 ? part + i * npar * sizeof(float) : gpar;
+    DCN_TRY(dcn_backward(h, &P.d[i], (float*)(dx + b0 * xi), (float*)(doff + b0 * fi),
+                         (float*)dwo, (float*)dw, (float*)(dgo + b0 * oi),
+                         (float*)(dgx + b0 * xi), (float*)(pp + p_gw * es),
+                         d->has_bias ? (float*)(pp + p_gb * es) : nullptr,
+                         (float*)(pp + p_gwo * es), (float*)(pp + p_gbo * es),
+                         grad_off_out ? (float*)(dgoff + b0 * fi) : nullptr,
+                         (char*)s->ws + P.ws_off[i], P.ws_off[i + 1] - P.ws_off[i],
+                         reuse ? DCN_BWD_COL_IN_WS : 0));
+    if (i > 0) DCN_TRY(download(i - 1));
+  }
+  if (P.n > 1)  // fp32 only (chunk_count)
+    HIP_TRY(dcn::launch_sum_partials((const float*)part, P.n, npar, (float*)gpar, h->stream));
+  DCN_TRY(download(P.n - 1));
+  DCN_TRY(d2h(h, h->stream, grad_w, gpar + p_gw * es, nw * es));
+  if (d->has_bias) DCN_TRY(d2h(h, h->stream, grad_b, gpar + p_gb * es, g.O * es));
+  DCN_TRY(d2h(h, h->stream, grad_w_off, gpar + p_gwo * es, nwo * es));
+  DCN_TRY(d2h(h, h->stream, grad_b_off, gpar + p_gbo * es, g.J * es));
+  HIP_TRY(hipStreamSynchronize(h->cout));
   HIP_TRY(hipStreamSynchronize(h->stream));
+  return DCN_OK;
+}
+
+int default_state(dcn_handle* h, dcn_host_state** s) {
+  DCN_TRY(set_device(h));
+  if (!h->hs0) {
+    h->hs0 = new dcn_host_state();
+    h->hs0->h = h;
+  }
+  *s = h->hs0;
   return DCN_OK;
 }
 }  // namespace
 
+int dcn_host_state_create(dcn_handle* h, dcn_host_state** out) {
+  if (!out) return fail(DCN_ERR_INVALID, "null out pointer");
+  *out = nullptr;
+  DCN_TRY(set_device(h));
+  auto* s = new dcn_host_state();
+  s->h = h;
+  h->states.push_back(s);
+  *out = s;
+  return DCN_OK;
+}
+
+int dcn_host_state_destroy(dcn_host_state* s) {
+  if (!s) return DCN_OK;
+  if (dcn_handle* h = s->h) {
+    (void)hipSetDevice(h->device);
+    (void)hipStreamSynchronize(h->stream);
+    state_free(s);
+    h->states.erase(std::remove(h->states.begin(), h->states.end(), s), h->states.end());
+  }
+  delete s;
+  return DCN_OK;
+}
+
+int dcn_host_state_set_chunks(dcn_host_state* s, int chunks) {
+  DCN_TRY(check_state(s));
+  if (chunks < 0) return fail(DCN_ERR_INVALID, "chunks must be >= 0 (0 = auto)");
+  s->chunks = chunks;
+  return DCN_OK;
+}
+
+int dcn_forward_host_s(dcn_host_state* s, const dcn_desc* d, const float* x, const float* w_off,
+                       const float* b_off, const float* w, const float* b, float* out,
+                       float* off) {
+  return forward_host(s, d, x, w_off, b_off, w, b, out, off);
+}
+
+int dcn_backward_host_s(dcn_host_state* s, const dcn_desc* d, const float* x, const float* off,
+                        const float* w_off, const float* w, const float* grad_out,
+                        float* grad_x, float* grad_w, float* grad_b, float* grad_w_off,
+                        float* grad_b_off, float* grad_off_out, int flags) {
+  if (flags & ~DCN_HOST_REUSE_FWD) return fail(DCN_ERR_INVALID, "unknown dcn_backward_host flag");
+  return backward_host(s, d, x, off, w_off, w, grad_out, grad_x, grad_w, grad_b, grad_w_off,
+                       grad_b_off, grad_off_out, flags);
+}
+
 int dcn_forward_host(dcn_handle* h, const dcn_desc* d, const float* x, const float* w_off,
                      const float* b_off, const float* w, const float* b, float* out, float* off) {
-  Geo g;
-  DCN_TRY(make_geo(d, &g));
-  DCN_TRY(set_device(h));
-  if (!out) return fail(DCN_ERR_INVALID, "dcn_forward_host: out is required");
-  h->hfwd_valid = false;
-  const size_t nx = (size_t)g.B * g.C * g.HWi, nwo = (size_t)g.J * g.C * g.N, nw = (size_t)g.O * g.K;
-  const size_t nout = (size_t)g.B * g.O * g.HW, noff = (size_t)g.B * g.J * g.HW;
-  const size_t es = elem_bytes(g);
-  float *dx, *dwo, *dbo, *dw, *db_ = nullptr, *dout, *doff;
-  DCN_TRY(host_buf(h, HB_X, nx * es, &dx));
-  DCN_TRY(host_buf(h, HB_WO, nwo * es, &dwo));
-  DCN_TRY(host_buf(h, HB_BO, (size_t)g.J * es, &dbo));
-  DCN_TRY(host_buf(h, HB_W, nw * es, &dw));
-  if (d->has_bias) DCN_TRY(host_buf(h, HB_B, (size_t)g.O * es, &db_));
-  DCN_TRY(host_buf(h, HB_OUT, nout * es, &dout));
-  DCN_TRY(host_buf(h, HB_OFF, noff * es, &doff));
-  // sized for the backward too, so a DCN_HOST_REUSE_FWD backward finds the columns in place
-  DCN_TRY(ensure_ws(h, ws_layout(g, true).total));
-  DCN_TRY(h2d(h, dx, x, nx * es));
-  DCN_TRY(h2d(h, dwo, w_off, nwo * es));
-  DCN_TRY(h2d(h, dbo, b_off, g.J * es));
-  DCN_TRY(h2d(h, dw, w, nw * es));
-  if (d->has_bias) DCN_TRY(h2d(h, db_, b, g.O * es));
-  DCN_TRY(dcn_forward(h, d, dx, dwo, dbo, dw, db_, dout, doff, h->ws, h->ws_bytes));
-  DCN_TRY(d2h(h, out, dout, nout * es));
-  if (off) DCN_TRY(d2h(h, off, doff, noff * es));
-  HIP_TRY(hipStreamSynchronize(h->stream));
-  h->hfwd_valid = off != nullptr;  // a reusing backward names the offsets it was given
-  h->hfwd_desc = *d;
-  h->hfwd_x = x;
-  h->hfwd_wo = w_off;
-  h->hfwd_w = w;
-  h->hfwd_off = off;
-  return DCN_OK;
+  dcn_host_state* s;
+  DCN_TRY(default_state(h, &s));
+  return forward_host(s, d, x, w_off, b_off, w, b, out, off);
 }
 
 int dcn_backward_host(dcn_handle* h, const dcn_desc* d, const float* x, const float* off,
                       const float* w_off, const float* w, const float* grad_out, float* grad_x,
                       float* grad_w, float* grad_b, float* grad_w_off, float* grad_b_off,
                       float* grad_off_out) {
-  return backward_host(h, d, x, off, w_off, w, grad_out, grad_x, grad_w, grad_b, grad_w_off,
+  dcn_host_state* s;
+  DCN_TRY(default_state(h, &s));
+  return backward_host(s, d, x, off, w_off, w, grad_out, grad_x, grad_w, grad_b, grad_w_off,
                        grad_b_off, grad_off_out, 0);
 }
 
@@ -1210,7 +1456,9 @@ int dcn_backward_host_ex(dcn_handle* h, const dcn_desc* d, const float* x, const
                          float* grad_x, float* grad_w, float* grad_b, float* grad_w_off,
                          float* grad_b_off, float* grad_off_out, int flags) {
   if (flags & ~DCN_HOST_REUSE_FWD) return fail(DCN_ERR_INVALID, "unknown dcn_backward_host_ex flag");
-  return backward_host(h, d, x, off, w_off, w, grad_out, grad_x, grad_w, grad_b, grad_w_off,
+  dcn_host_state* s;
+  DCN_TRY(default_state(h, &s));
+  return backward_host(s, d, x, off, w_off, w, grad_out, grad_x, grad_w, grad_b, grad_w_off,
                        grad_b_off, grad_off_out, flags);
 }
 
@@ -1278,14 +1526,14 @@ int dcn_roi_pool_fwd_host(dcn_handle* h, const dcn_roi_desc* d, const float* fea
   DCN_TRY(db.alloc(nf * 4, &df));
   DCN_TRY(db.alloc(nr * 4, &dr));
   DCN_TRY(db.alloc(nout * 4, &dout));
-  DCN_TRY(h2d(h, df, features, nf * 4));
-  DCN_TRY(h2d(h, dr, rois, nr * 4));
+  DCN_TRY(h2d(h, h->stream, df, features, nf * 4));
+  DCN_TRY(h2d(h, h->stream, dr, rois, nr * 4));
   if (offsets) {
     DCN_TRY(db.alloc(no * 4, &doffs));
-    DCN_TRY(h2d(h, doffs, offsets, no * 4));
+    DCN_TRY(h2d(h, h->stream, doffs, offsets, no * 4));
   }
   DCN_TRY(dcn_roi_pool_fwd(h, d, df, dr, doffs, dout));
-  DCN_TRY(d2h(h, out, dout, nout * 4));
+  DCN_TRY(d2h(h, h->stream, out, dout, nout * 4));
   HIP_TRY(hipStreamSynchronize(h->stream));
   return DCN_OK;
 }
@@ -1305,17 +1553,17 @@ int dcn_roi_pool_bwd_host(dcn_handle* h, const dcn_roi_desc* d, const float* fea
   DCN_TRY(db.alloc(nr * 4, &dr));
   DCN_TRY(db.alloc(nout * 4, &dgo));
   DCN_TRY(db.alloc(nf * 4, &dgf));
-  DCN_TRY(h2d(h, df, features, nf * 4));
-  DCN_TRY(h2d(h, dr, rois, nr * 4));
-  DCN_TRY(h2d(h, dgo, grad_out, nout * 4));
+  DCN_TRY(h2d(h, h->stream, df, features, nf * 4));
+  DCN_TRY(h2d(h, h->stream, dr, rois, nr * 4));
+  DCN_TRY(h2d(h, h->stream, dgo, grad_out, nout * 4));
   if (offsets) {
     DCN_TRY(db.alloc(no * 4, &doffs));
-    DCN_TRY(h2d(h, doffs, offsets, no * 4));
+    DCN_TRY(h2d(h, h->stream, doffs, offsets, no * 4));
   }
   if (grad_offsets) DCN_TRY(db.alloc(no * 4, &dgoffs));
   DCN_TRY(dcn_roi_pool_bwd(h, d, df, dr, doffs, dgo, dgf, dgoffs));
-  DCN_TRY(d2h(h, grad_features, dgf, nf * 4));
-  if (grad_offsets) DCN_TRY(d2h(h, grad_offsets, dgoffs, no * 4));
+  DCN_TRY(d2h(h, h->stream, grad_features, dgf, nf * 4));
+  if (grad_offsets) DCN_TRY(d2h(h, h->stream, grad_offsets, dgoffs, no * 4));
   HIP_TRY(hipStreamSynchronize(h->stream));
   return DCN_OK;
 }

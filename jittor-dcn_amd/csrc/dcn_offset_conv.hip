@@ -1691,12 +1691,12 @@ __global__ __launch_bounds__(256) void woff_to_f32frag(const float* __restrict__
   wf[i] = j < J ? w[((size_t)j * C + c) * 9 + t] : 0.f;
 }
 
-template <int ROWS, int RPW>  // output rows per workgroup, rows per wave (same pixel tile)
-__global__ __launch_bounds__(ROWS * 256 / RPW) __attribute__((amdgpu_waves_per_eu(2))) void
+template <int ROWS>  // output rows per workgroup; 4 * ROWS waves
+__global__ __launch_bounds__(ROWS * 256) __attribute__((amdgpu_waves_per_eu(2))) void
 offset_conv_fwd_mfma_xt(Geo g, const float* __restrict__ x, const float* __restrict__ wf,
                         const float* __restrict__ b_off, float* __restrict__ off,
                         float* __restrict__ xT) {
-  constexpr int NT = ROWS * 256 / RPW, NR = ROWS + 2, CP = kXtCP;
+  constexpr int NT = ROWS * 256, NR = ROWS + 2, CP = kXtCP;
   constexpr int RW = kXtRWmax;              // window row pitch (pixels): compile-time offsets
   constexpr int WIN = NR * RW * CP;         // floats per window buffer
   constexpr int BUF = WIN + kXtWts;
@@ -1704,7 +1704,6 @@ offset_conv_fwd_mfma_xt(Geo g, const float* __restrict__ x, const float* __restr
   __shared__ __attribute__((aligned(16))) float lds[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tt = w & 3, r0 = (w >> 2) * RPW;  // this wave's pixel tile and first row
   const Block3 blk = xcd_block();
   const int ho0 = blk.x * ROWS, b = blk.z;
   const int H = g.H, W = g.W, C = g.C, NQ = W / 4;
@@ -1772,15 +1771,15 @@ offset_conv_fwd_mfma_xt(Geo g, const float* __restrict__ x, const float* __restr
       if (idx < kXtWts / 4) reinterpret_cast<float4*>(L + WIN)[idx] = sw[u];
     }
   };
-  f32x4 acc[RPW];
-  float e0[RPW], e1[RPW];
-#pragma unroll
-  for (int r = 0; r < RPW; ++r) {
-    acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
-    e0[r] = e1[r] = 0.f;
-  }
-  // A column of each tap: pixel 4m + tt + tx, clamped for the pixels past W (discarded)
-  const int pc = min(4 * m + tt, W - 1);
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  float e0 = 0.f, e1 = 0.f;
+  // Wave w's pixel tile: pixels 16w .. 16w+15 of the ROWS x W block, row-major, so tiles
+  // span rows and only the last one can hold padding (r02 gave each row 4 tiles of 16
+  // pixels: 64 MFMA rows per 56-pixel row at config 3). A waves past the block's last
+  // tile only stage. A row m = pixel 16w + m (clamped; the clamped rows are discarded).
+  const int npx = ROWS * W;
+  const bool has_tile = 16 * w < npx;
+  const int pa = min(16 * w + m, npx - 1), ra = pa / W, ca = pa - ra * W;
   auto step = [&](int k, float4(&sxn)[kSx], float4(&swn)[kSw]) __attribute__((always_inline)) {
     // LDS buffer k&1 holds chunk k; (sxn, swn) chunk k+1; the other set chunk k+2 (in flight)
     const int bf = k & 1;
@@ -1798,30 +1797,29 @@ offset_conv_fwd_mfma_xt(Geo g, const float* __restrict__ x, const float* __restr
       }
     }
     const float* LB = L + WIN;
+    if (has_tile) {
 #pragma unroll 1
-    for (int ty = 0; ty < 3; ++ty)
+      for (int ty = 0; ty < 3; ++ty)
 #pragma unroll
-    for (int tx = 0; tx < 3; ++tx) {
-      const int t = ty * 3 + tx;
-      const float4 bw = *reinterpret_cast<const float4*>(LB + (t * 64 + lane) * 4);
-      const float4 v0 = *reinterpret_cast<const float4*>(LB + 9 * 256 + (t * 4 + gq) * 8);
-      const float4 v1 = *reinterpret_cast<const float4*>(LB + 9 * 256 + (t * 4 + gq) * 8 + 4);
-#pragma unroll
-      for (int r = 0; r < RPW; ++r) {
+      for (int tx = 0; tx < 3; ++tx) {
+        const int t = ty * 3 + tx;
+        const float4 bw = *reinterpret_cast<const float4*>(LB + (t * 64 + lane) * 4);
+        const float4 v0 = *reinterpret_cast<const float4*>(LB + 9 * 256 + (t * 4 + gq) * 8);
+        const float4 v1 = *reinterpret_cast<const float4*>(LB + 9 * 256 + (t * 4 + gq) * 8 + 4);
         const float4 a =
-            *reinterpret_cast<const float4*>(L + ((r0 + r + ty) * RW + pc + tx) * CP + 4 * gq);
-        acc[r] = mfma16(a.x, bw.x, acc[r]);
-        acc[r] = mfma16(a.y, bw.y, acc[r]);
-        acc[r] = mfma16(a.z, bw.z, acc[r]);
-        acc[r] = mfma16(a.w, bw.w, acc[r]);
-        e0[r] = fmaf(a.x, v0.x, e0[r]);
-        e1[r] = fmaf(a.x, v0.y, e1[r]);
-        e0[r] = fmaf(a.y, v0.z, e0[r]);
-        e1[r] = fmaf(a.y, v0.w, e1[r]);
-        e0[r] = fmaf(a.z, v1.x, e0[r]);
-        e1[r] = fmaf(a.z, v1.y, e1[r]);
-        e0[r] = fmaf(a.w, v1.z, e0[r]);
-        e1[r] = fmaf(a.w, v1.w, e1[r]);
+            *reinterpret_cast<const float4*>(L + ((ra + ty) * RW + ca + tx) * CP + 4 * gq);
+        acc = mfma16(a.x, bw.x, acc);
+        acc = mfma16(a.y, bw.y, acc);
+        acc = mfma16(a.z, bw.z, acc);
+        acc = mfma16(a.w, bw.w, acc);
+        e0 = fmaf(a.x, v0.x, e0);
+        e1 = fmaf(a.x, v0.y, e1);
+        e0 = fmaf(a.y, v0.z, e0);
+        e1 = fmaf(a.y, v0.w, e1);
+        e0 = fmaf(a.z, v1.x, e0);
+        e1 = fmaf(a.z, v1.y, e1);
+        e0 = fmaf(a.w, v1.z, e0);
+        e1 = fmaf(a.w, v1.w, e1);
       }
     }
     if (k + 1 < nch) store_chunk(bf ^ 1, sxn, swn);
@@ -1840,23 +1838,25 @@ offset_conv_fwd_mfma_xt(Geo g, const float* __restrict__ x, const float* __restr
   // through LDS as [row][j][64 pixels], then runs of consecutive pixels per offset channel
   float* T = lds;  // the buffers are free: the last barrier followed the last reads
   const int j = lane & 15;
-#pragma unroll
-  for (int r = 0; r < RPW; ++r) {
+  if (has_tile) {
     // lane groups' VALU partials (channels 4g..4g+3 of every chunk) in a fixed order
-    float s0 = e0[r], s1 = e1[r];
+    float s0 = e0, s1 = e1;
     s0 += __shfl_xor(s0, 16);
     s1 += __shfl_xor(s1, 16);
     s0 += __shfl_xor(s0, 32);
     s1 += __shfl_xor(s1, 32);
-    const int rr = r0 + r;
     if (j < g.J) {
       const float bj = b_off[j];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) T[(rr * 18 + j) * 64 + 4 * (4 * gq + i) + tt] = acc[r][i] + bj;
+      for (int i = 0; i < 4; ++i) {  // D row 4gq + i = pixel 16w + 4gq + i
+        const int p = 16 * w + 4 * gq + i, ro = p / W;
+        if (p < npx) T[(ro * 18 + j) * 64 + p - ro * W] = acc[i] + bj;
+      }
     }
-    if (lane < 16) {
-      if (g.J > 16) T[(rr * 18 + 16) * 64 + 4 * m + tt] = s0 + b_off[16];
-      if (g.J > 17) T[(rr * 18 + 17) * 64 + 4 * m + tt] = s1 + b_off[17];
+    if (lane < 16 && 16 * w + m < npx) {
+      const int p = 16 * w + m, ro = p / W, co = p - ro * W;
+      if (g.J > 16) T[(ro * 18 + 16) * 64 + co] = s0 + b_off[16];
+      if (g.J > 17) T[(ro * 18 + 17) * 64 + co] = s1 + b_off[17];
     }
   }
   __syncthreads();
@@ -1885,7 +1885,7 @@ hipError_t launch_offset_conv_fwd_xt(const Geo& g, const float* x, const float* 
       hipLaunchKernelGGL(kern, dim3((g.H + rows - 1) / rows, 1, g.B), dim3(nt), 0, s, g, x, wf,
                          b_off, off, xT);
     };
-    go(offset_conv_fwd_mfma_xt<2, 1>, 2, 512);
+    go(offset_conv_fwd_mfma_xt<2>, 2, 512);
   }
   return hipGetLastError();
 }

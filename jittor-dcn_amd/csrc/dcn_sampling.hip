@@ -734,14 +734,19 @@ __global__ __launch_bounds__(256) void bins_emit(Geo g, int nch, int NB,
 // K5 fused (∂x + ∂offset from ONE pass over the binned ∂col rows).
 // One block = a kTR x kTQ tile (template parameters) of INPUT pixels of one image and kTR+1 waves. Bin
 // (br, bc) holds the samples whose top-left corner is (br-1, bc-1) (K5b); wave w walks
-// bin row br = R0+w (bin columns Q0..Q0+kTQ, samples in sorted order), reading each
-// ∂colT row once, and accumulates into the two pixel rows that bin row touches: r0
-// (tile row w-1, weight 1-fr) and r0+1 (tile row w, weight fr). The bin loop is
-// unrolled, so accumulator indices are static (registers). Tile row t is then wave t's
-// lower row + wave t+1's upper row, combined through LDS in that fixed order.
-// ∂offset of a sample is computed once, by the wave/block that owns its bin (bin corner
-// inside the tile; row/column -1 owned by the first tile), from the tile's
-// (kTR+1) x (kTQ+1) xT window staged in LDS (corners at row/column -1 are outside the
+// bin row br = R0+w (bin columns Q0..Q0+kTQ-1, and W too in the last column of tiles;
+// samples in sorted order), reading each ∂colT row once, and accumulates into the two pixel
+// rows that bin row touches: r0 (tile row w-1, weight 1-fr) and r0+1 (tile row w, weight
+// fr). The bin loop is unrolled, so accumulator indices are static (registers). Tile row t
+// is then wave t's lower row + wave t+1's upper row, combined through LDS in that fixed
+// order. Bin column Q0 also feeds pixel column Q0-1, the left tile's last one: that share
+// is written as boundary partials as soon as the column is done (cpart[b][r][tile
+// column][lower, upper][C]: wave w's two rows, so no registers stay held for them), which
+// col2im_fold adds to the left tile's ∂xT afterwards. No bin column is read by two tiles
+// (r02 read the shared column from both sides: (kTQ+1)/kTQ of the ∂col rows).
+// ∂offset of a sample is computed once, by the block that reads its bin (bin row R0 is
+// read by two tiles: the lower one, w >= 1, owns it), from the tile's (kTR+1) x (kTQ+1)
+// xT window (rows R0..R0+kTR, columns Q0-1..Q0+kTQ-1) staged in LDS (corners outside the
 // image: zero). ∂offset uses offgrad_cl's op order (per-lane channel sums, fixed xor
 // tree). Used for deform_groups == 1, C % 4 == 0, C <= 256.
 // ---------------------------------------------------------------------------
@@ -759,11 +764,13 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
                                                            const int* __restrict__ start,
                                                            const GT* __restrict__ gcolT,
                                                            float* __restrict__ gxT,
-                                                           float* __restrict__ goff, int b0,
+                                                           float* __restrict__ goff,
+                                                           float* __restrict__ cpart, int b0,
                                                            int tq_n) {
   constexpr int kC2iThreads = (kTR + 1) * 64, WR = kTR + 1, WQ = kTQ + 1;
-  constexpr int WIN = WR * WQ * 64, UPR = kTR * kTQ * 64;  // float4 slots
-  __shared__ float4 lds[WIN > UPR ? WIN : UPR];  // xT window, then the upper rows
+  // float4 slots: the xT window, then the upper rows
+  constexpr int WIN = WR * WQ * 64, UPR = kTR * kTQ * 64;
+  __shared__ float4 lds[WIN > UPR ? WIN : UPR];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const Block3 blk = xcd_block();
@@ -773,7 +780,7 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
   const int c = lane * 4;
   const bool cok = c < g.C;
   const XT* xb = xT + (size_t)b * g.HWi * g.C;
-  // xT rows R0..R0+kTR, cols Q0..Q0+kTQ (zero outside the image) into registers; they go
+  // xT rows R0..R0+kTR, cols Q0-1..Q0+kTQ-1 (zero outside the image) into registers; they go
   // to LDS after each wave has started its record / ∂col row stream, and the barrier
   // orders LDS only, so the stream's first rows are in flight across it (r01 staged the
   // window first: the stream began a full staging round trip later)
@@ -783,8 +790,8 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
   for (int k = 0; k < WIT; ++k) {
     const int idx = tid + k * kC2iThreads;
     const int pix = idx >> 6, l = idx & 63;
-    const int r = R0 + pix / WQ, q = Q0 + pix % WQ, cc = l * 4;
-    wv[k] = (idx < WIN && r < g.H && q < g.W && cc < g.C)
+    const int r = R0 + pix / WQ, q = Q0 - 1 + pix % WQ, cc = l * 4;
+    wv[k] = (idx < WIN && r < g.H && q >= 0 && q < g.W && cc < g.C)
                 ? ld4(xb + ((size_t)r * g.W + q) * g.C + cc)
                 : make_float4(0.f, 0.f, 0.f, 0.f);
   }
@@ -799,14 +806,15 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
   float4 up[kTQ], dn[kTQ];  // pixel rows r0 (tile row w-1) and r0+1 (tile row w)
 #pragma unroll
   for (int j = 0; j < kTQ; ++j) up[j] = dn[j] = z4;
+  float4 lup = z4, ldn = z4;  // the same two rows at pixel column Q0-1 (boundary partial)
   const int br = R0 + w;  // bin row = r0 + 1
   const bool act = br <= g.H;
   const bool drow = w >= 1 || br == 0;  // owns the ∂offset of this bin row
-  // the row's bins (br, Q0..Q0+kTQ) are consecutive, so their records are one
-  // contiguous range: fetch it 64 records per vector load (lane l <- record l) and
-  // take each with v_readlane — no scalar-load round trip per sample
+  // the row's bins (br, Q0..Q0+kTQ-1; ..W in the last tile column) are consecutive, so
+  // their records are one contiguous range: fetch it 64 records per vector load (lane l <-
+  // record l) and take each with v_readlane — no scalar-load round trip per sample
   const int bin0 = min(br, g.H) * (g.W + 1) + Q0;
-  const int nbin = min(kTQ, g.W - Q0) + 1;
+  const int nbin = tq_i == tq_n - 1 ? g.W - Q0 + 1 : kTQ;
   int bst[kTQ + 2];
 #pragma unroll
   for (int k = 0; k <= kTQ + 1; ++k) bst[k] = act ? st[bin0 + min(k, nbin)] : 0;
@@ -846,8 +854,6 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
     for (int bj = 0; bj <= kTQ; ++bj) {
       if (bj >= nbin) break;
-      const int bc = Q0 + bj;
-      const bool doff = drow && (bj >= 1 || bc == 0);
       const int lo = bst[bj], hi = bst[bj + 1];
       for (int i = lo; i < hi; i += U) {
         int4 R[U];
@@ -877,15 +883,19 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
           if (bj >= 1) {
             up[bj - 1] = fma4(gr * gc, gv[u], up[bj - 1]);
             dn[bj - 1] = fma4(fr * gc, gv[u], dn[bj - 1]);
+          } else {
+            lup = fma4(gr * gc, gv[u], lup);
+            ldn = fma4(fr * gc, gv[u], ldn);
           }
-          if (doff) {
-            // corners (r0, c0) .. (r0+1, c0+1) at window (w-1, bj-1) .. (w, bj)
-            const float4* w4 = lds + ((w - 1) * WQ + (bj - 1)) * 64 + lane;
-            const bool rA = w >= 1, cA = bj >= 1;
-            const float4 a = (rA && cA) ? w4[0] : z4;
-            const float4 bq = rA ? w4[64] : z4;
-            const float4 cq = cA ? w4[WQ * 64] : z4;
-            const float4 d = w4[(WQ + 1) * 64];
+          if (drow) {
+            // corners (r0, c0) .. (r0+1, c0+1) at window (w-1, bj) .. (w, bj+1); column
+            // bj+1 = kTQ+1 is W (the last tile column's bin W): outside the image
+            const float4* w4 = lds + ((w - 1) * WQ + bj) * 64 + lane;
+            const bool rA = w >= 1, cB = bj + 1 <= kTQ;
+            const float4 a = rA ? w4[0] : z4;
+            const float4 bq = (rA && cB) ? w4[64] : z4;
+            const float4 cq = w4[WQ * 64];
+            const float4 d = cB ? w4[(WQ + 1) * 64] : z4;
             float diy = 0.f, dix = 0.f;
             acc_dgrad(fr, fc, gv[u], a, bq, cq, d, diy, dix);
             diy = wave_sum(diy);
@@ -896,6 +906,12 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
             }
           }
         }
+      }
+      if (bj == 0 && tq_i > 0 && cok) {  // the left boundary partials of bin column Q0
+        const size_t rs = (size_t)tq_n * 2 * g.C;  // pixel-row stride
+        float* cp = cpart + (size_t)bl * g.H * rs + (size_t)tq_i * 2 * g.C + c;
+        if (w < kTR && br < g.H) *reinterpret_cast<float4*>(cp + br * rs) = ldn;
+        if (w >= 1) *reinterpret_cast<float4*>(cp + (br - 1) * rs + g.C) = lup;
       }
     }
   }
@@ -911,6 +927,25 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
       if (Q0 + j < g.W)
         *reinterpret_cast<float4*>(gxT + (((size_t)b * g.H + r) * g.W + Q0 + j) * g.C + c) =
             add4(dn[j], lds[(w * kTQ + j) * 64 + lane]);
+  }
+}
+
+// ∂xT of the last pixel column of each tile column but the last += the boundary partials the
+// tile to its right wrote (col2im_tile): ∂xT + (lower + upper), in that order, after K5.
+__global__ __launch_bounds__(256) void col2im_fold(Geo g, const float4* __restrict__ cpart,
+                                                   float4* __restrict__ gxT, int b0, int nb,
+                                                   int tq_n, int tq) {
+  const int C4 = g.C >> 2;
+  const size_t n = (size_t)nb * g.H * (tq_n - 1) * C4;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    const int c4 = (int)(i % C4);
+    size_t t = i / C4;
+    const int k = 1 + (int)(t % (tq_n - 1));
+    t /= (tq_n - 1);
+    const int r = (int)(t % g.H), bl = (int)(t / g.H);
+    float4* d = gxT + (((size_t)(b0 + bl) * g.H + r) * g.W + k * tq - 1) * C4 + c4;
+    const float4* p = cpart + (((size_t)bl * g.H + r) * tq_n + k) * 2 * C4 + c4;
+    *d = add4(*d, add4(p[0], p[C4]));
   }
 }
 
@@ -1200,10 +1235,12 @@ static bool can_vec4(const Geo& g) { return g.C % 4 == 0 && g.Cg % 4 == 0; }
 
 static int bins_nch(const Geo& g) { return (g.HW * g.N + kBinChunk - 1) / kBinChunk; }
 static bool k5_fused(const Geo& g);
+constexpr int kK5TQ = 4;  // fused K5 tile columns (both element types)
+static int k5_tq_n(const Geo& g) { return (g.W + kK5TQ - 1) / kK5TQ; }
 
 // Bins workspace: start[seg][NB+1] | H[seg][nch][NBp] | R[seg][nch][NBp] |
-// sorted[seg][nch][kBinChunk] (16 B) | rec[seg][NS] (unfused K5 only) | brec[seg][NS] (int4;
-// slist, int, for the unfused K5).
+// sorted[seg][nch][kBinChunk] (16 B) | rec[seg][NS] (unfused K5 only) | cpart[seg][H][tq_n][C]
+// [2] (fused K5's boundary partials) | brec[seg][NS] (int4; slist, int, for the unfused K5).
 size_t bins_ws_bytes(const Geo& g, int nb) {
   const size_t NB = (size_t)(g.H + 1) * (g.W + 1), NS = (size_t)g.HW * g.N;
   const size_t seg = (size_t)nb * g.G, nch = bins_nch(g);
@@ -1212,6 +1249,7 @@ size_t bins_ws_bytes(const Geo& g, int nb) {
   b += 2 * al(seg * nch * bins_nbp((int)NB) * 4);
   b += al(seg * nch * kBinChunk * 16);
   if (!k5_fused(g)) b += al(seg * NS * 16);
+  else b += al(seg * g.H * k5_tq_n(g) * 2 * g.C * 4);
   b += al(seg * NS * 16);
   return b;
 }
@@ -1264,6 +1302,7 @@ struct BinsWs {
   int *start, *H, *R, *slist;
   uint4* sorted;
   float4* rec;
+  float* cpart;
   int4* brec;
 };
 static BinsWs bins_ptrs(const Geo& g, void* bins_ws, int nb) {
@@ -1281,9 +1320,13 @@ static BinsWs bins_ptrs(const Geo& g, void* bins_ws, int nb) {
   P.sorted = reinterpret_cast<uint4*>(w);
   w += al(seg * nch * kBinChunk * 16);
   P.rec = nullptr;
+  P.cpart = nullptr;
   if (!k5_fused(g)) {
     P.rec = reinterpret_cast<float4*>(w);
     w += al(seg * NS * 16);
+  } else {
+    P.cpart = reinterpret_cast<float*>(w);
+    w += al(seg * g.H * k5_tq_n(g) * 2 * g.C * 4);
   }
   P.brec = reinterpret_cast<int4*>(w);
   P.slist = reinterpret_cast<int*>(w);  // sorted lists (unfused K5) share that region
@@ -1326,6 +1369,7 @@ static BinsWs bins_view(const Geo& g, void* bins_ws, int b0, int nb, int bins_nb
   const size_t NB = (size_t)(g.H + 1) * (g.W + 1), NS = (size_t)g.HW * g.N;
   P.start += (size_t)b0 * g.G * (NB + 1);
   P.brec += (size_t)b0 * g.G * NS;
+  if (P.cpart) P.cpart += (size_t)b0 * g.H * k5_tq_n(g) * 2 * g.C;
   return P;
 }
 
@@ -1336,9 +1380,17 @@ static BinsWs bins_view(const Geo& g, void* bins_ws, int b0, int nb, int bins_nb
 template <int U, int TQ, int WPE, int TR, typename GT, typename XT>
 static void launch_c2i(const Geo& g, const XT* xT, const BinsWs& P, const GT* gcolT, float* gxT,
                        float* goff, int b0, int nb, hipStream_t s) {
+  static_assert(TQ == kK5TQ, "cpart is sized for kK5TQ tile columns");
   const int tr_n = (g.H + TR - 1) / TR, tq_n = (g.W + TQ - 1) / TQ;
   hipLaunchKernelGGL((col2im_tile<U, TQ, GT, XT, WPE, TR>), dim3(tr_n * tq_n, 1, nb),
-                     dim3((TR + 1) * 64), 0, s, g, xT, P.brec, P.start, gcolT, gxT, goff, b0, tq_n);
+                     dim3((TR + 1) * 64), 0, s, g, xT, P.brec, P.start, gcolT, gxT, goff, P.cpart,
+                     b0, tq_n);
+  if (tq_n > 1) {
+    const size_t n = (size_t)nb * g.H * (tq_n - 1) * (g.C / 4);
+    hipLaunchKernelGGL(col2im_fold, dim3((unsigned)std::min<size_t>((n + 255) / 256, 8192)),
+                       dim3(256), 0, s, g, reinterpret_cast<const float4*>(P.cpart),
+                       reinterpret_cast<float4*>(gxT), b0, nb, tq_n, TQ);
+  }
 }
 
 template <typename GT, typename XT>

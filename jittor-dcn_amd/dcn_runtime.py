@@ -15,7 +15,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DCN_LIB", os.path.join(HERE, "lib", "libdcn.so"))
 
-ABI_VERSION = 3  # include/dcn.h DCN_ABI_VERSION
+ABI_VERSION = 4  # include/dcn.h DCN_ABI_VERSION
 HOST_REUSE_FWD = 2  # include/dcn.h DCN_HOST_REUSE_FWD
 DCN_F32, DCN_BF16 = 0, 1
 DCN_BWD_COL_IN_WS = 1
@@ -76,6 +76,12 @@ SIGNATURES = {
     "dcn_backward_host": [_vp, _dp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "dcn_backward_host_ex": [_vp, _dp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                              ctypes.c_int],
+    "dcn_host_state_create": [_vp, ctypes.POINTER(_vp)],
+    "dcn_host_state_destroy": [_vp],
+    "dcn_host_state_set_chunks": [_vp, ctypes.c_int],
+    "dcn_forward_host_s": [_vp, _dp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "dcn_backward_host_s": [_vp, _dp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                            ctypes.c_int],
     "dcn_prof_enable": [_vp, ctypes.c_int],
     "dcn_prof_read": [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), _ip],
     "dcn_prof_reset": [_vp],
@@ -283,6 +289,36 @@ class Handle:
 
     def prof_reset(self):
         check(self.lib.dcn_prof_reset(self.h), "dcn_prof_reset")
+
+
+class HostState:
+    """One dcn_host_state (include/dcn.h): a module's device copies of x / offsets / weights
+    and its own workspace on `handle`, so its backward reuses its forward's columns whatever
+    other modules ran on the handle in between. Keeps the handle alive."""
+
+    def __init__(self, handle: Handle, chunks: int = 0):
+        self.handle, self.lib = handle, handle.lib
+        s = ctypes.c_void_p()
+        check(self.lib.dcn_host_state_create(handle.h, ctypes.byref(s)), "dcn_host_state_create")
+        self.s = s
+        self.host_seq = 0  # bumped by every call on this state (see HostFwdCtx)
+        if chunks:
+            self.set_chunks(chunks)
+
+    def set_chunks(self, chunks: int):
+        """Image chunks of the transfer pipeline: 0 = auto, else min(chunks, B, 16)."""
+        check(self.lib.dcn_host_state_set_chunks(self.s, int(chunks)), "dcn_host_state_set_chunks")
+
+    def close(self):
+        if getattr(self, "s", None):
+            self.lib.dcn_host_state_destroy(self.s)
+            self.s = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def ptr(a):

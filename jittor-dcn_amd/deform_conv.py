@@ -55,24 +55,28 @@ def _f32(a):
 
 class HostFwdCtx:
     """What a dcn_backward_numpy needs to reuse its forward's device state (libdcn's
-    DCN_HOST_REUSE_FWD): the exact arrays the forward uploaded and the handle's call
-    sequence number at the time. Reuse happens only when no other host call ran since."""
+    DCN_HOST_REUSE_FWD): the host state (a module's rt.HostState, or the handle's own) the
+    forward ran on, the exact arrays it uploaded and the state's call sequence number at the
+    time. Reuse happens only when no other call ran on that state since."""
 
-    __slots__ = ("handle", "seq", "arrays")
+    __slots__ = ("owner", "seq", "arrays")
 
-    def __init__(self, handle, seq, x, w_off, w, off):
+    def __init__(self, owner, seq, x, w_off, w, off):
         # the arrays themselves stay referenced (their memory cannot be recycled meanwhile);
         # they are matched by data pointer, as the library checks them
-        self.handle, self.seq, self.arrays = handle, seq, (x, w_off, w, off)
+        self.owner, self.seq, self.arrays = owner, seq, (x, w_off, w, off)
 
-    def matches(self, h, x, w_off, w, off):
-        return (self.handle is h and self.seq == h.host_seq
+    def matches(self, owner, x, w_off, w, off):
+        return (self.owner is owner and self.seq == owner.host_seq
                 and all(a.ctypes.data == b.ctypes.data and a.shape == b.shape
                         for a, b in zip(self.arrays, (x, w_off, w, off))))
 
 
-def dcn_forward_numpy(x, w_off, b_off, w, b, stride, padding, handle=None, return_ctx=False):
-    """out, off = DeformConv2d.execute on host arrays (one libdcn call). With return_ctx,
+def dcn_forward_numpy(x, w_off, b_off, w, b, stride, padding, handle=None, return_ctx=False,
+                      state=None):
+    """out, off = DeformConv2d.execute on host arrays (one libdcn call). state: a
+    rt.HostState (one per module; or a callable returning it) to run on instead of the
+    handle's own. With return_ctx,
     also a HostFwdCtx for dcn_backward_numpy(ctx=...)."""
     x, w_off, b_off, w = _f32(x), _f32(w_off), _f32(b_off), _f32(w)
     b = None if b is None else _f32(b)
@@ -86,50 +90,68 @@ def dcn_forward_numpy(x, w_off, b_off, w, b, stride, padding, handle=None, retur
         off = np.empty((0, w_off.shape[0], Ho, Wo), np.float32)
         # no forward state to reuse: dcn_backward_numpy takes ctx=None (and B == 0 there too)
         return (out, off, None) if return_ctx else (out, off)
-    h = handle or rt.default_handle()  # after the empty-batch case: it launches nothing
+    # after the empty-batch case: it launches nothing
+    if callable(state):  # a module's host_state, resolved only when there is work
+        state = state()
+    h = state.handle if state is not None else (handle or rt.default_handle())
     desc = rt.make_desc(B, C, H, W, O, (kh, kw), stride, padding, bias=b is not None)
     Ho, Wo = rt.out_shape(desc)
     out = hostmem.empty((B, O, Ho, Wo))
     off = hostmem.empty((B, w_off.shape[0], Ho, Wo))
-    h.host_seq += 1
-    rt.check(h.lib.dcn_forward_host(h.h, desc, rt.ptr(x), rt.ptr(w_off), rt.ptr(b_off), rt.ptr(w),
-                                    rt.ptr(b), rt.ptr(out), rt.ptr(off)), "dcn_forward_host")
+    owner = state if state is not None else h
+    owner.host_seq += 1
+    args = (desc, rt.ptr(x), rt.ptr(w_off), rt.ptr(b_off), rt.ptr(w), rt.ptr(b), rt.ptr(out),
+            rt.ptr(off))
+    if state is not None:
+        rt.check(h.lib.dcn_forward_host_s(state.s, *args), "dcn_forward_host_s")
+    else:
+        rt.check(h.lib.dcn_forward_host(h.h, *args), "dcn_forward_host")
     if return_ctx:
-        return out, off, HostFwdCtx(h, h.host_seq, x, w_off, w, off)
+        return out, off, HostFwdCtx(owner, owner.host_seq, x, w_off, w, off)
     return out, off
 
 
 def dcn_backward_numpy(x, off, w_off, w, has_bias, grad_out, stride, padding, handle=None,
-                       ctx=None):
-    """Grads of DeformConv2d.execute (dict keyed like the state dict, plus 'x', 'offset').
-    ctx: the forward's HostFwdCtx; when nothing else ran on the handle since, x / off /
-    weights are not uploaded again and the forward's columns are reused."""
+                       ctx=None, state=None, offset_grad=True):
+    """Grads of DeformConv2d.execute (dict keyed like the state dict, plus 'x' and, with
+    offset_grad, 'offset'). ctx: the forward's HostFwdCtx; when nothing else ran on its
+    host state since, x / off / weights are not uploaded again and the forward's columns
+    are reused. state: the rt.HostState to run on (default: ctx's, else the handle's)."""
     x, off, w_off, w, grad_out = map(_f32, (x, off, w_off, w, grad_out))
     B, C, H, W = x.shape
     O, _, kh, kw = w.shape
     if B == 0:  # empty batch: nothing sampled, every parameter gradient is zero
         g = {"x": np.empty_like(x), "weight": np.zeros_like(w),
              "offset_conv.weight": np.zeros_like(w_off),
-             "offset_conv.bias": np.zeros(w_off.shape[0], np.float32),
-             "offset": np.empty_like(off)}
+             "offset_conv.bias": np.zeros(w_off.shape[0], np.float32)}
+        if offset_grad:
+            g["offset"] = np.empty_like(off)
         if has_bias:
             g["bias"] = np.zeros(O, np.float32)
         return g
-    h = handle or (ctx.handle if ctx is not None else rt.default_handle())
+    if callable(state):
+        state = state()
+    if state is None and ctx is not None and isinstance(ctx.owner, rt.HostState):
+        state = ctx.owner
+    h = state.handle if state is not None else (
+        handle or (ctx.owner if ctx is not None else rt.default_handle()))
+    owner = state if state is not None else h
     desc = rt.make_desc(B, C, H, W, O, (kh, kw), stride, padding, bias=has_bias)
     g = {"x": hostmem.empty_like(x), "weight": hostmem.empty_like(w),
          "offset_conv.weight": hostmem.empty_like(w_off),
-         "offset_conv.bias": np.empty(w_off.shape[0], np.float32),
-         "offset": hostmem.empty_like(off)}
+         "offset_conv.bias": np.empty(w_off.shape[0], np.float32)}
+    if offset_grad:
+        g["offset"] = hostmem.empty_like(off)
     gb = np.empty(O, np.float32) if has_bias else None
-    flags = rt.HOST_REUSE_FWD if ctx is not None and ctx.matches(h, x, w_off, w, off) else 0
-    h.host_seq += 1
-    rt.check(h.lib.dcn_backward_host_ex(h.h, desc, rt.ptr(x), rt.ptr(off), rt.ptr(w_off),
-                                        rt.ptr(w), rt.ptr(grad_out), rt.ptr(g["x"]),
-                                        rt.ptr(g["weight"]), rt.ptr(gb),
-                                        rt.ptr(g["offset_conv.weight"]),
-                                        rt.ptr(g["offset_conv.bias"]), rt.ptr(g["offset"]),
-                                        flags), "dcn_backward_host_ex")
+    flags = rt.HOST_REUSE_FWD if ctx is not None and ctx.matches(owner, x, w_off, w, off) else 0
+    owner.host_seq += 1
+    args = (desc, rt.ptr(x), rt.ptr(off), rt.ptr(w_off), rt.ptr(w), rt.ptr(grad_out),
+            rt.ptr(g["x"]), rt.ptr(g["weight"]), rt.ptr(gb), rt.ptr(g["offset_conv.weight"]),
+            rt.ptr(g["offset_conv.bias"]), rt.ptr(g.get("offset")), flags)
+    if state is not None:
+        rt.check(h.lib.dcn_backward_host_s(state.s, *args), "dcn_backward_host_s")
+    else:
+        rt.check(h.lib.dcn_backward_host_ex(h.h, *args), "dcn_backward_host_ex")
     if has_bias:
         g["bias"] = gb
     return g
@@ -290,12 +312,21 @@ class DeformConv2dNumpy(Module):
         self.weight = Parameter(rng.normal(0.0, std, (out_channels, in_channels, *self.kernel_size)))
         self.bias = Parameter(np.zeros(out_channels, np.float32)) if bias else None
         self._ctx = None
+        self._hstate = None
+
+    def host_state(self):
+        """This module's device state (rt.HostState on the thread's default handle): its
+        backward reuses its own forward's columns however many modules share the handle."""
+        h = rt.default_handle()
+        if self._hstate is None or self._hstate.handle is not h:
+            self._hstate = rt.HostState(h)
+        return self._hstate
 
     def execute(self, x):
         x = _f32(x)
         out, off, hctx = dcn_forward_numpy(x, self.offset_conv.weight, self.offset_conv.bias,
                                            self.weight, self.bias, self.stride, self.padding,
-                                           return_ctx=True)
+                                           return_ctx=True, state=self.host_state)
         self._ctx = (x, off, hctx) if self.training else None
         return out
 
@@ -305,7 +336,8 @@ class DeformConv2dNumpy(Module):
             raise RuntimeError("backward() needs a preceding execute() in training mode")
         x, off, hctx = self._ctx
         g = dcn_backward_numpy(x, off, self.offset_conv.weight, self.weight, self.bias is not None,
-                               grad_out, self.stride, self.padding, ctx=hctx)
+                               grad_out, self.stride, self.padding, ctx=hctx,
+                               state=self.host_state, offset_grad=False)
         for name, p in self.named_parameters():
             p.grad = g[name] if p.grad is None else p.grad + g[name]
         return g["x"]
@@ -382,24 +414,26 @@ if HAVE_JITTOR:  # pragma: no cover
         """jt.Function whose execute/grad call libdcn; inputs are the module's Vars so
         Jittor autodiff routes gradients to offset_conv.{weight,bias}, weight, bias."""
 
-        def execute(self, x, w_off, b_off, w, b, stride, padding):
-            self.stride, self.padding = stride, padding
+        def execute(self, x, w_off, b_off, w, b, stride, padding, state):
+            self.stride, self.padding, self.state = stride, padding, state
             self.has_bias = b is not None
             xn, won, wn = x.numpy(), w_off.numpy(), w.numpy()
             xn, won, wn = _f32(xn), _f32(won), _f32(wn)
             out, off, hctx = dcn_forward_numpy(xn, won, b_off.numpy(), wn,
                                                None if b is None else b.numpy(), stride, padding,
-                                               return_ctx=True)
+                                               return_ctx=True, state=state)
             self.saved = (xn, off, won, wn, hctx)
             return jt.array(out)
 
         def grad(self, grad_out):
             xn, off, won, wn, hctx = self.saved
             g = dcn_backward_numpy(xn, off, won, wn, self.has_bias, grad_out.numpy(),
-                                   self.stride, self.padding, ctx=hctx)
+                                   self.stride, self.padding, ctx=hctx, state=self.state,
+                                   offset_grad=False)
             gb = jt.array(g["bias"]) if self.has_bias else None
             return (jt.array(g["x"]), jt.array(g["offset_conv.weight"]),
-                    jt.array(g["offset_conv.bias"]), jt.array(g["weight"]), gb, None, None)
+                    jt.array(g["offset_conv.bias"]), jt.array(g["weight"]), gb, None, None,
+                    None)
 
     class DeformConv2d(jnn.Module):
         def __init__(self, in_channels, out_channels, kernel_size=3, stride=1, padding=1,
@@ -419,10 +453,14 @@ if HAVE_JITTOR:  # pragma: no cover
             self.bias = jt.init.constant(shape=[out_channels], value=0.0) if bias else None
             self.offset_conv.weight = jt.zeros_like(self.offset_conv.weight)
             self.offset_conv.bias = jt.zeros_like(self.offset_conv.bias)
+            self._hstate = None
+
+        host_state = DeformConv2dNumpy.host_state
 
         def execute(self, x):
             return _DCNFunction.apply(x, self.offset_conv.weight, self.offset_conv.bias,
-                                      self.weight, self.bias, self.stride, self.padding)
+                                      self.weight, self.bias, self.stride, self.padding,
+                                      self.host_state)
     class _RoIPoolFunction(jt.Function):
         """jt.Function for both RoI pools: ∂features and ∂offsets reach Jittor autodiff
         (the boxes get none, as they come from the data)."""

@@ -110,6 +110,18 @@ def test_config3_full_batch_every_tensor_vs_c_oracle(gpu_handle):
     out, off, g = _device_fwd_bwd(gpu_handle, c)
     ro, roff, rg = _c_oracle_all(c, off)
     _check_all(out, off, g, ro, roff, rg, "config3")
+    # the host-pointer path on a module's state: auto image chunks (205 MB of x -> 9), the
+    # transfers pipelined with the kernels, the backward reusing each chunk's columns
+    from deform_conv import dcn_backward_numpy, dcn_forward_numpy
+    st = rt.HostState(gpu_handle)
+    hout, hoff, ctx = dcn_forward_numpy(c["x"], c["w_off"], c["b_off"], c["w"], c["b"],
+                                        c["stride"], c["padding"], state=st, return_ctx=True)
+    # the per-image offset conv does not depend on how the batch is cut
+    np.testing.assert_array_equal(hoff, off, err_msg="config3 host offsets")
+    hg = dcn_backward_numpy(c["x"], hoff, c["w_off"], c["w"], True, c["grad_out"], c["stride"],
+                            c["padding"], ctx=ctx)
+    st.close()
+    _check_all(hout, hoff, hg, ro, roff, rg, "config3 host (chunked)")
 
 
 def test_config3_full_size_bitwise_reproducible(gpu_handle):

@@ -36,13 +36,13 @@ def jdc():
         jittor_standin.uninstall()
 
 
-def _oracle_fwd(x, w_off, b_off, w, b, stride, padding, handle=None, return_ctx=False):
+def _oracle_fwd(x, w_off, b_off, w, b, stride, padding, return_ctx=False, **kw):
     out, off, _ = O.forward(x, w_off, b_off, w, b, stride, padding)
     res = out.astype(np.float32), off.astype(np.float32)
     return res + (None,) if return_ctx else res
 
 
-def _oracle_bwd(x, off, w_off, w, has_bias, grad_out, stride, padding, handle=None, ctx=None):
+def _oracle_bwd(x, off, w_off, w, has_bias, grad_out, stride, padding, **kw):
     b = np.zeros(w.shape[0], np.float32)
     _, _, cache = O.forward(x, w_off, np.zeros(w_off.shape[0], np.float32), w, b, stride,
                             padding, offsets=off)
