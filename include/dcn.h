@@ -37,7 +37,7 @@ extern "C" {
 #endif
 
 #define DCN_ABI_VERSION 4 /* 2: dcn_allreduce_grads takes a dtype; dcn_set_comm, dcn_set_grad_stream;
-                             3: dcn_backward_host_ex; 4: dcn_host_state */
+                             3: dcn_backward_host_ex; 4: dcn_host_state, dcn_host_alloc */
 
 typedef enum {
   DCN_OK = 0,
@@ -89,6 +89,13 @@ int dcn_synchronize(dcn_handle* h);
 /* ---- device memory helpers (ctypes callers without another runtime) -------- */
 int dcn_malloc(dcn_handle* h, size_t bytes, void** ptr);
 int dcn_free(dcn_handle* h, void* ptr);
+/* Page-locked host memory (hipHostMalloc): the host path's recycled output arrays
+ * (jittor-dcn_amd/hostmem.py). A device-to-host copy into pageable memory runs as a copy
+ * kernel through a staging buffer, on the CUs beside the path's own kernels (r03 trace:
+ * the offset conv of a pipelined chunk 3x slower beside it); into page-locked memory it
+ * is a DMA. */
+int dcn_host_alloc(dcn_handle* h, size_t bytes, void** ptr);
+int dcn_host_free(void* ptr);
 int dcn_memcpy_h2d(dcn_handle* h, void* dst, const void* src, size_t bytes);
 int dcn_memcpy_d2h(dcn_handle* h, void* dst, const void* src, size_t bytes);
 int dcn_memset_zero(dcn_handle* h, void* dst, size_t bytes);
@@ -153,7 +160,7 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x,
  *
  * The batch is cut into image chunks whose transfers run beside the kernels (the upload
  * of chunk i+1 and the download of chunk i-1 while chunk i computes). fp32 only: about
- * 24 MB of x per chunk, at most 16 chunks (dcn_host_state_set_chunks); bf16 and a handle
+ * 52 MB of x per chunk, at most 16 chunks (dcn_host_state_set_chunks); bf16 and a handle
  * with a communicator use one chunk. With several chunks the parameter gradients are
  * the chunk partials summed in chunk order (deterministic; not bitwise the one-chunk
  * sums). The dcn_*_host calls below use the handle's own host state; a network of

@@ -838,6 +838,19 @@ int dcn_free(dcn_handle* h, void* ptr) {
   return DCN_OK;
 }
 
+int dcn_host_alloc(dcn_handle* h, size_t bytes, void** ptr) {
+  if (!ptr) return fail(DCN_ERR_INVALID, "null out pointer");
+  *ptr = nullptr;
+  DCN_TRY(set_device(h));
+  HIP_TRY(hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocDefault));
+  return DCN_OK;
+}
+
+int dcn_host_free(void* ptr) {
+  if (ptr) HIP_TRY(hipHostFree(ptr));
+  return DCN_OK;
+}
+
 int dcn_memcpy_h2d(dcn_handle* h, void* dst, const void* src, size_t bytes) {
   DCN_TRY(set_device(h));
   HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->stream));
@@ -1164,7 +1177,9 @@ int d2h(dcn_handle* h, hipStream_t s, void* dst, const void* src, size_t bytes) 
 // kernels, instead of transfers + kernels. Each chunk has its own workspace slice, which
 // keeps that chunk's columns from the forward for the backward.
 constexpr int kMaxHostChunks = 16;
-constexpr size_t kHostChunkBytes = size_t(24) << 20;  // auto: about this much x per chunk
+// auto: about this much x per chunk. r03, config 3 (205 MB of x), fwd + bwd incl. PCIe:
+// 1 chunk 23.4 ms, 2 17.2, 4 17.0, 8 18.1, 9 (24 MB) 17.9
+constexpr size_t kHostChunkBytes = size_t(52) << 20;
 
 struct ChunkPlan {
   int n = 1;
@@ -1222,7 +1237,7 @@ struct PipelineDrain {
   }
 };
 
-// stream `s` waits for event slot k, recorded on stream `from`
+// stream `s` waits for event slot k, recorded on stream `from` now
 int hop(dcn_handle* h, int k, hipStream_t from, hipStream_t s) {
   HIP_TRY(hipEventRecord(h->hev[k], from));
   HIP_TRY(hipStreamWaitEvent(s, h->hev[k], 0));
@@ -1264,9 +1279,11 @@ int forward_host(dcn_host_state* s, const dcn_desc* d, const float* x, const flo
   DCN_TRY(h2d(h, h->stream, dbo, b_off, g.J * es));
   DCN_TRY(h2d(h, h->stream, dw, w, nw));
   if (d->has_bias) DCN_TRY(h2d(h, h->stream, db_, b, g.O * es));
+  // chunk i's download waits for the event recorded right after its kernels were queued
+  // (not for whatever the stream holds by the time the download is issued)
   auto download = [&](int i) -> int {
     const size_t b0 = P.b0[i], nb = P.d[i].B;
-    DCN_TRY(hop(h, 2 * i + 1, h->stream, h->cout));
+    HIP_TRY(hipStreamWaitEvent(h->cout, h->hev[2 * i + 1], 0));
     DCN_TRY(d2h(h, h->cout, (char*)out + b0 * oi, dout + b0 * oi, nb * oi));
     if (off) DCN_TRY(d2h(h, h->cout, (char*)off + b0 * fi, doff + b0 * fi, nb * fi));
     return DCN_OK;
@@ -1279,6 +1296,7 @@ int forward_host(dcn_host_state* s, const dcn_desc* d, const float* x, const flo
                         (float*)dw, (float*)db_, (float*)(dout + b0 * oi),
                         (float*)(doff + b0 * fi), (char*)s->ws + P.ws_off[i],
                         P.ws_off[i + 1] - P.ws_off[i]));
+    HIP_TRY(hipEventRecord(h->hev[2 * i + 1], h->stream));
     if (i > 0) DCN_TRY(download(i - 1));
   }
   DCN_TRY(download(P.n - 1));
@@ -1339,9 +1357,9 @@ int backward_host(dcn_host_state* s, const dcn_desc* d, const float* x, const fl
     DCN_TRY(h2d(h, h->stream, dwo, w_off, nwo * es));
     DCN_TRY(h2d(h, h->stream, dw, w, nw * es));
   }
-  auto download = [&](int i) -> int {
+  auto download = [&](int i) -> int {  // as the forward's
     const size_t b0 = P.b0[i], nb = P.d[i].B;
-    DCN_TRY(hop(h, 2 * i + 1, h->stream, h->cout));
+    HIP_TRY(hipStreamWaitEvent(h->cout, h->hev[2 * i + 1], 0));
     DCN_TRY(d2h(h, h->cout, (char*)grad_x + b0 * xi, dgx + b0 * xi, nb * xi));
     if (grad_off_out)
       DCN_TRY(d2h(h, h->cout, (char*)grad_off_out + b0 * fi, dgoff + b0 * fi, nb * fi));
@@ -1364,6 +1382,7 @@ int backward_host(dcn_host_state* s, const dcn_desc* d, const float* x, const fl
                          grad_off_out ? (float*)(dgoff + b0 * fi) : nullptr,
                          (char*)s->ws + P.ws_off[i], P.ws_off[i + 1] - P.ws_off[i],
                          reuse ? DCN_BWD_COL_IN_WS : 0));
+    HIP_TRY(hipEventRecord(h->hev[2 * i + 1], h->stream));
     if (i > 0) DCN_TRY(download(i - 1));
   }
   if (P.n > 1)  // fp32 only (chunk_count)

@@ -751,8 +751,37 @@ __global__ __launch_bounds__(256) void bins_emit(Geo g, int nch, int NB,
 // tree). Used for deform_groups == 1, C % 4 == 0, C <= 256.
 // ---------------------------------------------------------------------------
 
+// Packed fp32 (v_pk_fma_f32 / v_pk_add_f32 / v_pk_mul_f32: two lanes' elements per
+// instruction): each element's operation is the scalar one, so the results are the same bits.
+// K5 is bound by VALU issue (r03 PMC at config 3: 202 M VALU instructions, ≈112 per sample),
+// so halving the elementwise ones is its lever.
+__device__ __forceinline__ f32x2 lo2(float4 v) { return f32x2{v.x, v.y}; }
+__device__ __forceinline__ f32x2 hi2(float4 v) { return f32x2{v.z, v.w}; }
+__device__ __forceinline__ float4 cat4(f32x2 a, f32x2 b) { return make_float4(a.x, a.y, b.x, b.y); }
 __device__ __forceinline__ float4 fma4(float w, float4 g, float4 a) {
-  return make_float4(fmaf(w, g.x, a.x), fmaf(w, g.y, a.y), fmaf(w, g.z, a.z), fmaf(w, g.w, a.w));
+  const f32x2 w2 = {w, w};
+  return cat4(__builtin_elementwise_fma(w2, lo2(g), lo2(a)),
+              __builtin_elementwise_fma(w2, hi2(g), hi2(a)));
+}
+// acc_dgrad on 4 channels with the per-element dbilerp_row / _col in packed form; the
+// per-channel accumulation chains stay in order x, y, z, w (same bits as acc_dgrad)
+__device__ __forceinline__ void acc_dgrad4p(float fr, float fc, float4 gv, float4 a, float4 b,
+                                            float4 c, float4 d, float& diy, float& dix) {
+  const f32x2 fr2 = {fr, fr}, fc2 = {fc, fc}, gr2 = {1.0f - fr, 1.0f - fr},
+              gc2 = {1.0f - fc, 1.0f - fc};
+  // dbilerp_row = fmaf(fc, d - b, (1-fc) * (c - a)); dbilerp_col = fmaf(fr, d - c, (1-fr) * (b - a))
+  const f32x2 rl = __builtin_elementwise_fma(fc2, lo2(d) - lo2(b), gc2 * (lo2(c) - lo2(a)));
+  const f32x2 rh = __builtin_elementwise_fma(fc2, hi2(d) - hi2(b), gc2 * (hi2(c) - hi2(a)));
+  const f32x2 sl = __builtin_elementwise_fma(fr2, lo2(d) - lo2(c), gr2 * (lo2(b) - lo2(a)));
+  const f32x2 sh = __builtin_elementwise_fma(fr2, hi2(d) - hi2(c), gr2 * (hi2(b) - hi2(a)));
+  diy = fmaf(gv.x, rl.x, diy);
+  dix = fmaf(gv.x, sl.x, dix);
+  diy = fmaf(gv.y, rl.y, diy);
+  dix = fmaf(gv.y, sl.y, dix);
+  diy = fmaf(gv.z, rh.x, diy);
+  dix = fmaf(gv.z, sh.x, dix);
+  diy = fmaf(gv.w, rh.y, diy);
+  dix = fmaf(gv.w, sh.y, dix);
 }
 __device__ __forceinline__ float4 add4(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
@@ -768,9 +797,11 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
                                                            float* __restrict__ cpart, int b0,
                                                            int tq_n) {
   constexpr int kC2iThreads = (kTR + 1) * 64, WR = kTR + 1, WQ = kTQ + 1;
-  // float4 slots: the xT window, then the upper rows
-  constexpr int WIN = WR * WQ * 64, UPR = kTR * kTQ * 64;
-  __shared__ float4 lds[WIN > UPR ? WIN : UPR];
+  // float4 slots: a zero row (window row -1: wave 0's ∂offset reads it only at image row
+  // -1, so no select), the xT window; then the upper rows
+  constexpr int ZR = WQ * 64, WIN = WR * WQ * 64, UPR = kTR * kTQ * 64;
+  __shared__ float4 lds_[ZR + WIN > UPR ? ZR + WIN : UPR];
+  float4* const lds = lds_ + ZR;  // the window; the upper rows use lds_ from slot 0
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const Block3 blk = xcd_block();
@@ -817,108 +848,169 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
   const int nbin = tq_i == tq_n - 1 ? g.W - Q0 + 1 : kTQ;
   int bst[kTQ + 2];
 #pragma unroll
-  for (int k = 0; k <= kTQ + 1; ++k) bst[k] = act ? st[bin0 + min(k, nbin)] : 0;
+  for (int k = 0; k <= kTQ + 1; ++k)  // wave-uniform: scalar registers, scalar loop bounds
+    bst[k] = __builtin_amdgcn_readfirstlane(act ? st[bin0 + min(k, nbin)] : 0);
   const int rowlo = bst[0], rowhi = bst[nbin];
-  const int cc = cok ? c : 0;  // clamped channel: loads never need a guard
-  // Software pipeline over the row's records (contiguous across its bins): batch k+1's
-  // records (v_readlane from a 64-record page) and ∂colT rows are issued before batch
-  // k is consumed. Batches never straddle a bin, so each bin's compute keeps static
-  // accumulator indices while the prefetch flows across bin boundaries.
-  int p0 = rowlo;
-  int4 pg = p0 + lane < rowhi ? rb[p0 + lane] : make_int4(0, 0, 0, 0);
+  // Software pipeline over the row's records (contiguous across its bins), 64 records (a
+  // segment) at a time: lane l holds record seg+l (a buffer load that returns 0 past the
+  // end, so no branch), and every load inside a segment is
+  // unconditional (indices clamped into it). hipcc then counts vmcnt across the loop instead
+  // of draining it at each conditional load (r02: one conditional page reload per batch made
+  // every batch wait for all loads and ∂offset stores in flight). Batch k+1's records
+  // (v_readlane) and ∂colT rows are issued before batch k is consumed. Batches never
+  // straddle a bin, so each bin's compute keeps static accumulator indices while the
+  // prefetch flows across bin boundaries. A sample's ∂offset stays in the lane of its
+  // record until the segment ends: one scattered vector store per segment, none per sample.
+  const auto rrec = __builtin_amdgcn_make_buffer_rsrc(const_cast<int4*>(rb), 0,
+                                                      (int)(g.HW * g.N * 16), 0x00020000);
+  int seg = rowlo, segend = rowlo;
+  int rowhi_c = bst[1] > rowlo ? bst[1] : rowhi;  // end of the current phase's records
+  int4 pg = make_int4(0, 0, 0, 0);
+  auto load_seg = [&](int s0) {
+    seg = s0;
+    segend = min(s0 + 64, rowhi_c);
+    const unsigned o = s0 + lane < segend ? (unsigned)(s0 + lane) * 16u : 0x80000000u;
+    const auto q = __builtin_amdgcn_raw_buffer_load_b128(rrec, o, 0, 0);
+    pg = make_int4((int)q[0], (int)q[1], (int)q[2], (int)q[3]);
+  };
   int4 nR[U];
-  // rows in flight as loaded (bf16: 8 B per lane, converted when consumed)
+  // rows in flight as loaded (bf16: 8 B per lane, converted when consumed); buffer loads, the
+  // lanes past C out of range (they read 0: no select on the values)
   typedef typename std::conditional<sizeof(GT) == 2, uint2, float4>::type RowT;
   RowT nx[U];
+  const auto rcol = __builtin_amdgcn_make_buffer_rsrc(const_cast<GT*>(gb), 0,
+                                                      (int)((size_t)g.HW * g.K * sizeof(GT)),
+                                                      0x00020000);
+  const unsigned coff = cok ? (unsigned)(c * sizeof(GT)) : 0x80000000u;
   auto issue = [&](int ni) {
-    if (ni >= rowhi) return;
-    if (ni + U > p0 + 64) {  // next page (rows of more than 64 samples)
-      p0 = ni;
-      pg = p0 + lane < rowhi ? rb[p0 + lane] : make_int4(0, 0, 0, 0);
-    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int l = min(ni + u, rowhi - 1) - p0;
+      const int l = min(ni + u, segend - 1) - seg;  // wave-uniform, in [0, 64)
       nR[u] = make_int4(__builtin_amdgcn_readlane(pg.x, l), __builtin_amdgcn_readlane(pg.y, l),
                         __builtin_amdgcn_readlane(pg.z, l), __builtin_amdgcn_readlane(pg.w, l));
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) nx[u] = *reinterpret_cast<const RowT*>(gb + nR[u].x + cc);
+    for (int u = 0; u < U; ++u) {
+      const unsigned o = (unsigned)nR[u].x * (unsigned)sizeof(GT) + coff;
+      if constexpr (sizeof(GT) == 2) {
+        const auto q = __builtin_amdgcn_raw_buffer_load_b64(rcol, o, 0, 0);
+        nx[u] = make_uint2(q[0], q[1]);
+      } else {
+        const auto q = __builtin_amdgcn_raw_buffer_load_b128(rcol, o, 0, 0);
+        nx[u] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]),
+                            __uint_as_float(q[3]));
+      }
+    }
   };
-  issue(rowlo);  // (nothing for a wave past the last bin row: rowlo == rowhi == 0)
+  // two phases: bin column 0 (its left-boundary partials die with it), then columns 1..
+  const int mid = bst[1];
+  const bool any0 = act && mid > rowlo, any1 = act && rowhi > mid;
+  if (any0) {
+    load_seg(rowlo);
+    issue(rowlo);
+  } else if (any1) {
+    load_seg(mid);
+    issue(mid);
+  }
 #pragma unroll
   for (int k = 0; k < WIT; ++k)
     if (tid + k * kC2iThreads < WIN) lds[tid + k * kC2iThreads] = wv[k];
+  for (int k = tid; k < ZR; k += kC2iThreads) lds_[k] = z4;
   lds_barrier();
-  if (act) {
+  // the samples [rlo, rhi) of bin columns BJ0..BJ1-1, segment by segment (the first segment
+  // already loaded and issued)
+  auto phase = [&](auto BJ0, auto BJ1, int rlo, int rhi) __attribute__((always_inline)) {
+    constexpr int kB0 = decltype(BJ0)::value, kB1 = decltype(BJ1)::value;
+    for (int s0 = rlo;;) {
+      float oy = 0.f, ox = 0.f;  // ∂offset of record seg+lane
 #pragma unroll
-    for (int bj = 0; bj <= kTQ; ++bj) {
-      if (bj >= nbin) break;
-      const int lo = bst[bj], hi = bst[bj + 1];
-      for (int i = lo; i < hi; i += U) {
-        int4 R[U];
-        float4 gv[U];
+      for (int bj = kB0; bj < kB1; ++bj) {
+        if (bj >= nbin) break;
+        const int lo = max(bst[bj], seg), hi = min(bst[bj + 1], segend);
+        for (int i = lo; i < hi; i += U) {
+          int4 R[U];
+          float4 gv[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          R[u] = nR[u];
-          if constexpr (sizeof(GT) == 2) {
-            const uint2 q = nx[u];
-            gv[u] = cok ? make_float4(__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
-                                      __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u))
-                        : z4;
-          } else {
-            gv[u] = cok ? nx[u] : z4;
+          for (int u = 0; u < U; ++u) {
+            R[u] = nR[u];
+            if constexpr (sizeof(GT) == 2) {
+              const uint2 q = nx[u];
+              gv[u] = make_float4(__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
+                                  __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u));
+            } else {
+              gv[u] = nx[u];
+            }
           }
-        }
-        issue(i + U < hi ? i + U : hi);  // next batch of this bin, else the next bin's first
+          issue(i + U < hi ? i + U : hi);  // next batch of this bin, else the next bin's first
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (i + u >= hi) break;
-          const float fr = __int_as_float(R[u].y), fc = __int_as_float(R[u].z);
-          const float gr = 1.0f - fr, gc = 1.0f - fc;
-          if (bj < kTQ) {
-            up[bj] = fma4(gr * fc, gv[u], up[bj]);
-            dn[bj] = fma4(fr * fc, gv[u], dn[bj]);
-          }
-          if (bj >= 1) {
-            up[bj - 1] = fma4(gr * gc, gv[u], up[bj - 1]);
-            dn[bj - 1] = fma4(fr * gc, gv[u], dn[bj - 1]);
-          } else {
-            lup = fma4(gr * gc, gv[u], lup);
-            ldn = fma4(fr * gc, gv[u], ldn);
-          }
-          if (drow) {
-            // corners (r0, c0) .. (r0+1, c0+1) at window (w-1, bj) .. (w, bj+1); column
-            // bj+1 = kTQ+1 is W (the last tile column's bin W): outside the image
-            const float4* w4 = lds + ((w - 1) * WQ + bj) * 64 + lane;
-            const bool rA = w >= 1, cB = bj + 1 <= kTQ;
-            const float4 a = rA ? w4[0] : z4;
-            const float4 bq = (rA && cB) ? w4[64] : z4;
-            const float4 cq = w4[WQ * 64];
-            const float4 d = cB ? w4[(WQ + 1) * 64] : z4;
-            float diy = 0.f, dix = 0.f;
-            acc_dgrad(fr, fc, gv[u], a, bq, cq, d, diy, dix);
-            diy = wave_sum(diy);
-            dix = wave_sum(dix);
-            if (lane == 0) {
-              gob[R[u].w] = diy * sy;
-              gob[(size_t)g.N * g.HW + R[u].w] = dix * sx;
+          for (int u = 0; u < U; ++u) {
+            if (i + u >= hi) break;
+            const float fr = __int_as_float(R[u].y), fc = __int_as_float(R[u].z);
+            const float gr = 1.0f - fr, gc = 1.0f - fc;
+            if (bj < kTQ) {
+              up[bj] = fma4(gr * fc, gv[u], up[bj]);
+              dn[bj] = fma4(fr * fc, gv[u], dn[bj]);
+            }
+            if (bj >= 1) {
+              up[bj - 1] = fma4(gr * gc, gv[u], up[bj - 1]);
+              dn[bj - 1] = fma4(fr * gc, gv[u], dn[bj - 1]);
+            } else {
+              lup = fma4(gr * gc, gv[u], lup);
+              ldn = fma4(fr * gc, gv[u], ldn);
+            }
+            if (drow) {
+              // corners (r0, c0) .. (r0+1, c0+1) at window (w-1, bj) .. (w, bj+1); column
+              // bj+1 = kTQ+1 is W (the last tile column's bin W): outside the image
+              const float4* w4 = lds + ((w - 1) * WQ + bj) * 64 + lane;
+              const bool cB = bj + 1 <= kTQ;  // (bj is unrolled: a constant)
+              const float4 a = w4[0];
+              const float4 bq = cB ? w4[64] : z4;
+              const float4 cq = w4[WQ * 64];
+              const float4 d = cB ? w4[(WQ + 1) * 64] : z4;
+              float diy = 0.f, dix = 0.f;
+              acc_dgrad4p(fr, fc, gv[u], a, bq, cq, d, diy, dix);
+              diy = wave_sum(diy);
+              dix = wave_sum(dix);
+              const bool mine = lane == i + u - seg;
+              oy = mine ? diy : oy;
+              ox = mine ? dix : ox;
             }
           }
         }
       }
-      if (bj == 0 && tq_i > 0 && cok) {  // the left boundary partials of bin column Q0
-        const size_t rs = (size_t)tq_n * 2 * g.C;  // pixel-row stride
-        float* cp = cpart + (size_t)bl * g.H * rs + (size_t)tq_i * 2 * g.C + c;
-        if (w < kTR && br < g.H) *reinterpret_cast<float4*>(cp + br * rs) = ldn;
-        if (w >= 1) *reinterpret_cast<float4*>(cp + (br - 1) * rs + g.C) = lup;
+      if (drow && seg + lane < segend) {
+        gob[pg.w] = oy * sy;
+        gob[(size_t)g.N * g.HW + pg.w] = ox * sx;
       }
+      s0 += 64;
+      if (s0 >= rhi) break;
+      load_seg(s0);
+      issue(s0);
     }
+  };
+  if (any0) {
+    auto rhi0 = mid;  // segments end at the bin column's end
+    rowhi_c = rhi0;
+    phase(std::integral_constant<int, 0>(), std::integral_constant<int, 1>(), rowlo, rhi0);
+  }
+  if (act && tq_i > 0 && cok) {  // bin column Q0 is done: its left boundary partials
+    const size_t rs = (size_t)tq_n * 2 * g.C;  // pixel-row stride
+    float* cp = cpart + (size_t)bl * g.H * rs + (size_t)tq_i * 2 * g.C + c;
+    if (w < kTR && br < g.H) *reinterpret_cast<float4*>(cp + br * rs) = ldn;
+    if (w >= 1) *reinterpret_cast<float4*>(cp + (br - 1) * rs + g.C) = lup;
+  }
+  if (any1) {
+    rowhi_c = rowhi;
+    if (any0) {
+      load_seg(mid);
+      issue(mid);
+    }
+    phase(std::integral_constant<int, 1>(), std::integral_constant<int, kTQ + 1>(), mid, rowhi);
   }
   __syncthreads();  // window no longer read: reuse the LDS for the upper rows
   if (w >= 1)
 #pragma unroll
-    for (int j = 0; j < kTQ; ++j) lds[((w - 1) * kTQ + j) * 64 + lane] = up[j];
+    for (int j = 0; j < kTQ; ++j) lds_[((w - 1) * kTQ + j) * 64 + lane] = up[j];
   __syncthreads();
   const int r = R0 + w;
   if (w < kTR && r < g.H && cok) {
@@ -926,7 +1018,7 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
     for (int j = 0; j < kTQ; ++j)
       if (Q0 + j < g.W)
         *reinterpret_cast<float4*>(gxT + (((size_t)b * g.H + r) * g.W + Q0 + j) * g.C + c) =
-            add4(dn[j], lds[(w * kTQ + j) * 64 + lane]);
+            add4(dn[j], lds_[(w * kTQ + j) * 64 + lane]);
   }
 }
 
@@ -1396,20 +1488,18 @@ static void launch_c2i(const Geo& g, const XT* xT, const BinsWs& P, const GT* gc
 template <typename GT, typename XT>
 static void launch_k5_fused(const Geo& g, const XT* xT, const BinsWs& P, const GT* gcolT,
                             float* gxT, float* goff, int b0, int nb, hipStream_t s) {
-  // U = 2 rows in flight per wave for both element types: U = 4 for the half-length bf16
-  // rows measured slower (r02, config 4: 0.192 against 0.187 ms; 95 VGPRs, 5 waves/SIMD)
-  // bf16 rows stay raw (8 B per lane) until consumed, so 3 rows in flight fit the 6-waves-per-
-  // SIMD budget (80 VGPRs): config 4 0.189 (U = 2, converted at load) -> 0.162 (U = 2 raw) ->
-  // 0.154 ms (U = 3 raw); U = 4 spills at 6 waves and runs 0.178 at 5. fp32 rows (16 B per lane) with U = 3 spill 32 B at 6 waves: 0.67 -> 0.88 ms.
-  // Tile rows (kTR; kTR + 1 waves per workgroup): 4 -> 7 (r02) cuts the bin rows read twice
+  // U rows in flight per wave. r02 (per-batch conditional loads): bf16 rows kept raw (8 B
+  // per lane) until consumed: config 4 0.189 (U = 2, converted at load) -> 0.162 (U = 2 raw)
+  // -> 0.154 ms (U = 3 raw). Tile rows (kTR; kTR + 1 waves per workgroup): 4 -> 7 (r02) cuts the bin rows read twice
   // (a tile re-reads the bin row it shares with the tile below: 5/4 -> 8/7 of the ∂col rows)
   // at the same 24 waves per CU (3 workgroups of 8, 40 KB of window each). Config 3 fp32 /
   // config 4 bf16: kTR 4 0.667 / 0.152 ms, 5 0.651 / 0.163, 6 0.630 / 0.151, 7 0.568 / 0.129,
   // 8 (2 workgroups per CU) 0.658 / 0.167, 11 0.585 / 0.137.
-  if constexpr (sizeof(GT) == 2)
-    return launch_c2i<3, 4, 6, 7>(g, xT, P, gcolT, gxT, goff, b0, nb, s);
-  else
-    return launch_c2i<2, 4, 6, 7>(g, xT, P, gcolT, gxT, goff, b0, nb, s);
+  // r03 (segmented records, packed math; A/B at config 3 / config 4, col2im scope incl. the
+  // fold): fp32 U = 2 at 6 waves/SIMD spills 24 B: 0.669-0.673 ms; U = 2 at 5: 0.571;
+  // U = 3 at 5 (95 VGPRs): 0.564-0.568; U = 3 at 4: 0.565. bf16 U = 3 at 5: 0.123-0.124,
+  // U = 4 at 5: 0.123, U = 3 at 6 (spills): 0.146.
+  launch_c2i<3, 4, 5, 7>(g, xT, P, gcolT, gxT, goff, b0, nb, s);
 }
 
 hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, const float* off,

@@ -60,6 +60,8 @@ SIGNATURES = {
     "dcn_synchronize": [_vp],
     "dcn_malloc": [_vp, _sz, ctypes.POINTER(_vp)],
     "dcn_free": [_vp, _vp],
+    "dcn_host_alloc": [_vp, _sz, ctypes.POINTER(_vp)],
+    "dcn_host_free": [_vp],
     "dcn_memcpy_h2d": [_vp, _vp, _vp, _sz],
     "dcn_memcpy_d2h": [_vp, _vp, _vp, _sz],
     "dcn_memset_zero": [_vp, _vp, _sz],

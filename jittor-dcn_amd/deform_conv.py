@@ -96,6 +96,7 @@ def dcn_forward_numpy(x, w_off, b_off, w, b, stride, padding, handle=None, retur
     h = state.handle if state is not None else (handle or rt.default_handle())
     desc = rt.make_desc(B, C, H, W, O, (kh, kw), stride, padding, bias=b is not None)
     Ho, Wo = rt.out_shape(desc)
+    hostmem.use_pinned(h)  # page-locked result blocks: their downloads are DMAs
     out = hostmem.empty((B, O, Ho, Wo))
     off = hostmem.empty((B, w_off.shape[0], Ho, Wo))
     owner = state if state is not None else h
@@ -137,6 +138,7 @@ def dcn_backward_numpy(x, off, w_off, w, has_bias, grad_out, stride, padding, ha
         handle or (ctx.owner if ctx is not None else rt.default_handle()))
     owner = state if state is not None else h
     desc = rt.make_desc(B, C, H, W, O, (kh, kw), stride, padding, bias=has_bias)
+    hostmem.use_pinned(h)
     g = {"x": hostmem.empty_like(x), "weight": hostmem.empty_like(w),
          "offset_conv.weight": hostmem.empty_like(w_off),
          "offset_conv.bias": np.empty(w_off.shape[0], np.float32)}

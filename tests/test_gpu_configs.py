@@ -110,7 +110,7 @@ def test_config3_full_batch_every_tensor_vs_c_oracle(gpu_handle):
     out, off, g = _device_fwd_bwd(gpu_handle, c)
     ro, roff, rg = _c_oracle_all(c, off)
     _check_all(out, off, g, ro, roff, rg, "config3")
-    # the host-pointer path on a module's state: auto image chunks (205 MB of x -> 9), the
+    # the host-pointer path on a module's state: auto image chunks (205 MB of x -> 4), the
     # transfers pipelined with the kernels, the backward reusing each chunk's columns
     from deform_conv import dcn_backward_numpy, dcn_forward_numpy
     st = rt.HostState(gpu_handle)

@@ -15,7 +15,5 @@ bash tools/prof_cfg.sh ${T}_c3 3 > gpurun_out/kstats_${T}_c3.txt && \
 bash tools/prof_cfg.sh ${T}_c4 4 > gpurun_out/kstats_${T}_c4.txt && \
 grep -iE "col2im|fold|bins|total" gpurun_out/kstats_${T}_c3.txt gpurun_out/kstats_${T}_c4.txt | head -30 && \
 echo "== host" && \
-timeout -k 10 300 python -u tools/host_rate.py --chunks ${CHUNKS:-1,4,8,12,16,0} --steps 4 && \
-timeout -k 10 300 python -u tools/host_rate.py --chunks 1,0 --stack 4 --steps 2
-echo "== bf16 K1 A/B" && \
-CONFIG=4 bash tools/ab_cfg.sh k1b 0 2 3 4 0 2 3
+timeout -k 10 300 python -u tools/host_rate.py --chunks ${CHUNKS:-1,4,0} --steps 4 && \
+timeout -k 10 300 python -u tools/host_rate.py --chunks 1,0 --stack 4 --steps 3
