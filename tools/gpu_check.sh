@@ -17,5 +17,5 @@ echo "== bench" && \
 timeout -k 10 420 python bench.py --steps $STEPS --warmup 3 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err && \
 cat gpurun_out/bench_$TAG.json && \
 echo "== rocprofv3" && \
-timeout -k 10 420 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-strong > gpurun_out/prof_$TAG.log 2>&1 && \
+timeout -k 10 420 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-strong --no-host-path > gpurun_out/prof_$TAG.log 2>&1 && \
 echo "done"

@@ -20,6 +20,6 @@ timeout -k 10 420 python -u -m pytest tests -m gpu -q -rf -x --timeout 120 --tim
 tail -15 gpurun_out/pytest_gpu_r03b.log
 [ $rc -eq 0 ] || { echo "pytest rc=$rc"; exit $rc; }
 echo "== rocprofv3" && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r03b -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-strong > gpurun_out/prof_r03b.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof4_r03b -o run --output-format csv -- python3 bench.py --config 4 --steps 5 --warmup 2 --no-cpu-baseline --no-strong > gpurun_out/prof4_r03b.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r03b -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-strong --no-host-path > gpurun_out/prof_r03b.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof4_r03b -o run --output-format csv -- python3 bench.py --config 4 --steps 5 --warmup 2 --no-cpu-baseline --no-strong --no-host-path > gpurun_out/prof4_r03b.log 2>&1 && \
 echo done
