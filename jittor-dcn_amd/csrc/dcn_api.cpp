@@ -1177,8 +1177,9 @@ int d2h(dcn_handle* h, hipStream_t s, void* dst, const void* src, size_t bytes) 
 // kernels, instead of transfers + kernels. Each chunk has its own workspace slice, which
 // keeps that chunk's columns from the forward for the backward.
 constexpr int kMaxHostChunks = 16;
-// auto: about this much x per chunk. r03, config 3 (205 MB of x), fwd + bwd incl. PCIe:
-// 1 chunk 23.4 ms, 2 17.2, 4 17.0, 8 18.1, 9 (24 MB) 17.9
+// auto: about this much x per chunk. r03, config 3 (205 MB of x), fwd + bwd incl. PCIe,
+// equal chunks: 1 chunk 23.4 ms, 2 17.2, 4 17.0, 8 18.1, 9 (24 MB) 17.9; half-size first
+// and last chunks (make_plan): 3 16.5, 4 15.9, 5 16.4, 6 17.2
 constexpr size_t kHostChunkBytes = size_t(52) << 20;
 
 struct ChunkPlan {
@@ -1200,19 +1201,29 @@ int chunk_count(const dcn_host_state* s, const Geo& g) {
   return std::max(1, std::min(std::min(n, kMaxHostChunks), g.B));
 }
 
+// Chunk i spans images [b0[i], b0[i+1]). With 3 or more chunks the first and the last are
+// half the size of the others: nothing overlaps the first chunk's upload or the last one's
+// kernels and download, so those two are kept short.
 int make_plan(const dcn_desc* d, const Geo& g, int n, ChunkPlan* P) {
   P->n = n;
+  const long W2 = n >= 3 ? 2L * n - 2 : 2L * n;  // total weight in half units
+  auto start = [&](int i) -> int {  // cumulative weight of chunks < i, in half units
+    const long h = n >= 3 ? (i == 0 ? 0 : 2L * i - 1) : 2L * i;
+    return (int)((long)g.B * std::min(h, W2) / W2);
+  };
+  for (int i = 0; i <= n; ++i) P->b0[i] = start(i);
+  for (int i = 1; i <= n; ++i)  // every chunk at least one image (n <= B)
+    P->b0[i] = std::max(P->b0[i], P->b0[i - 1] + 1);
+  for (int i = n - 1; i >= 0; --i) P->b0[i] = std::min(P->b0[i], P->b0[i + 1] - 1);
   size_t off = 0;
   for (int i = 0; i < n; ++i) {
-    P->b0[i] = (int)((long)g.B * i / n);
     P->d[i] = *d;
-    P->d[i].B = (int)((long)g.B * (i + 1) / n) - P->b0[i];
+    P->d[i].B = P->b0[i + 1] - P->b0[i];
     Geo gi;
     DCN_TRY(make_geo(&P->d[i], &gi));
     P->ws_off[i] = off;
     off += (ws_layout(gi, true).total + 255) & ~size_t(255);
   }
-  P->b0[n] = g.B;
   P->ws_off[n] = off;
   return DCN_OK;
 }
