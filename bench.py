@@ -580,8 +580,10 @@ def main():
 
 def host_path_rate(cfg, config, steps=4):
     """The reference caller's path through the drop-in: DeformConv2d fwd + bwd on host (NumPy)
-    arrays, i.e. dcn_forward_host + dcn_backward_host_ex (persistent device copies, pinned
-    staging, the backward reusing its forward's columns). PCIe-inclusive, so never `value`."""
+    arrays on a module's host state (dcn_forward_host_s + dcn_backward_host_s: persistent
+    device copies, the image-chunk transfer pipeline, the backward reusing its forward's
+    columns), one module and (fwd + bwd configs with C == O and stride 1) a stack of four
+    (train.py:304-318: all forwards, then all backwards). PCIe-inclusive, never `value`."""
     from deform_conv import dcn_backward_numpy, dcn_forward_numpy
     import dcn_runtime as rt
 
@@ -614,6 +616,29 @@ def host_path_rate(cfg, config, steps=4):
         step()
     el = (time.perf_counter() - t0) / steps
     st.close()
+    stack = None
+    if not fwd_only and C == O_ and s == 1 and (Ho, Wo) == (H, W):
+        sts = [rt.HostState(h) for _ in range(4)]
+
+        def stack_step():
+            xi, ctxs = x, []
+            for sti in sts:
+                o, f, c = dcn_forward_numpy(xi, wo, bo, w, b, (s, s), (p, p), state=sti,
+                                            return_ctx=True)
+                ctxs.append((xi, f, c))
+                xi = o
+            g = gout
+            for xi, f, c in reversed(ctxs):
+                g = dcn_backward_numpy(xi, f, wo, w, True, g, (s, s), (p, p), ctx=c,
+                                       offset_grad=False)["x"]
+
+        stack_step()
+        t0 = time.perf_counter()
+        for _ in range(2):
+            stack_step()
+        stack = round((time.perf_counter() - t0) / 2 / 4 * 1e3, 3)
+        for sti in sts:
+            sti.close()
     h.close()
     moved = (x.nbytes + gout.nbytes * (0 if fwd_only else 1) + B * O_ * Ho * Wo * 4
              + B * 2 * N * Ho * Wo * 4 + (0 if fwd_only else x.nbytes))
@@ -624,6 +649,7 @@ def host_path_rate(cfg, config, steps=4):
             "config": f"config{config}", "steps": steps, "ms_per_step": round(el * 1e3, 3),
             "value": round(B * Ho * Wo * N / el / 1e9, 5), "unit": "Gsamples/s",
             "pcie_bytes_per_step": int(moved),
+            "stack4_ms_per_module": stack,
             "transfers": "direct from / to the arrays (recycled resident outputs, hostmem.py)"
                          if os.environ.get("DCN_HOST_STAGING", "0") == "0" else
                          "pinned staging ring (DCN_HOST_STAGING=1)"}
