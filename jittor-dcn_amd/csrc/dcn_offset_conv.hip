@@ -488,7 +488,10 @@ __device__ __forceinline__ void stage_goff(const Geo& g, const float* __restrict
   // quotient there (checked for every d <= 8192, idx < 65536), instead of ~40-instruction
   // integer divides per element
   const unsigned mp = 0xffffffffu / (unsigned)plane + 1u, ms = 0xffffffffu / (unsigned)SW + 1u;
-  const float* gb = goff + (size_t)b * g.J * g.HW;
+  // buffer loads: a position outside the image reads 0 through the range check (no select
+  // after the load, which ties each load's wait to its own condition register)
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(goff + (size_t)b * g.J * g.HW),
+                                                    0, (int)((size_t)g.J * g.HW * 4), 0x00020000);
   for (int i0 = threadIdx.x; i0 < n; i0 += blockDim.x * kU) {
     float v[kU];
     int dst[kU];
@@ -499,14 +502,16 @@ __device__ __forceinline__ void stage_goff(const Geo& g, const float* __restrict
       const int sr = (int)__umulhi((unsigned)rem, ms), sc = rem - sr * SW;
       const int ho = y0 + sr - (g.kh - 1) * g.dh + g.ph, wo = sc - (g.kw - 1) * g.dw + g.pw;
       const bool ok = ho >= 0 && ho < g.Ho && wo >= 0 && wo < g.Wo;
-      const int hc = min(max(ho, 0), g.Ho - 1), wc = min(max(wo, 0), g.Wo - 1);
-      v[u] = gb[(size_t)j * g.HW + hc * g.Wo + wc];
-      v[u] = ok ? v[u] : 0.f;
+      const unsigned o = ok ? (unsigned)((j * g.HW + ho * g.Wo + wo) * 4) : 0x80000000u;
+      v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o, 0, 0));
       dst[u] = rem * g.J + j;
     }
+    // unconditional: a slot past n holds element n-1 (clamped idx) and rewrites it with its
+    // own value, so no exec-masked store blocks (each makes the waitcnt pass drain, vmcnt(0));
+    // the barrier keeps all kU loads issued before the first store
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int u = 0; u < kU; ++u)
-      if (i0 + u * (int)blockDim.x < n) S[dst[u]] = v[u];
+    for (int u = 0; u < kU; ++u) S[dst[u]] = v[u];
   }
 }
 
@@ -738,6 +743,11 @@ __global__ __launch_bounds__(256) void offset_wgrad_mfma_m1(Geo g, const float* 
         va[1] = fmaf(a, vb[1], va[1]);
         ring[d] = ld(min(lo, last));
         lo += step_x;
+        // keep the load here, kPf steps ahead of its use: left alone, the scheduler hoists
+        // the later steps' MFMAs above it, so the ring's loads issue at the end of the
+        // unrolled body, just before the next iteration's first use (a barrier that holds
+        // only the vector-memory instructions, mask 0x78F, still lets that happen)
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   }  // chunks
@@ -854,6 +864,8 @@ __global__ __launch_bounds__(256, 4) void offset_dgrad_mfma(Geo g, const float* 
       for (int u = 0; u < 4; ++u)
         mfma16x4_acc(acc[0][u], acc[1][u], acc[2][u], acc[3][u], a[0], a[1], a[2], a[3], bv[u]);
       lda(ks + kPf, ra[d]);
+      // the loads stay kPf steps ahead (offset_wgrad_mfma_m1 says why)
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 #pragma unroll
@@ -1207,25 +1219,28 @@ __device__ __forceinline__ void stage_goff8(const Geo& g, const float* __restric
   constexpr int kU = 8;
   const int plane = SR * SW, n = plane * J8;
   const unsigned mp = 0xffffffffu / (unsigned)plane + 1u, ms = 0xffffffffu / (unsigned)SW + 1u;
-  const float* gb = goff + (size_t)b * g.J * g.HW;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(goff + (size_t)b * g.J * g.HW),
+                                                    0, (int)((size_t)g.J * g.HW * 4), 0x00020000);
   for (int i0 = threadIdx.x; i0 < n; i0 += blockDim.x * kU) {
     float v[kU];
     int dst[kU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {  // sc fastest: coalesced reads
+    for (int u = 0; u < kU; ++u) {  // sc fastest: coalesced reads (stage_goff's buffer loads)
       const int idx = min(i0 + u * (int)blockDim.x, n - 1);
       const int j = (int)__umulhi((unsigned)idx, mp), rem = idx - j * plane;
       const int sr = (int)__umulhi((unsigned)rem, ms), sc = rem - sr * SW;
       const int ho = y0 + sr - (g.kh - 1) * g.dh + g.ph, wo = sc - (g.kw - 1) * g.dw + g.pw;
       const bool ok = j < g.J && ho >= 0 && ho < g.Ho && wo >= 0 && wo < g.Wo;
-      const int hc = min(max(ho, 0), g.Ho - 1), wc = min(max(wo, 0), g.Wo - 1);
-      v[u] = gb[(size_t)min(j, g.J - 1) * g.HW + hc * g.Wo + wc];
-      v[u] = ok ? v[u] : 0.f;
+      const unsigned o = ok ? (unsigned)((j * g.HW + ho * g.Wo + wo) * 4) : 0x80000000u;
+      v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o, 0, 0));
       dst[u] = rem * PJ + j;
     }
+    // unconditional: a slot past n holds element n-1 (clamped idx) and rewrites it with its
+    // own value, so no exec-masked store blocks (each makes the waitcnt pass drain, vmcnt(0));
+    // the barrier keeps all kU loads issued before the first store
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int u = 0; u < kU; ++u)
-      if (i0 + u * (int)blockDim.x < n) S[dst[u]] = v[u];
+    for (int u = 0; u < kU; ++u) S[dst[u]] = v[u];
   }
 }
 
@@ -1666,6 +1681,7 @@ __global__ __launch_bounds__(256) void offset_bwd_generic(Geo g, const float* __
 // writes them to xT, so no separate transpose pass reads x again. Every sum has a fixed
 // order: deterministic.
 // ---------------------------------------------------------------------------
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kXtCP = 20, kXtRWmax = 64, kXtWts = 9 * 64 * 4 + 9 * 4 * 8;  // floats
 
 // per 16-channel chunk cg, kXtWts floats: B[t][lane][s] = w_off[j = lane&15][c][t] with
@@ -1701,7 +1717,11 @@ offset_conv_fwd_mfma_xt(Geo g, const float* __restrict__ x, const float* __restr
   constexpr int WIN = NR * RW * CP;         // floats per window buffer
   constexpr int BUF = WIN + kXtWts;
   constexpr int kSx = (16 * NR * 16 + NT - 1) / NT, kSw = (kXtWts / 4 + NT - 1) / NT;
-  __shared__ __attribute__((aligned(16))) float lds[2 * BUF];
+  // 2 buffers, then a trash slot per lane: staging slots with nothing to stage write there,
+  // so the LDS stores need no exec-masked branch (a masked block makes the waitcnt pass
+  // assume its waits may not have run and drain the chunks in flight, vmcnt(0), every step)
+  constexpr int TRASH = 2 * BUF;
+  __shared__ __attribute__((aligned(16))) float lds[2 * BUF + 256];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const Block3 blk = xcd_block();
@@ -1726,7 +1746,7 @@ offset_conv_fwd_mfma_xt(Geo g, const float* __restrict__ x, const float* __restr
     const int y = ho0 - 1 + row;
     const bool in = row < NR;
     gx[u] = in && y >= 0 && y < H ? (cc * H + y) * W + 4 * q : -1;
-    lx[u] = in ? (row * RW + 1 + 4 * q) * CP + cc : -1;
+    lx[u] = in ? (row * RW + 1 + 4 * q) * CP + cc : TRASH - BUF + lane;  // (relative to L)
   }
   // branch-free loads (buffer range checks give the zeros), so no conditional load makes the
   // compiler drain the prefetch early
@@ -1734,6 +1754,8 @@ offset_conv_fwd_mfma_xt(Geo g, const float* __restrict__ x, const float* __restr
                                                     0, (int)((size_t)C * H * W * 4), 0x00020000);
   const auto rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wf), 0,
                                                     (int)((size_t)(C / 16) * kXtWts * 4), 0x00020000);
+  const auto rxt = __builtin_amdgcn_make_buffer_rsrc(xT + (size_t)b * C * H * W, 0,
+                                                     (int)((size_t)C * H * W * 4), 0x00020000);
   auto load_chunk = [&](int k, float4(&sx)[kSx], float4(&sw)[kSw]) __attribute__((always_inline)) {
     k = min(k, nch - 1);  // past the end: a harmless re-load (no conditional loads)
 #pragma unroll
@@ -1755,20 +1777,20 @@ offset_conv_fwd_mfma_xt(Geo g, const float* __restrict__ x, const float* __restr
   auto store_chunk = [&](int bf, const float4(&sx)[kSx], const float4(&sw)[kSw])
                          __attribute__((always_inline)) {
     float* L = lds + bf * BUF;
+    const int tr = (1 - bf) * BUF;  // lx's trash slots are relative to buffer 1
 #pragma unroll
     for (int u = 0; u < kSx; ++u) {
-      if (lx[u] >= 0) {
-        float* d = L + lx[u];
-        d[0] = sx[u].x;
-        d[CP] = sx[u].y;
-        d[2 * CP] = sx[u].z;
-        d[3 * CP] = sx[u].w;
-      }
+      float* d = L + lx[u] + (lx[u] >= TRASH - BUF ? tr : 0);
+      d[0] = sx[u].x;
+      d[CP] = sx[u].y;
+      d[2 * CP] = sx[u].z;
+      d[3 * CP] = sx[u].w;
     }
 #pragma unroll
     for (int u = 0; u < kSw; ++u) {
       const int idx = tid + NT * u;
-      if (idx < kXtWts / 4) reinterpret_cast<float4*>(L + WIN)[idx] = sw[u];
+      float* d = idx < kXtWts / 4 ? L + WIN + 4 * idx : lds + TRASH + 4 * (lane & 31);
+      *reinterpret_cast<float4*>(d) = sw[u];
     }
   };
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1783,21 +1805,26 @@ offset_conv_fwd_mfma_xt(Geo g, const float* __restrict__ x, const float* __restr
   auto step = [&](int k, float4(&sxn)[kSx], float4(&swn)[kSw]) __attribute__((always_inline)) {
     // LDS buffer k&1 holds chunk k; (sxn, swn) chunk k+1; the other set chunk k+2 (in flight)
     const int bf = k & 1;
+    const bool live = k < nch;  // the pair's second step past an odd chunk count: staging only
     const float* L = lds + bf * BUF;
     {  // input rows ho0.. (window rows 1..ROWS), this chunk's 16 channels -> xT
       const int part = tid & 3;
       constexpr int kXs = (ROWS * RW + NT / 4 - 1) / (NT / 4);  // fixed trip count: the
 #pragma unroll                                                // waitcnt pass keeps counting
       for (int u = 0; u < kXs; ++u) {
+        // branch-free: slots past the block read LDS word 0 and store out of range (dropped)
         const int i = (tid >> 2) + u * (NT / 4);
         const int r = i / W, px = i - r * W, y = ho0 + r;
-        if (i < ROWS * W && y < H)
-          *reinterpret_cast<float4*>(xT + ((size_t)(b * H + y) * W + px) * C + k * 16 + 4 * part) =
-              *reinterpret_cast<const float4*>(L + ((1 + r) * RW + 1 + px) * CP + 4 * part);
+        const bool ok = live && i < ROWS * W && y < H;
+        const float4 v = *reinterpret_cast<const float4*>(
+            L + (ok ? ((1 + r) * RW + 1 + px) * CP + 4 * part : 0));
+        const unsigned o = ok ? (unsigned)(((y * W + px) * C + k * 16 + 4 * part) * 4) : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4{v.x, v.y, v.z, v.w}),
+                                               rxt, o, 0, 0);
       }
     }
     const float* LB = L + WIN;
-    if (has_tile) {
+    if (has_tile && live) {
 #pragma unroll 1
       for (int ty = 0; ty < 3; ++ty)
 #pragma unroll
@@ -1822,7 +1849,8 @@ offset_conv_fwd_mfma_xt(Geo g, const float* __restrict__ x, const float* __restr
         e1 = fmaf(a.w, v1.w, e1);
       }
     }
-    if (k + 1 < nch) store_chunk(bf ^ 1, sxn, swn);
+    // unconditional: past the last chunk it stages a re-loaded chunk nobody reads
+    store_chunk(bf ^ 1, sxn, swn);
     load_chunk(k + 3, sxn, swn);
     lds_barrier();
   };
@@ -1831,9 +1859,12 @@ offset_conv_fwd_mfma_xt(Geo g, const float* __restrict__ x, const float* __restr
   store_chunk(0, sx0, sw0);
   load_chunk(2, sx0, sw0);
   lds_barrier();
+  // both steps of a pair always run: a conditional second step is a path on which the
+  // waitcnt pass sees the other register set's loads missing, and it then waits for them
+  // (vmcnt 4..1 instead of 9..6) in every first step
   for (int k = 0; k < nch; k += 2) {
     step(k, sx1, sw1);
-    if (k + 1 < nch) step(k + 1, sx0, sw0);
+    step(k + 1, sx0, sw0);
   }
   // through LDS as [row][j][64 pixels], then runs of consecutive pixels per offset channel
   float* T = lds;  // the buffers are free: the last barrier followed the last reads
@@ -1870,7 +1901,8 @@ offset_conv_fwd_mfma_xt(Geo g, const float* __restrict__ x, const float* __restr
 bool offset_fwd_mfma_xt_ok(const Geo& g) {
   return g.dt == DCN_F32 && g.kh == 3 && g.kw == 3 && g.sh == 1 && g.sw == 1 && g.dh == 1 &&
          g.dw == 1 && g.ph == 1 && g.pw == 1 && g.Ho == g.H && g.Wo == g.W &&
-         g.W + 2 <= kXtRWmax && g.W % 4 == 0 && g.C % 16 == 0 && g.J >= 1 && g.J <= 18;
+         g.W + 2 <= kXtRWmax && g.W % 4 == 0 && g.C % 16 == 0 && g.J >= 1 && g.J <= 18 &&
+         (size_t)g.C * g.H * g.W * 4 < (1u << 31);  // one image of x / xT per buffer range
 }
 
 // off and xT (channels-last x) from x in one pass; wf: offset_conv_wt_floats(g) scratch
