@@ -240,7 +240,7 @@ def main():
     ap.add_argument("--alt-math", type=int, default=6, choices=(0, 3, 6, 9),
                     help="also time this GEMM arithmetic after the headline run (N=1, fp32 "
                          "configs; 0 = skip) and report it under 'alt'")
-    ap.add_argument("--fwd-path", type=int, default=0, choices=(0, 1, 2),
+    ap.add_argument("--fwd-path", type=int, default=0, choices=(0, 1, 2, 3),
                     help="forward schedule (include/dcn.h dcn_fwd_path): 0 auto, 1 K1 + vendor "
                          "GEMM + bias, 2 fused im2col+GEMM where it applies")
     ap.add_argument("--graph", type=int, default=0, choices=(0, 1),

@@ -323,14 +323,29 @@ int dcn_set_math(dcn_handle* h, int math);
 int dcn_get_math(dcn_handle* h, int* math);
 
 /* ---- forward schedule ----------------------------------------------------------- */
-/* How the fp32 forward (deform_conv.py:41-80) runs after the offset conv.
- * DCN_FWD_FUSED: the fused kernel (bilinear im2col gathered straight into the f32 MFMA
- * GEMM's LDS tiles, bias in the epilogue; the columns are still written for the backward)
- * wherever it applies: DCN_F32, deform_groups 1, kh*kw <= 9, C % 32 == 0, O % 128 == 0,
- * native math; otherwise (and for DCN_BF16) the unfused schedule. DCN_FWD_UNFUSED: K1 im2col, then the
+/* How the forward (deform_conv.py:41-80) runs after the offset conv.
+ * DCN_BF16 (dcn_fused_bf16.hip): DCN_FWD_FUSED gathers the bilinear samples from an LDS
+ * window of the channels-last x straight into the B operand of bf16 MFMAs (bias and the
+ * bf16 rounding in the epilogue) and still writes the columns for a DCN_BWD_COL_IN_WS
+ * backward; DCN_FWD_FUSED_NOCOL never writes a column (forward-only callers: no_grad /
+ * inference, deform_conv.py:56 under jt.no_grad); a DCN_BWD_COL_IN_WS backward on the
+ * workspace of such a forward recomputes the columns. Both need C % 64 == 0, O % 256 == 0,
+ * deform_groups 1, kh*kw <= 9; elsewhere they take the unfused schedule. Same columns bit
+ * for bit as K1; out to fp32 rounding of a different summation order before the bf16
+ * rounding.
+ * DCN_F32: DCN_FWD_FUSED (and _NOCOL, which for fp32 still writes the columns) runs the
+ * fused kernel (bilinear im2col gathered straight into the f32 MFMA GEMM's LDS tiles, bias
+ * in the epilogue; the columns are still written for the backward) wherever it applies:
+ * deform_groups 1, kh*kw <= 9, C % 32 == 0, O % 128 == 0, native math; otherwise the
+ * unfused schedule. DCN_FWD_UNFUSED: K1 im2col, then the
  * vendor GEMM, then the bias. DCN_FWD_AUTO (default): the schedule measured faster for the
  * geometry. Same results to fp32 rounding (the columns bit for bit). */
-typedef enum { DCN_FWD_AUTO = 0, DCN_FWD_UNFUSED = 1, DCN_FWD_FUSED = 2 } dcn_fwd_path;
+typedef enum {
+  DCN_FWD_AUTO = 0,
+  DCN_FWD_UNFUSED = 1,
+  DCN_FWD_FUSED = 2,
+  DCN_FWD_FUSED_NOCOL = 3
+} dcn_fwd_path;
 int dcn_set_fwd_path(dcn_handle* h, int path);
 
 /* ---- development A/B knobs ------------------------------------------------------ *

@@ -116,6 +116,7 @@ struct WsLayout {
   // (DCN_BF16 keeps its channels-last x in `xT` as bf16; xT32 is the fp32 one that only the
   // VALU offset-conv fallbacks read, wb16 the bf16 weights of the MFMA offset conv)
   size_t x32 = 0, xT32 = 0, wb16 = 0, woff32 = 0, boff32 = 0, b32 = 0, off32 = 0, out32 = 0;
+  size_t wfr = 0;  // fused bf16 forward: Wf in MFMA lane order
   size_t gx32 = 0, gw32 = 0, gb32 = 0, gwo32 = 0, gbo32 = 0, goff32 = 0;
   size_t total = 0;
 };
@@ -151,6 +152,8 @@ WsLayout ws_layout(const Geo& g, bool bwd) {
     L.b32 = take((size_t)g.O * f);
     L.off32 = take((size_t)g.B * g.J * g.HW * f);
     L.out32 = take((size_t)g.B * g.O * g.HW * f);
+    L.wfr = take(dcn::fused_fwd_bf16_ok(g) ? dcn::fused_fwd_bf16_wfr_elems(g) * sizeof(dcn::bf16_t)
+                                           : 0);
   }
   if (bwd) {
     // ∂W partials; first also the ∂b tile sums of the fused ∂out transpose
@@ -187,6 +190,9 @@ struct dcn_handle {
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   dcn::GemmEngine* gemm = nullptr;
   int fwd_path = DCN_FWD_AUTO;  // dcn_set_fwd_path
+  // workspace of the last DCN_BF16 forward that left no columns in it (DCN_FWD_FUSED_NOCOL):
+  // a DCN_BWD_COL_IN_WS backward on it recomputes them instead of reading stale ones
+  const void* nocol_ws = nullptr;
   // data-parallel gradient exchange (dcn_set_comm / dcn_set_grad_stream): the ∂W/∂b
   // all-reduce runs on comm_stream as soon as they are final (dw_main / dw_aux), beside the
   // rest of the backward; the stream waits for comm_done before anything later
@@ -358,7 +364,7 @@ int core_forward(dcn_handle* h, const Geo& g, const float* x, const float* off, 
     HIP_TRY(dcn::launch_nchw_to_nhwc(x, xT, g.B, g.C, g.HWi, h->stream));
   }
   const bool want_fused =
-      h->fwd_path == DCN_FWD_FUSED || (h->fwd_path == DCN_FWD_AUTO && dcn::fused_fwd_pays(g));
+      h->fwd_path == DCN_FWD_FUSED || h->fwd_path == DCN_FWD_FUSED_NOCOL || (h->fwd_path == DCN_FWD_AUTO && dcn::fused_fwd_pays(g));
   if (want_fused && dcn::fused_fwd_ok(g) && !use_split(h, g) && !dcn::get_force_generic()) {
     // f2: im2col gathered into the GEMM's LDS tiles, bias in the epilogue; the columns are
     // still written for the ∂W GEMM of the backward (DCN_BWD_COL_IN_WS)
@@ -554,6 +560,20 @@ int forward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x,
                                           F32(L.part), st));
       HIP_TRY(dcn::launch_round_to_bf16(off32, off, (size_t)g.B * g.J * g.HW, st));
     }
+  }
+  const bool fused_ok = dcn::fused_fwd_bf16_ok(g) && !dcn::get_force_generic();
+  const bool nocol = fused_ok && h->fwd_path == DCN_FWD_FUSED_NOCOL;
+  h->nocol_ws = nocol ? base : (h->nocol_ws == base ? nullptr : h->nocol_ws);
+  if (fused_ok && (h->fwd_path == DCN_FWD_FUSED || nocol ||
+                   (h->fwd_path == DCN_FWD_AUTO && dcn::fused_fwd_bf16_pays(g)))) {
+    // f2: the bilinear gather feeds the bf16 MFMAs straight from an LDS window of xT; bias
+    // and the bf16 rounding in the epilogue; the columns are written only for a backward
+    // that reuses them (not for DCN_FWD_FUSED_NOCOL)
+    ProfScope ps(h, DCN_K_GEMM_FWD);
+    HIP_TRY(dcn::launch_fused_fwd_bf16(g, xT, off32, w, BF(L.wfr),
+                                       has_bias ? F32(L.b32) : nullptr, out,
+                                       nocol ? nullptr : BF(L.col), st));
+    return DCN_OK;
   }
   {
     ProfScope ps(h, DCN_K_IM2COL);
@@ -1017,9 +1037,11 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
     using dcn::bf16_t;
     auto C = [](const float* p) { return reinterpret_cast<const bf16_t*>(p); };
     auto M = [](float* p) { return reinterpret_cast<bf16_t*>(p); };
+    // a DCN_FWD_FUSED_NOCOL forward left no columns in this workspace: recompute them
+    const bool col_valid = (flags & DCN_BWD_COL_IN_WS) != 0 && h->nocol_ws != ws;
     return backward_bf16(h, g, d->has_bias != 0, C(x), C(off), C(w_off), C(w), C(grad_out),
                          M(grad_x), M(grad_w), M(grad_b), M(grad_w_off), M(grad_b_off),
-                         M(grad_off_out), base, L, (flags & DCN_BWD_COL_IN_WS) != 0);
+                         M(grad_off_out), base, L, col_valid);
   }
   auto F = [&](size_t o) { return reinterpret_cast<float*>(base + o); };
   float* goff = grad_off_out ? grad_off_out : F(L.goff);
@@ -1693,7 +1715,8 @@ int dcn_set_grad_stream(dcn_handle* h, void* s) {
 
 int dcn_set_fwd_path(dcn_handle* h, int path) {
   if (!h) return fail(DCN_ERR_INVALID, "dcn_set_fwd_path: null handle");
-  if (path != DCN_FWD_AUTO && path != DCN_FWD_UNFUSED && path != DCN_FWD_FUSED)
+  if (path != DCN_FWD_AUTO && path != DCN_FWD_UNFUSED && path != DCN_FWD_FUSED &&
+      path != DCN_FWD_FUSED_NOCOL)
     return fail(DCN_ERR_INVALID, "dcn_set_fwd_path: unknown path " + std::to_string(path));
   h->fwd_path = path;
   return DCN_OK;

@@ -1,0 +1,358 @@
+// dcn_fused_bf16.hip — f2 for DCN_BF16: the deformable im2col gathered straight into the B
+// operand of bf16 MFMAs (out = Wf · colᵀ + bias, deform_conv.py:41-80), so the forward never
+// reads a column matrix back from HBM; the columns are written only when the caller keeps
+// them for the ∂W GEMM of the backward (colT != NULL).
+//
+// Workgroup = one output tile of kTH × kTW pixels (7 × 16 = 112 slots = 7 MFMA column blocks
+// of 16) × 256 output channels; 4 waves, wave w owns output channels 64w..64w+63 (4 row
+// blocks of 16) over all 112 slots: 28 accumulators of v_mfma_f32_16x16x32_bf16.
+//
+//   * Sample records (prologue): per slot and tap the reference coordinate chain
+//     (sample_tap: deform_conv.py:34-39,62-68, Q1-Q4), reduced to the four bilinear weights
+//     (the canonical products (1-fr)(1-fc), (1-fr)fc, fr(1-fc), fr·fc of bilerp()) and where
+//     the corners are: in the LDS window, in the overflow area, or nowhere (zero).
+//   * x window (per 64-channel slice): the tile's zero-offset footprint with a 2-pixel margin
+//     (rows follow w, columns follow h: Q1) of the channels-last bf16 xT, staged in LDS;
+//     pixels outside the image hold zeros (grid_sample zeros padding).
+//   * Overflow: samples whose corners leave the window have their 64-channel column slice
+//     built once per slice from global memory (issued with the window loads, one latency),
+//     up to kOvf per tile; beyond that a sample reads its corners from global memory in line.
+//   * k loop: k = n·C + c in the order (slice, tap, 32-channel half). Per step the block
+//     gathers the [112 slots][32 channels] B tile into one of two LDS buffers (one 8-channel
+//     unit = 4 corner reads of 16 B, fp32 bilerp in bilerp()'s op order, one bf16 rounding:
+//     the bits of K1's columns) while the MFMAs consume the other; A fragments (the weights,
+//     pre-swizzled into MFMA lane order) come from L2 one step ahead. One barrier per step.
+//   * Epilogue: bf16(acc + bias[o]) straight to NCHW out (launch_bias_to_bf16's rounding).
+#include <climits>
+
+#include "dcn_device.h"
+
+namespace dcn {
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+constexpr int kTH = 7, kTW = 16;  // output tile rows (h) × columns (w)
+constexpr int kPB = kTH * kTW / 16;  // 16-slot MFMA column blocks
+constexpr int kSlots = kPB * 16;
+constexpr int kMar = 2;
+constexpr int kWR = kTW + 2 * kMar, kWQ = kTH + 2 * kMar;  // window rows (follow w), cols (h)
+constexpr int kWPix = kWR * kWQ;
+constexpr int kCS = 64;               // channels per window slice
+constexpr int kWPitch = 2 * kCS + 16;  // bytes per window pixel (16 B pad: bank spread)
+constexpr int kBPitch = 80;           // bytes per slot of a B tile (32 channels + 16 B pad)
+constexpr int kMaxN = 9;
+constexpr int kOvf = 48;              // overflow samples per tile with a precomputed slice
+constexpr int kUnits = kSlots * 4;    // 8-channel units per step (448)
+constexpr int kOT = 256;              // output channels per workgroup
+
+constexpr int kLdsWin = 0;
+constexpr int kLdsB = kLdsWin + kWPix * kWPitch;
+constexpr int kLdsRecW = kLdsB + 2 * kSlots * kBPitch;
+constexpr int kLdsRecM = kLdsRecW + kSlots * kMaxN * 16;
+constexpr int kLdsOvfT = kLdsRecM + kSlots * kMaxN * 4;
+constexpr int kLdsOvfD = kLdsOvfT + kOvf * 16;
+constexpr int kLdsCnt = kLdsOvfD + kOvf * 2 * kCS;
+constexpr int kLds = kLdsCnt + 16;
+static_assert(kLds <= 80 * 1024, "two workgroups per CU");
+
+constexpr int kMZero = -1;  // record meta: sample contributes 0 (or slot outside the output)
+// meta >= 0: window pixel of corner (r0, c0); meta = -2 - j: overflow entry j (j < kOvf) or,
+// for j >= kOvf, corners read from global memory in line
+
+// bilerp() with its weight products precomputed (same products, same op order); each
+// 32-bit word (2 channels) of the four corners is unpacked where it is used
+__device__ __forceinline__ unsigned blend2(float4 wv, unsigned a, unsigned b, unsigned c,
+                                           unsigned d) {
+  float lo = wv.x * __uint_as_float(a << 16), hi = wv.x * __uint_as_float(a & 0xffff0000u);
+  lo = fmaf(wv.y, __uint_as_float(b << 16), lo), hi = fmaf(wv.y, __uint_as_float(b & 0xffff0000u), hi);
+  lo = fmaf(wv.z, __uint_as_float(c << 16), lo), hi = fmaf(wv.z, __uint_as_float(c & 0xffff0000u), hi);
+  lo = fmaf(wv.w, __uint_as_float(d << 16), lo), hi = fmaf(wv.w, __uint_as_float(d & 0xffff0000u), hi);
+  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+}
+__device__ __forceinline__ uint4 blend8(float4 wv, uint4 ua, uint4 ub, uint4 uc, uint4 ud) {
+  return make_uint4(blend2(wv, ua.x, ub.x, uc.x, ud.x), blend2(wv, ua.y, ub.y, uc.y, ud.y),
+                    blend2(wv, ua.z, ub.z, uc.z, ud.z), blend2(wv, ua.w, ub.w, uc.w, ud.w));
+}
+
+__device__ __forceinline__ uint4 ld16_if(const bf16_t* p, bool ok) {
+  return ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0u, 0u, 0u, 0u);
+}
+
+// the 8 channels at c of sample (r0, c0) from global memory (corners outside the image: 0)
+__device__ __forceinline__ uint4 gather_global(const Geo& g, const bf16_t* __restrict__ xb, int r0,
+                                               int c0, int c, float4 wv) {
+  const bool r0ok = r0 >= 0, r1ok = r0 + 1 < g.H, c0ok = c0 >= 0, c1ok = c0 + 1 < g.W;
+  const long rs = (long)g.W * g.C;
+  const bf16_t* p00 = xb + ((long)r0 * g.W + c0) * (long)g.C + c;
+  const uint4 ua = ld16_if(p00, r0ok && c0ok);
+  const uint4 ub = ld16_if(p00 + g.C, r0ok && c1ok);
+  const uint4 uc = ld16_if(p00 + rs, r1ok && c0ok);
+  const uint4 ud = ld16_if(p00 + rs + g.C, r1ok && c1ok);
+  return blend8(wv, ua, ub, uc, ud);
+}
+
+__device__ __forceinline__ bf16x8_t as_frag(uint4 u) { return __builtin_bit_cast(bf16x8_t, u); }
+
+// wfr[ob][ks][lane][8] = Wf[16·ob + (lane & 15)][32·ks + 8·(lane >> 4) + e]: the A fragment of
+// v_mfma_f32_16x16x32_bf16 for output-channel block ob and k step ks, one 16-B load per lane
+__global__ __launch_bounds__(256) void wf_to_frag16(const bf16_t* __restrict__ w,
+                                                    bf16_t* __restrict__ wfr, int O, int K) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)O * K) return;
+  const int e = (int)(i & 7), l = (int)((i >> 3) & 63);
+  const long rest = i >> 9;
+  const int NKS = K / 32, ob = (int)(rest / NKS), ks = (int)(rest - (long)ob * NKS);
+  wfr[i] = w[(size_t)(16 * ob + (l & 15)) * K + 32 * ks + 8 * (l >> 4) + e];
+}
+
+template <bool STORE>
+__global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __restrict__ xT,
+                                                         const float* __restrict__ off,
+                                                         const bf16_t* __restrict__ wfr,
+                                                         const float* __restrict__ bias,
+                                                         bf16_t* __restrict__ out,
+                                                         bf16_t* __restrict__ colT, int tw_n) {
+  __shared__ __attribute__((aligned(16))) char lds[kLds];
+  char* const win = lds + kLdsWin;
+  char* const bt = lds + kLdsB;
+  float4* const recw = reinterpret_cast<float4*>(lds + kLdsRecW);
+  int* const recm = reinterpret_cast<int*>(lds + kLdsRecM);
+  int4* const ovft = reinterpret_cast<int4*>(lds + kLdsOvfT);
+  char* const ovfd = lds + kLdsOvfD;
+  int* const cnt = reinterpret_cast<int*>(lds + kLdsCnt);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const Block3 blk = xcd_block();
+  const int b = blk.y;
+  const int th_i = blk.x / tw_n, tw_i = blk.x - th_i * tw_n;
+  const int h0 = th_i * kTH, w0 = tw_i * kTW;
+  const int o0 = blk.z * kOT + 64 * wave;
+  const int rlo = (int)floorf((float)w0 * (float)(g.H - 1) / (float)(g.Wo - 1)) - kMar;
+  const int qlo = (int)floorf((float)h0 * (float)(g.W - 1) / (float)(g.Ho - 1)) - kMar;
+  const bf16_t* const xb = xT + (size_t)b * g.HWi * g.C;
+  const int N = g.N;
+
+  // ---- records ----
+  if (tid == 0) cnt[0] = 0;
+  __syncthreads();
+  for (int s = tid; s < kSlots * N; s += 256) {
+    const int p = s / N, n = s - p * N;
+    const int h = h0 + p / kTW, w = w0 + p % kTW;
+    int meta = kMZero;
+    float4 wv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (h < g.Ho && w < g.Wo) {
+      const Tap t = sample_tap(g, off, b, 0, n, h * g.Wo + w);
+      if (t.ok) {
+        const float gr = 1.0f - t.fr, gc = 1.0f - t.fc;
+        wv = make_float4(gr * gc, gr * t.fc, t.fr * gc, t.fr * t.fc);
+        const int rr = t.r0 - rlo, qq = t.c0 - qlo;
+        if (rr >= 0 && rr + 1 < kWR && qq >= 0 && qq + 1 < kWQ) {
+          meta = rr * kWQ + qq;
+        } else {
+          const int j = atomicAdd(cnt, 1);  // any order: each entry is computed on its own
+          meta = -2 - j;
+          if (j < kOvf) ovft[j] = make_int4(t.r0, t.c0, p * kMaxN + n, 0);
+        }
+      }
+    }
+    recm[p * kMaxN + n] = meta;
+    recw[p * kMaxN + n] = wv;
+  }
+  __syncthreads();
+  const int novf = min(cnt[0], kOvf);
+
+  // ---- per-thread production units: u = tid, tid + 256 (u < kUnits): slot u>>2, 8-ch group u&3
+  const int nu = (tid + 256 < kUnits) ? 2 : 1;
+  int uslot[2], ucg[2];
+  unsigned ucol[2];  // the slot's column row in image b (elements), or ~0u outside the output
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int u = min(tid + 256 * k, kUnits - 1);
+    uslot[k] = u >> 2;
+    ucg[k] = u & 3;
+    const int h = h0 + uslot[k] / kTW, w = w0 + uslot[k] % kTW;
+    ucol[k] = (h < g.Ho && w < g.Wo) ? (unsigned)(h * g.Wo + w) * (unsigned)g.K : ~0u;
+  }
+
+  f32x4 acc[4][kPB];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < kPB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int NKS = g.K / 32;
+  const int spq = 2 * N;  // steps per slice
+  const int nslices = g.C / kCS;
+  // A fragments of step s of slice cs: k = n·C + 64·cs + 32·half
+  auto load_a = [&](int cs, int s, uint4 (&a)[4]) {
+    const int ks = ((s >> 1) * g.C + kCS * cs + 32 * (s & 1)) >> 5;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      a[i] = *reinterpret_cast<const uint4*>(
+          wfr + ((size_t)(((o0 >> 4) + i) * NKS + ks) * 64 + lane) * 8);
+  };
+  // gather step s of slice cs into B buffer buf (and, with STORE, the column rows)
+  auto produce = [&](int cs, int s, int buf) {
+    const int n = s >> 1, hh = s & 1;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (k < nu) {
+        const int slot = uslot[k], cg = ucg[k];
+        const int meta = recm[slot * kMaxN + n];
+        uint4 o = make_uint4(0u, 0u, 0u, 0u);
+        if (meta >= 0) {
+          const float4 wv = recw[slot * kMaxN + n];
+          const char* wp = win + meta * kWPitch + hh * 64 + cg * 16;
+          const uint4 ua = *reinterpret_cast<const uint4*>(wp);
+          const uint4 ub = *reinterpret_cast<const uint4*>(wp + kWPitch);
+          const uint4 uc = *reinterpret_cast<const uint4*>(wp + kWQ * kWPitch);
+          const uint4 ud = *reinterpret_cast<const uint4*>(wp + (kWQ + 1) * kWPitch);
+          o = blend8(wv, ua, ub, uc, ud);
+        } else if (meta != kMZero) {
+          const int j = -2 - meta;
+          if (j < kOvf) {
+            o = *reinterpret_cast<const uint4*>(ovfd + j * 2 * kCS + hh * 64 + cg * 16);
+          } else {  // more overflow samples than the area holds: corners from global memory
+            const int h = h0 + slot / kTW, w = w0 + slot % kTW;
+            const Tap t = sample_tap(g, off, b, 0, n, h * g.Wo + w);
+            o = gather_global(g, xb, t.r0, t.c0, kCS * cs + 32 * hh + 8 * cg,
+                              recw[slot * kMaxN + n]);
+          }
+        }
+        *reinterpret_cast<uint4*>(bt + buf * kSlots * kBPitch + slot * kBPitch + cg * 16) = o;
+        if (STORE && ucol[k] != ~0u) {
+          unsigned* dst = reinterpret_cast<unsigned*>(
+              colT + (size_t)b * g.HW * g.K + ucol[k] + (n * g.C + kCS * cs + 32 * hh + 8 * cg));
+          __builtin_nontemporal_store(o.x, dst);
+          __builtin_nontemporal_store(o.y, dst + 1);
+          __builtin_nontemporal_store(o.z, dst + 2);
+          __builtin_nontemporal_store(o.w, dst + 3);
+        }
+      }
+    }
+  };
+  auto mfma_step = [&](int buf, const uint4 (&a)[4]) {
+    const char* bb = bt + buf * kSlots * kBPitch + (lane & 15) * kBPitch + (lane >> 4) * 16;
+#pragma unroll
+    for (int pb = 0; pb < kPB; ++pb) {
+      const bf16x8_t bv = as_frag(*reinterpret_cast<const uint4*>(bb + pb * 16 * kBPitch));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        acc[i][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a[i]), bv, acc[i][pb], 0, 0, 0);
+    }
+  };
+
+  uint4 aE[4], aO[4];
+  for (int cs = 0; cs < nslices; ++cs) {
+    __syncthreads();  // the previous slice's window, overflow and B tiles are consumed
+    {
+      // window slice: kWPix pixels × 8 parts of 16 B; overflow corners loaded alongside
+      constexpr int TOT = kWPix * 8, IT = (TOT + 255) / 256;
+      uint4 v[IT];
+#pragma unroll
+      for (int k = 0; k < IT; ++k) {
+        const int idx = tid + k * 256;
+        const int pix = idx >> 3, part = idx & 7;
+        const int rr = pix / kWQ, qq = pix - rr * kWQ;
+        const int r = rlo + rr, q = qlo + qq;
+        const bool ok = idx < TOT && r >= 0 && r < g.H && q >= 0 && q < g.W;
+        v[k] = ld16_if(xb + ((size_t)r * g.W + q) * g.C + kCS * cs + 8 * part, ok);
+      }
+      // overflow: novf entries × 8 units of 8 channels
+      uint4 ov[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int idx = tid + 256 * k;
+        ov[k] = make_uint4(0u, 0u, 0u, 0u);
+        if (idx < novf * 8) {
+          const int4 e = ovft[idx >> 3];
+          ov[k] = gather_global(g, xb, e.x, e.y, kCS * cs + 8 * (idx & 7), recw[e.z]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < IT; ++k) {
+        const int idx = tid + k * 256;
+        if (idx < TOT)
+          *reinterpret_cast<uint4*>(win + (idx >> 3) * kWPitch + (idx & 7) * 16) = v[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int idx = tid + 256 * k;
+        if (idx < novf * 8)
+          *reinterpret_cast<uint4*>(ovfd + (idx >> 3) * 2 * kCS + (idx & 7) * 16) = ov[k];
+      }
+    }
+    load_a(cs, 0, aE);
+    __syncthreads();
+    produce(cs, 0, 0);
+    __syncthreads();
+    for (int s = 0; s < spq; s += 2) {
+      load_a(cs, s + 1, aO);
+      produce(cs, s + 1, 1);
+      mfma_step(0, aE);
+      __syncthreads();
+      if (s + 2 < spq) {
+        load_a(cs, s + 2, aE);
+        produce(cs, s + 2, 0);
+      }
+      mfma_step(1, aO);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: out[b][o][h][w] = bf16(acc + bias[o]); C/D: col = lane & 15, row = 4(lane>>4)+r
+  const int wcol = w0 + (lane & 15);
+  if (wcol < g.Wo) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = o0 + 16 * i + 4 * (lane >> 4) + r;
+        const float bv = bias ? bias[o] : 0.f;
+        bf16_t* op = out + ((size_t)b * g.O + o) * g.HW + wcol;
+#pragma unroll
+        for (int pb = 0; pb < kPB; ++pb) {
+          const int h = h0 + pb;
+          if (h < g.Ho) op[(size_t)h * g.Wo] = f2bf(acc[i][pb][r] + bv);
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+bool fused_fwd_bf16_ok(const Geo& g) {
+  const long lim = 1l << 31;
+  return g.dt == DCN_BF16 && g.G == 1 && g.N <= kMaxN && g.C % kCS == 0 && g.O % kOT == 0 &&
+         g.Ho >= 2 && g.Wo >= 2 && (long)g.O * g.K < lim && (long)g.HW * g.K < (1l << 31);
+}
+
+// measured against K1 + hipBLASLt + bias at config 4
+bool fused_fwd_bf16_pays(const Geo& g) {
+  (void)g;
+  return false;
+}
+
+size_t fused_fwd_bf16_wfr_elems(const Geo& g) { return (size_t)g.O * g.K; }
+
+hipError_t launch_fused_fwd_bf16(const Geo& g, const bf16_t* xT, const float* off,
+                                 const bf16_t* w, bf16_t* wfr, const float* bias, bf16_t* out,
+                                 bf16_t* colT, hipStream_t s) {
+  if (!fused_fwd_bf16_ok(g)) return hipErrorInvalidValue;
+  const long nw = (long)g.O * g.K;
+  hipLaunchKernelGGL(wf_to_frag16, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, w, wfr,
+                     g.O, g.K);
+  const int th_n = (g.Ho + kTH - 1) / kTH, tw_n = (g.Wo + kTW - 1) / kTW;
+  const dim3 grid(th_n * tw_n, g.B, g.O / kOT);
+  if (colT)
+    hipLaunchKernelGGL(fwd_fused_bf16<true>, grid, dim3(256), 0, s, g, xT, off, wfr, bias, out,
+                       colT, tw_n);
+  else
+    hipLaunchKernelGGL(fwd_fused_bf16<false>, grid, dim3(256), 0, s, g, xT, off, wfr, bias, out,
+                       colT, tw_n);
+  return hipGetLastError();
+}
+
+}  // namespace dcn

@@ -68,6 +68,15 @@ bool fused_fwd_pays(const Geo& g);  // DCN_FWD_AUTO picks the fused kernel
 void set_fused_workgroups(int n);    // test hook (dcn_debug_fused_workgroups)
 hipError_t launch_fused_fwd(const Geo& g, const float* xT, const float* off, const float* Wf,
                             const float* bias, float* out, float* colT, hipStream_t s);
+// dcn_fused_bf16.hip (f2, DCN_BF16): im2col gathered from an LDS window of xT straight into
+// the B operand of bf16 MFMAs, out = bf16(Wf·colᵀ + bias) (NCHW); writes colT only when
+// colT != NULL. wfr: scratch of fused_fwd_bf16_wfr_elems(g) bf16 (weights in MFMA lane order).
+bool fused_fwd_bf16_ok(const Geo& g);
+bool fused_fwd_bf16_pays(const Geo& g);  // DCN_FWD_AUTO picks it
+size_t fused_fwd_bf16_wfr_elems(const Geo& g);
+hipError_t launch_fused_fwd_bf16(const Geo& g, const bf16_t* xT, const float* off,
+                                 const bf16_t* w, bf16_t* wfr, const float* bias, bf16_t* out,
+                                 bf16_t* colT, hipStream_t s);
 // dcn_offset_conv.hip:
 // wt / wt2: scratch of offset_conv_wt_floats(g) floats (transposed w_off copies).
 size_t offset_conv_wt_floats(const Geo& g);

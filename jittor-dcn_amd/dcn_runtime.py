@@ -19,7 +19,7 @@ ABI_VERSION = 4  # include/dcn.h DCN_ABI_VERSION
 HOST_REUSE_FWD = 2  # include/dcn.h DCN_HOST_REUSE_FWD
 DCN_F32, DCN_BF16 = 0, 1
 DCN_BWD_COL_IN_WS = 1
-DCN_FWD_AUTO, DCN_FWD_UNFUSED, DCN_FWD_FUSED = 0, 1, 2
+DCN_FWD_AUTO, DCN_FWD_UNFUSED, DCN_FWD_FUSED, DCN_FWD_FUSED_NOCOL = 0, 1, 2, 3
 DCN_MATH_F32, DCN_MATH_F32_BF16X3, DCN_MATH_F32_BF16X6, DCN_MATH_F32_BF16X9 = 0, 3, 6, 9
 KERNEL_IDS = {
     "offset_fwd": 0, "im2col": 1, "gemm_fwd": 2, "bias_fwd": 3, "bwd_bias": 4,
@@ -259,7 +259,8 @@ class Handle:
         check(self.lib.dcn_set_math(self.h, int(math)), "dcn_set_math")
 
     def set_fwd_path(self, path: int):
-        """0 DCN_FWD_AUTO (measured-faster schedule), 1 DCN_FWD_UNFUSED, 2 DCN_FWD_FUSED."""
+        """0 DCN_FWD_AUTO (measured-faster schedule), 1 DCN_FWD_UNFUSED, 2 DCN_FWD_FUSED,
+        3 DCN_FWD_FUSED_NOCOL (DCN_BF16: no columns written)."""
         check(self.lib.dcn_set_fwd_path(self.h, int(path)), "dcn_set_fwd_path")
 
     # --- data-parallel gradient exchange (include/dcn.h) ---------------------------
