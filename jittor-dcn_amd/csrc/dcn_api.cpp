@@ -616,13 +616,19 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
   DCN_TRY(fork_aux(h));
   HIP_TRY(dcn::launch_bins(g, off32, base + L.bins, goff32, 0, g.B,
                            h->aux));
+  // f2 without a column matrix (DCN_FWD_FUSED_NOCOL): ∂W with the columns recomputed from
+  // xT inside the MFMA kernel, so the ∂columns are the only large buffer of the step
+  const bool dw_fused = !col_valid && h->fwd_path == DCN_FWD_FUSED_NOCOL &&
+                        dcn::fused_dw_bf16_ok(g) && !dcn::get_force_generic();
   if (!col_valid) {
     {
       ProfScope ps(h, DCN_K_XPOSE);
       HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(x, xT, g.B, g.C, g.HWi, st));
     }
-    ProfScope ps(h, DCN_K_IM2COL);
-    HIP_TRY(dcn::launch_im2col_bf16(g, xT, off32, col, 0, g.B, st));
+    if (!dw_fused) {
+      ProfScope ps(h, DCN_K_IM2COL);
+      HIP_TRY(dcn::launch_im2col_bf16(g, xT, off32, col, 0, g.B, st));
+    }
   }
   const bool exch = h->comm != nullptr;  // sum the fp32 copies over ranks, then round
   if (has_bias) {
@@ -630,13 +636,16 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
     dcn::launch_channel_sum_bf16(gout, g.B, g.O, g.HW, F32(L.gb32), st, exch ? nullptr : gb);
   }
   bf16_t* goutT = BF(L.goutT);
-  const int dwg = dw_groups(g);
+  const int dwg = dw_fused ? 0 : dw_groups(g);
   {
     ProfScope ps(h, DCN_K_GEMM_DW);
     dcn::GemmSpec sp;
     sp.bf16_ab = true;
     int nparts = g.B;
-    if (dwg > 0) {
+    if (dw_fused) {
+      HIP_TRY(dcn::launch_fused_dw_bf16(g, xT, off32, gout, F32(L.parts), st));
+      nparts = dcn::fused_dw_bf16_groups(g);
+    } else if (dwg > 0) {
       // grouped NT over the pixels of B/dwg images (∂outT first, shared with ∂col)
       HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(gout, goutT, g.B, g.O, g.HW, st));
       const int pg = (g.B / dwg) * g.HW;

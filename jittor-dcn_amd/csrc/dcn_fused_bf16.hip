@@ -23,6 +23,7 @@
 //     the bits of K1's columns) while the MFMAs consume the other; A fragments (the weights,
 //     pre-swizzled into MFMA lane order) come from L2 one step ahead. One barrier per step.
 //   * Epilogue: bf16(acc + bias[o]) straight to NCHW out (launch_bias_to_bf16's rounding).
+#include <algorithm>
 #include <climits>
 
 #include "dcn_device.h"
@@ -31,6 +32,7 @@ namespace dcn {
 namespace {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 constexpr int kTH = 7, kTW = 16;  // output tile rows (h) × columns (w)
 constexpr int kPB = kTH * kTW / 16;  // 16-slot MFMA column blocks
@@ -93,6 +95,18 @@ __device__ __forceinline__ uint4 gather_global(const Geo& g, const bf16_t* __res
 }
 
 __device__ __forceinline__ bf16x8_t as_frag(uint4 u) { return __builtin_bit_cast(bf16x8_t, u); }
+// native-vector forms for the ∂W kernel (HIP's uint4 arrays captured by lambdas can end up in
+// scratch memory)
+__device__ __forceinline__ bf16x8_t as_frag(v4u u) { return __builtin_bit_cast(bf16x8_t, u); }
+__device__ __forceinline__ v4u as_v(uint4 u) { return __builtin_bit_cast(v4u, u); }
+__device__ __forceinline__ uint4 as_u(v4u u) { return __builtin_bit_cast(uint4, u); }
+__device__ __forceinline__ v4u ld16v_if(const bf16_t* p, bool ok) {
+  return ok ? *reinterpret_cast<const v4u*>(p) : v4u{0u, 0u, 0u, 0u};
+}
+__device__ __forceinline__ v4u blend8(float4 wv, v4u ua, v4u ub, v4u uc, v4u ud) {
+  return v4u{blend2(wv, ua.x, ub.x, uc.x, ud.x), blend2(wv, ua.y, ub.y, uc.y, ud.y),
+             blend2(wv, ua.z, ub.z, uc.z, ud.z), blend2(wv, ua.w, ub.w, uc.w, ud.w)};
+}
 
 // wfr[ob][ks][lane][8] = Wf[16·ob + (lane & 15)][32·ks + 8·(lane >> 4) + e]: the A fragment of
 // v_mfma_f32_16x16x32_bf16 for output-channel block ob and k step ks, one 16-B load per lane
@@ -321,6 +335,292 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
   }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// ∂W with the columns recomputed (f2's backward half): ∂Wf[o][n·C + c] = Σ_p ∂out[o][p] ·
+// col[p][n·C + c] (the autodiff of deform_conv.py:76), the bilinear samples gathered from an
+// LDS window straight into the B operand, so no column matrix exists in HBM.
+//
+// Workgroup = (16-channel slice cs, image group, 256 output channels); 8 waves, wave w owns
+// output channels 32w..32w+31 (2 row blocks) × all taps of the slice (N column blocks of 16):
+// 2·N accumulators of v_mfma_f32_16x16x32_bf16. It walks the 7 × 16 pixel tiles of its
+// images in a fixed order (the reduction over pixels, 4 k steps of 32 slots per tile, slots
+// 112..127 zero); per tile it gathers the [N taps][16 channels][128 slots] column tile (2016
+// units of 8 channels, written transposed with 32-bit LDS stores, two pixels per store) while
+// the MFMAs consume the previous tile's; the next tile's window, offsets and ∂out fragments
+// are loaded into registers a tile ahead. One barrier per tile. The window margin is 4 px,
+// so a sample outside it (|Δ| > ~4 px) is rare and reads its corners from global memory.
+// Partials per (image group) are summed in a fixed order afterwards (launch_sum_partials).
+constexpr int kDC = 16;                       // channels per slice
+constexpr int kDMar = 4;
+constexpr int kDWR = kTW + 2 * kDMar, kDWQ = kTH + 2 * kDMar;
+constexpr int kDWPix = kDWR * kDWQ;           // 360
+constexpr int kDWPitch = 2 * kDC + 16;        // 48 B per window pixel
+constexpr int kDSl = 128;                     // pixel slots per tile, padded to 4 k steps
+constexpr int kDRow = kDSl * 2 + 16;          // bytes per [tap][channel] row of the col tile
+constexpr int kDT = 512;
+constexpr int kDOB = 2;
+constexpr int kDPairs = (kSlots / 2) * kMaxN * 2;  // (slot pair, tap, 8-channel group)
+constexpr int kDLWin = 0;
+constexpr int kDLCol = kDLWin + 2 * kDWPix * kDWPitch;
+constexpr int kDLRecW = kDLCol + 2 * kMaxN * kDC * kDRow;
+constexpr int kDLRecM = kDLRecW + 2 * kSlots * kMaxN * 16;
+constexpr int kDLds = kDLRecM + 2 * kSlots * kMaxN * 4;
+static_assert(kDLds <= 160 * 1024, "one workgroup per CU");
+constexpr int kDSlow = -2;  // record meta: corners outside the window (global reads)
+
+template <int NG>
+__global__ __launch_bounds__(kDT) void dw_fused_bf16(Geo g, const bf16_t* __restrict__ xT,
+                                                     const float* __restrict__ off,
+                                                     const bf16_t* __restrict__ gout,
+                                                     float* __restrict__ parts, int tw_n,
+                                                     int ngrp) {
+  extern __shared__ __attribute__((aligned(16))) char dl[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // XCD-aware order: the channel slices of one image group share an XCD, so its L2 serves
+  // them the group's ∂out fragments and x windows
+  const Block3 blk = xcd_block();
+  const int cs = blk.x, grp = blk.y;
+  const int o0 = blk.z * kOT + 16 * kDOB * wave;
+  const int N = g.N;
+  const int tiles_img = ((g.Ho + kTH - 1) / kTH) * tw_n;
+  const int b_lo = (int)((long)grp * g.B / ngrp), b_hi = (int)((long)(grp + 1) * g.B / ngrp);
+  const int T = (b_hi - b_lo) * tiles_img;
+
+  struct TileId {
+    int b, h0, w0, rlo, qlo;
+  };
+  auto tile_id = [&](int t) {
+    TileId q;
+    const int ti = t % tiles_img;
+    q.b = b_lo + t / tiles_img;
+    q.h0 = (ti / tw_n) * kTH;
+    q.w0 = (ti % tw_n) * kTW;
+    q.rlo = (int)floorf((float)q.w0 * (float)(g.H - 1) / (float)(g.Wo - 1)) - kDMar;
+    q.qlo = (int)floorf((float)q.h0 * (float)(g.W - 1) / (float)(g.Ho - 1)) - kDMar;
+    return q;
+  };
+  // window slice of tile t: kDWPix pixels × 2 parts of 16 B (two per thread)
+  constexpr int kWL = (kDWPix * 2 + kDT - 1) / kDT;
+  auto win_load = [&](const TileId& q, v4u (&v)[kWL]) {
+    const bf16_t* xb = xT + (size_t)q.b * g.HWi * g.C + kDC * cs;
+#pragma unroll
+    for (int k = 0; k < kWL; ++k) {
+      const int idx = tid + k * kDT;
+      const int pix = idx >> 1, part = idx & 1;
+      const int rr = pix / kDWQ, qq = pix - rr * kDWQ;
+      const int r = q.rlo + rr, qc = q.qlo + qq;
+      const bool ok = idx < kDWPix * 2 && r >= 0 && r < g.H && qc >= 0 && qc < g.W;
+      v[k] = ld16v_if(xb + ((size_t)r * g.W + qc) * g.C + 8 * part, ok);
+    }
+  };
+  auto win_store = [&](int buf, const v4u (&v)[kWL]) {
+    char* wb = dl + kDLWin + buf * kDWPix * kDWPitch;
+#pragma unroll
+    for (int k = 0; k < kWL; ++k) {
+      const int idx = tid + k * kDT;
+      if (idx < kDWPix * 2) *reinterpret_cast<v4u*>(wb + (idx >> 1) * kDWPitch + (idx & 1) * 16) = v[k];
+    }
+  };
+  // records of tile t: the offsets (Δx, Δy) of its (slot, tap) samples, two per thread
+  constexpr int kRL = (kSlots * kMaxN + kDT - 1) / kDT;
+  auto rec_load = [&](const TileId& q, float (&dx)[kRL], float (&dy)[kRL]) {
+    const float* ob = off + (size_t)q.b * g.J * g.HW;
+#pragma unroll
+    for (int k = 0; k < kRL; ++k) {
+      const int sidx = tid + k * kDT;
+      const int p = sidx / N, n = sidx - p * N;
+      const int h = q.h0 + p / kTW, w = q.w0 + p % kTW;
+      const bool ok = sidx < kSlots * N && h < g.Ho && w < g.Wo;
+      const int m = ok ? h * g.Wo + w : 0;
+      dx[k] = ok ? ob[(size_t)n * g.HW + m] : 0.f;
+      dy[k] = ok ? ob[(size_t)(N + n) * g.HW + m] : 0.f;
+    }
+  };
+  auto rec_store = [&](int buf, const TileId& q, const float (&dx)[kRL], const float (&dy)[kRL]) {
+    float4* rw = reinterpret_cast<float4*>(dl + kDLRecW + buf * kSlots * kMaxN * 16);
+    int* rm = reinterpret_cast<int*>(dl + kDLRecM + buf * kSlots * kMaxN * 4);
+#pragma unroll
+    for (int k = 0; k < kRL; ++k) {
+      const int sidx = tid + k * kDT;
+      if (sidx < kSlots * N) {
+        const int p = sidx / N, n = sidx - p * N;
+        const int h = q.h0 + p / kTW, w = q.w0 + p % kTW;
+        int meta = kMZero;
+        float4 wv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (h < g.Ho && w < g.Wo) {
+          float iy, ix;
+          ref_coord(h, w, dx[k], dy[k], g, iy, ix);
+          const Tap t = make_tap(iy, ix, g);
+          if (t.ok) {
+            const float gr = 1.0f - t.fr, gc = 1.0f - t.fc;
+            wv = make_float4(gr * gc, gr * t.fc, t.fr * gc, t.fr * t.fc);
+            const int rr = t.r0 - q.rlo, qq = t.c0 - q.qlo;
+            meta = (rr >= 0 && rr + 1 < kDWR && qq >= 0 && qq + 1 < kDWQ) ? rr * kDWQ + qq : kDSlow;
+          }
+        }
+        rm[n * kSlots + p] = meta;
+        rw[n * kSlots + p] = wv;
+      }
+    }
+  };
+  // A fragments of tile t: ∂out[b][o][slot] for slots 32·ks + 8·(lane >> 4) .. +7, rows
+  // o0 + 16·ob + (lane & 15); slots outside the image (or >= 112) read as 0
+  auto a_load = [&](const TileId& q, v4u (&a)[kDOB][4]) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int sl = 32 * ks + 8 * (lane >> 4);  // 8 slots of one tile row (kTW = 16)
+      const int h = q.h0 + sl / kTW, w = q.w0 + sl % kTW;
+      const bool rowok = sl < kSlots && h < g.Ho;
+      const int nv = rowok ? min(8, g.Wo - w) : 0;
+#pragma unroll
+      for (int ob = 0; ob < kDOB; ++ob) {
+        const int o = o0 + 16 * ob + (lane & 15);
+        const bf16_t* src = gout + ((size_t)q.b * g.O + o) * g.HW + (size_t)h * g.Wo + w;
+        v4u v = {0u, 0u, 0u, 0u};
+        if (nv >= 8 && ((reinterpret_cast<uintptr_t>(src) & 7) == 0)) {
+          const uint2 lo = *reinterpret_cast<const uint2*>(src);
+          const uint2 hi = *reinterpret_cast<const uint2*>(src + 4);
+          v = v4u{lo.x, lo.y, hi.x, hi.y};
+        } else if (nv > 0) {
+          unsigned e[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) e[j] = j < nv ? (unsigned)src[j] : 0u;
+          v = v4u{e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16)};
+        }
+        a[ob][ks] = v;
+      }
+    }
+  };
+  // the column tile of tile t (records / window buffer rb) into col buffer cb: pair-unit u =
+  // (tap n, 8-channel group cg, slot pair sp), two per thread; consecutive lanes take
+  // consecutive slot pairs, so the transposed 32-bit stores of a wave hit distinct banks
+  auto produce = [&](const TileId& q, int rb, int cb) {
+    const char* wb = dl + kDLWin + rb * kDWPix * kDWPitch;
+    const float4* rw = reinterpret_cast<const float4*>(dl + kDLRecW + rb * kSlots * kMaxN * 16);
+    const int* rm = reinterpret_cast<const int*>(dl + kDLRecM + rb * kSlots * kMaxN * 4);
+    char* col = dl + kDLCol + cb * kMaxN * kDC * kDRow;
+    const bf16_t* xb = xT + (size_t)q.b * g.HWi * g.C + kDC * cs;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int u = tid + k * kDT;
+      const int sp = u % (kSlots / 2), rest = u / (kSlots / 2);
+      const int n = rest >> 1, cg = rest & 1;
+      if (n < N) {
+        v4u o2[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int slot = 2 * sp + e;
+          const int meta = rm[n * kSlots + slot];
+          const float4 wv = rw[n * kSlots + slot];
+          const char* wp = wb + max(meta, 0) * kDWPitch + cg * 16;
+          const v4u ua = *reinterpret_cast<const v4u*>(wp);
+          const v4u ub = *reinterpret_cast<const v4u*>(wp + kDWPitch);
+          const v4u uc = *reinterpret_cast<const v4u*>(wp + kDWQ * kDWPitch);
+          const v4u ud = *reinterpret_cast<const v4u*>(wp + (kDWQ + 1) * kDWPitch);
+          v4u o = blend8(wv, ua, ub, uc, ud);
+          const v4u z = {0u, 0u, 0u, 0u};
+          o = meta >= 0 ? o : z;
+          if (__any(meta == kDSlow)) {
+            if (meta == kDSlow) {
+              const int h = q.h0 + slot / kTW, w = q.w0 + slot % kTW;
+              const Tap t = sample_tap(g, off, q.b, 0, n, h * g.Wo + w);
+              o = as_v(gather_global(g, xb, t.r0, t.c0, 8 * cg, wv));
+            }
+          }
+          o2[e] = o;
+        }
+        // transposed: row (n, channel 8·cg + i), columns slot 2sp, 2sp+1 packed in 32 bits
+        char* dst = col + (n * kDC + 8 * cg) * kDRow + 4 * sp;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const unsigned a0 = o2[0][i], a1 = o2[1][i];
+          *reinterpret_cast<unsigned*>(dst + (2 * i) * kDRow) = (a0 & 0xffffu) | (a1 << 16);
+          *reinterpret_cast<unsigned*>(dst + (2 * i + 1) * kDRow) = (a0 >> 16) | (a1 & 0xffff0000u);
+        }
+      }
+    }
+  };
+
+  f32x4 acc[kDOB][kMaxN];
+#pragma unroll
+  for (int i = 0; i < kDOB; ++i)
+#pragma unroll
+    for (int n = 0; n < kMaxN; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mfma_tile = [&](int cb, const v4u (&a)[kDOB][4]) {
+    const char* col = dl + kDLCol + cb * kMaxN * kDC * kDRow + (lane & 15) * kDRow + (lane >> 4) * 16;
+#pragma unroll
+    for (int n = 0; n < kMaxN; ++n) {
+      if (n < N) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const v4u bv = *reinterpret_cast<const v4u*>(col + n * kDC * kDRow + ks * 64);
+#pragma unroll
+          for (int ob = 0; ob < kDOB; ++ob)
+            acc[ob][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a[ob][ks]), as_frag(bv),
+                                                               acc[ob][n], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  // zero both col buffers once (slots 112..127 and unused taps stay zero)
+  for (int i = tid * 16; i < 2 * kMaxN * kDC * kDRow; i += kDT * 16)
+    *reinterpret_cast<v4u*>(dl + kDLCol + i) = v4u{0u, 0u, 0u, 0u};
+  v4u wv_[kWL];
+  float dx[kRL], dy[kRL];
+  v4u aP[kDOB][4], aC[kDOB][4];
+  if (T > 0) {
+    const TileId q0 = tile_id(0);
+    win_load(q0, wv_);
+    rec_load(q0, dx, dy);
+    a_load(q0, aC);
+    win_store(0, wv_);
+    rec_store(0, q0, dx, dy);
+  }
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {
+    const TileId q = tile_id(t);
+    const bool nxt = t + 1 < T;
+    TileId qn = q;
+    if (nxt) {
+      qn = tile_id(t + 1);
+      win_load(qn, wv_);
+      rec_load(qn, dx, dy);
+    }
+    produce(q, t & 1, t & 1);
+    if (t > 0) mfma_tile((t - 1) & 1, aP);
+    // aP <- aC (tile t, used next iteration); aC <- tile t + 1
+#pragma unroll
+    for (int i = 0; i < kDOB; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) aP[i][ks] = aC[i][ks];
+    if (nxt) {
+      a_load(qn, aC);
+      win_store((t + 1) & 1, wv_);
+      rec_store((t + 1) & 1, qn, dx, dy);
+    }
+    __syncthreads();
+  }
+  if (T > 0) mfma_tile((T - 1) & 1, aP);
+
+  // partial ∂Wf[o][n·C + 16·cs + ch] of this image group; C/D: col = lane & 15 (ch), row =
+  // 4·(lane >> 4) + r (o)
+  float* pg = parts + (size_t)grp * g.O * g.K;
+#pragma unroll
+  for (int ob = 0; ob < kDOB; ++ob)
+#pragma unroll
+    for (int n = 0; n < kMaxN; ++n) {
+      if (n < N) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int o = o0 + 16 * ob + 4 * (lane >> 4) + r;
+          pg[(size_t)o * g.K + n * g.C + kDC * cs + (lane & 15)] = acc[ob][n][r];
+        }
+      }
+    }
+}
+
 }  // namespace
 
 bool fused_fwd_bf16_ok(const Geo& g) {
@@ -352,6 +652,32 @@ hipError_t launch_fused_fwd_bf16(const Geo& g, const bf16_t* xT, const float* of
   else
     hipLaunchKernelGGL(fwd_fused_bf16<false>, grid, dim3(256), 0, s, g, xT, off, wfr, bias, out,
                        colT, tw_n);
+  return hipGetLastError();
+}
+
+bool fused_dw_bf16_ok(const Geo& g) {
+  return g.dt == DCN_BF16 && g.G == 1 && g.N <= kMaxN && g.C % kDC == 0 && g.O % kOT == 0 &&
+         g.Ho >= 2 && g.Wo >= 2 && (long)g.O * g.K < (1l << 31) &&
+         (long)g.B * g.O * g.HW < (1l << 40);
+}
+
+int fused_dw_bf16_groups(const Geo& g) { return std::min(16, g.B); }
+
+hipError_t launch_fused_dw_bf16(const Geo& g, const bf16_t* xT, const float* off,
+                                const bf16_t* gout, float* parts, hipStream_t s) {
+  if (!fused_dw_bf16_ok(g)) return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    attr = true;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dw_fused_bf16<0>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, kDLds);
+    if (e != hipSuccess) return e;
+  }
+  const int ng = fused_dw_bf16_groups(g);
+  const int tw_n = (g.Wo + kTW - 1) / kTW;
+  const dim3 grid(g.C / kDC, ng, g.O / kOT);
+  hipLaunchKernelGGL(dw_fused_bf16<0>, grid, dim3(kDT), kDLds, s, g, xT, off, gout, parts, tw_n,
+                     ng);
   return hipGetLastError();
 }
 

@@ -77,6 +77,12 @@ size_t fused_fwd_bf16_wfr_elems(const Geo& g);
 hipError_t launch_fused_fwd_bf16(const Geo& g, const bf16_t* xT, const float* off,
                                  const bf16_t* w, bf16_t* wfr, const float* bias, bf16_t* out,
                                  bf16_t* colT, hipStream_t s);
+// ∂Wf partials with the columns recomputed from xT (no column matrix): parts[grp][O][K] for
+// fused_dw_bf16_groups(g) image groups, summed afterwards in a fixed order.
+bool fused_dw_bf16_ok(const Geo& g);
+int fused_dw_bf16_groups(const Geo& g);
+hipError_t launch_fused_dw_bf16(const Geo& g, const bf16_t* xT, const float* off,
+                                const bf16_t* gout, float* parts, hipStream_t s);
 // dcn_offset_conv.hip:
 // wt / wt2: scratch of offset_conv_wt_floats(g) floats (transposed w_off copies).
 size_t offset_conv_wt_floats(const Geo& g);
