@@ -63,14 +63,20 @@ constexpr int kMZero = -1;  // record meta: sample contributes 0 (or slot outsid
 // for j >= kOvf, corners read from global memory in line
 
 // bilerp() with its weight products precomputed (same products, same op order); each
-// 32-bit word (2 channels) of the four corners is unpacked where it is used
+// 32-bit word (2 channels) of the four corners is unpacked where it is used, and the two
+// channels go through packed fp32 math (v_pk_mul_f32 / v_pk_fma_f32: per lane the same
+// roundings as the scalar mul / fmaf chain, half the instructions)
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2v unpack2(unsigned a) {
+  return f32x2v{__uint_as_float(a << 16), __uint_as_float(a & 0xffff0000u)};
+}
 __device__ __forceinline__ unsigned blend2(float4 wv, unsigned a, unsigned b, unsigned c,
                                            unsigned d) {
-  float lo = wv.x * __uint_as_float(a << 16), hi = wv.x * __uint_as_float(a & 0xffff0000u);
-  lo = fmaf(wv.y, __uint_as_float(b << 16), lo), hi = fmaf(wv.y, __uint_as_float(b & 0xffff0000u), hi);
-  lo = fmaf(wv.z, __uint_as_float(c << 16), lo), hi = fmaf(wv.z, __uint_as_float(c & 0xffff0000u), hi);
-  lo = fmaf(wv.w, __uint_as_float(d << 16), lo), hi = fmaf(wv.w, __uint_as_float(d & 0xffff0000u), hi);
-  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+  f32x2v v = f32x2v{wv.x, wv.x} * unpack2(a);
+  v = __builtin_elementwise_fma(f32x2v{wv.y, wv.y}, unpack2(b), v);
+  v = __builtin_elementwise_fma(f32x2v{wv.z, wv.z}, unpack2(c), v);
+  v = __builtin_elementwise_fma(f32x2v{wv.w, wv.w}, unpack2(d), v);
+  return (unsigned)f2bf(v.x) | ((unsigned)f2bf(v.y) << 16);
 }
 __device__ __forceinline__ uint4 blend8(float4 wv, uint4 ua, uint4 ub, uint4 uc, uint4 ud) {
   return make_uint4(blend2(wv, ua.x, ub.x, uc.x, ud.x), blend2(wv, ua.y, ub.y, uc.y, ud.y),
@@ -567,42 +573,51 @@ __global__ __launch_bounds__(kDT) void dw_fused_bf16(Geo g, const bf16_t* __rest
   // zero both col buffers once (slots 112..127 and unused taps stay zero)
   for (int i = tid * 16; i < 2 * kMaxN * kDC * kDRow; i += kDT * 16)
     *reinterpret_cast<v4u*>(dl + kDLCol + i) = v4u{0u, 0u, 0u, 0u};
-  v4u wv_[kWL];
-  float dx[kRL], dy[kRL];
-  v4u aP[kDOB][4], aC[kDOB][4];
+  // raw window / offset loads of the tile after next, in two register sets used alternately
+  // (named, not indexed, so no copy waits for a load still in flight)
+  v4u wA[kWL], wB[kWL];
+  float dxA[kRL], dyA[kRL], dxB[kRL], dyB[kRL];
+  v4u aC[kDOB][4];
   if (T > 0) {
     const TileId q0 = tile_id(0);
-    win_load(q0, wv_);
-    rec_load(q0, dx, dy);
+    win_load(q0, wA);
+    rec_load(q0, dxA, dyA);
     a_load(q0, aC);
-    win_store(0, wv_);
-    rec_store(0, q0, dx, dy);
+    win_store(0, wA);
+    rec_store(0, q0, dxA, dyA);
+    if (T > 1) {
+      const TileId q1 = tile_id(1);
+      win_load(q1, wA);
+      rec_load(q1, dxA, dyA);
+    }
   }
   __syncthreads();
-  for (int t = 0; t < T; ++t) {
+  // iteration t: gather tile t (buffers t & 1) beside the MFMAs of tile t - 1; then the
+  // A fragments of tile t, and tile t + 1's window and records (loaded an iteration ago)
+  // into the other buffers; tile t + 2's loads are issued first
+  auto body = [&](int t, v4u (&wn)[kWL], float (&dxn)[kRL], float (&dyn)[kRL], v4u (&wf)[kWL],
+                  float (&dxf)[kRL], float (&dyf)[kRL]) {
     const TileId q = tile_id(t);
-    const bool nxt = t + 1 < T;
-    TileId qn = q;
-    if (nxt) {
-      qn = tile_id(t + 1);
-      win_load(qn, wv_);
-      rec_load(qn, dx, dy);
+    if (t + 2 < T) {
+      const TileId qf = tile_id(t + 2);
+      win_load(qf, wf);
+      rec_load(qf, dxf, dyf);
     }
     produce(q, t & 1, t & 1);
-    if (t > 0) mfma_tile((t - 1) & 1, aP);
-    // aP <- aC (tile t, used next iteration); aC <- tile t + 1
-#pragma unroll
-    for (int i = 0; i < kDOB; ++i)
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) aP[i][ks] = aC[i][ks];
-    if (nxt) {
-      a_load(qn, aC);
-      win_store((t + 1) & 1, wv_);
-      rec_store((t + 1) & 1, qn, dx, dy);
+    if (t > 0) mfma_tile((t - 1) & 1, aC);
+    a_load(q, aC);
+    if (t + 1 < T) {
+      const TileId qn = tile_id(t + 1);
+      win_store((t + 1) & 1, wn);
+      rec_store((t + 1) & 1, qn, dxn, dyn);
     }
     __syncthreads();
+  };
+  for (int t = 0; t < T; t += 2) {
+    body(t, wA, dxA, dyA, wB, dxB, dyB);
+    if (t + 1 < T) body(t + 1, wB, dxB, dyB, wA, dxA, dyA);
   }
-  if (T > 0) mfma_tile((T - 1) & 1, aP);
+  if (T > 0) mfma_tile((T - 1) & 1, aC);
 
   // partial ∂Wf[o][n·C + 16·cs + ch] of this image group; C/D: col = lane & 15 (ch), row =
   // 4·(lane >> 4) + r (o)
@@ -629,11 +644,10 @@ bool fused_fwd_bf16_ok(const Geo& g) {
          g.Ho >= 2 && g.Wo >= 2 && (long)g.O * g.K < lim && (long)g.HW * g.K < (1l << 31);
 }
 
-// measured against K1 + hipBLASLt + bias at config 4
-bool fused_fwd_bf16_pays(const Geo& g) {
-  (void)g;
-  return false;
-}
+// r03 at config 4 (C = O = 256, 28x28): the fused forward with its column stores 0.150 ms
+// against K1 0.069 + hipBLASLt 0.082 + bias 0.017 ms (step 0.686-0.701 vs 0.695-0.703 ms,
+// DESIGN.md §4.7); measured only with 256 input channels
+bool fused_fwd_bf16_pays(const Geo& g) { return g.C >= 256; }
 
 size_t fused_fwd_bf16_wfr_elems(const Geo& g) { return (size_t)g.O * g.K; }
 
