@@ -475,6 +475,25 @@ def main():
                "ms_per_step": round(el_alt / args.steps * 1e3, 4), "kernel_ms": alt_k,
                "note": "same synthetic step, GEMMs in exact-split bf16 MFMA arithmetic "
                        "(DESIGN.md §4.6); reported beside the headline, not as value"}
+    # DCN_BF16: the other forward schedules of the same step (include/dcn.h dcn_fwd_path),
+    # timed like the alt arithmetic, reported beside the headline, never as `value`
+    fwd_paths = None
+    if world == 1 and bf16 and args.fwd_path == 0 and not args.graph and not fwd_only:
+        h.prof_enable(0)
+        fwd_paths = {}
+        for name, pth in (("unfused (K1 + hipBLASLt + bias)", 1),
+                          ("fused, columns stored (DCN_FWD_FUSED)", 2),
+                          ("fused, no column matrix (DCN_FWD_FUSED_NOCOL: recomputed dW)", 3)):
+            h.set_fwd_path(pth)
+            for _ in range(max(2, args.warmup)):
+                step()
+            torch.cuda.synchronize(dev)
+            tp = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize(dev)
+            fwd_paths[name] = round((time.perf_counter() - tp) / args.steps * 1e3, 4)
+        h.set_fwd_path(0)
     k1_ms = kernel_ms.get("im2col")
     k1_b = k1_bytes(B, C, H, W, N, Ho, Wo, elem=2 if bf16 else 4, J=J)
     k1_name = K1_KERNEL if (G == 1 and C % 4 == 0) else "dcn::im2col_cl"
@@ -556,6 +575,7 @@ def main():
             "rooflines_other": other_rooflines(kernel_ms, B, C, O_, H, W, N, Ho, Wo, J, bf16,
                                                fwd_only),
             "alt": alt,
+            "fwd_paths_ms_per_step": fwd_paths,
             "strong_scaling": strong_res,
             "cpu_baseline": None,
             "cpu_baseline_other": None,
