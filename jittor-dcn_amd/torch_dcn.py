@@ -5,8 +5,10 @@ out_channels, kernel_size=3, stride=1, padding=1, bias=True), zero-initialised o
 conv, gauss-initialised weight) over GPU-resident torch tensors. Forward and backward
 are dcn_forward / dcn_backward on torch's current HIP stream, so there are no host
 copies. Each module keeps its workspace, so the backward reuses the forward's columns
-(DCN_BWD_COL_IN_WS). torch is only the tensor container here: every kernel is libdcn's,
-and a missing libdcn.so or HIP device raises (no fallback).
+(DCN_BWD_COL_IN_WS); a bf16 forward that no backward will follow (torch.no_grad, or no
+input needing a gradient: the reference's jt.no_grad inference, train.py:430) runs
+DCN_FWD_FUSED_NOCOL, which never writes the column matrix. torch is only the tensor container
+here: every kernel is libdcn's, and a missing libdcn.so or HIP device raises (no fallback).
 """
 from __future__ import annotations
 
@@ -51,7 +53,7 @@ class _Workspace:
 
 class DeformConv2dFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w_off, b_off, w, b, stride, padding, ws: _Workspace):
+    def forward(ctx, x, w_off, b_off, w, b, stride, padding, ws: _Workspace, nocol=False):
         if x.dtype not in _DT:
             raise TypeError("libdcn DeformConv2d takes float32 or bfloat16 tensors")
         x, w_off, b_off, w = (t.contiguous() for t in (x, w_off, b_off, w))
@@ -67,8 +69,15 @@ class DeformConv2dFunction(torch.autograd.Function):
         wsb = rt.workspace_bytes(desc, True)
         buf = ws.get(wsb, x.device)
         P = lambda t: None if t is None else t.data_ptr()
-        rt.check(h.lib.dcn_forward(h.h, desc, P(x), P(w_off), P(b_off), P(w), P(b), P(out),
-                                   P(off), P(buf), wsb), "dcn_forward")
+        nocol = nocol and x.dtype == torch.bfloat16
+        if nocol:  # forward-only: no columns for a backward
+            h.set_fwd_path(rt.DCN_FWD_FUSED_NOCOL)
+        try:
+            rt.check(h.lib.dcn_forward(h.h, desc, P(x), P(w_off), P(b_off), P(w), P(b), P(out),
+                                       P(off), P(buf), wsb), "dcn_forward")
+        finally:
+            if nocol:
+                h.set_fwd_path(rt.DCN_FWD_AUTO)
         ctx.save_for_backward(x, off, w_off, w)
         ctx.desc, ctx.ws, ctx.wsb, ctx.has_bias = desc, ws, wsb, b is not None
         ws.fwd_count += 1
@@ -90,7 +99,7 @@ class DeformConv2dFunction(torch.autograd.Function):
         rt.check(h.lib.dcn_backward(h.h, ctx.desc, P(x), P(off), P(w_off), P(w), P(gout), P(gx),
                                     P(gw), P(gb), P(gwo), P(gbo), None, P(buf), ctx.wsb, flags),
                  "dcn_backward")
-        return gx, gwo, gbo, gw, gb, None, None, None
+        return gx, gwo, gbo, gw, gb, None, None, None, None
 
 
 class DeformConv2d(torch.nn.Module):
@@ -114,6 +123,9 @@ class DeformConv2d(torch.nn.Module):
         self._ws = _Workspace()
 
     def forward(self, x):
+        params = (x, self.offset_conv.weight, self.offset_conv.bias, self.weight, self.bias)
+        needs_grad = torch.is_grad_enabled() and any(
+            t is not None and t.requires_grad for t in params)
         return DeformConv2dFunction.apply(x, self.offset_conv.weight, self.offset_conv.bias,
                                           self.weight, self.bias, self.stride, self.padding,
-                                          self._ws)
+                                          self._ws, not needs_grad)

@@ -167,3 +167,32 @@ def test_torch_module_surface_and_bf16():
     assert rel(yb.float(), y) <= 1e-2
     yb.float().sum().backward()
     assert mb.weight.grad is not None and mb.weight.grad.dtype == torch.bfloat16
+
+
+def test_torch_bf16_no_grad_forward_writes_no_columns():
+    """A bf16 forward under torch.no_grad (the reference's jt.no_grad inference,
+    train.py:430) runs DCN_FWD_FUSED_NOCOL: same output bits as the grad-enabled forward
+    (which DCN_FWD_AUTO runs fused with its columns stored at C >= 256), and the gradients of
+    a forward followed by a no-grad forward of the same module stay bit for bit: the no-grad
+    call advanced the workspace token, so the backward recomputes the columns."""
+    import torch_dcn
+    torch.manual_seed(3)
+    m = torch_dcn.DeformConv2d(256, 256, 3, 1, 1).cuda().to(torch.bfloat16)
+    with torch.no_grad():
+        m.offset_conv.weight.normal_(0, 1.0 / 48)
+        m.offset_conv.bias.uniform_(-0.5, 0.5)
+    x = torch.randn(2, 256, 14, 14, device="cuda", dtype=torch.bfloat16)
+    with torch.no_grad():
+        y0 = m(x)
+    xg = x.clone().requires_grad_(True)
+    y1 = m(xg)
+    assert torch.equal(y0.view(torch.int16), y1.detach().view(torch.int16))
+    g = torch.randn_like(y1)
+    y1.backward(g)
+    gw_a = m.weight.grad.clone()
+    m.weight.grad = None
+    y2 = m(xg)
+    with torch.no_grad():
+        m(x)  # a forward-only call in between: its columns are not written
+    y2.backward(g)
+    assert torch.equal(gw_a.view(torch.int16), m.weight.grad.view(torch.int16))
