@@ -220,6 +220,23 @@ def load_traffic(path, bf16=False):
     return None, None
 
 
+def load_fused_traffic(bf16_cfg4_glob="r*_pmc_hbm_config4.json"):
+    """HBM bytes per launch of the bf16 fused forward (columns stored) from the newest
+    committed config-4 PMC summary."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", bf16_cfg4_glob)))
+    for path in reversed(paths):
+        try:
+            with open(path) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            continue
+        for name, v in doc.get("kernels", {}).items():
+            if name.startswith("dcn::fwd_fused_bf16<true>"):
+                return int(v["hbm_bytes"]), f"{os.path.relpath(path, ROOT)}:{name}"
+    return None, None
+
+
 MATH_NAMES = {0: "f32 MFMA (rocBLAS/hipBLASLt)", 3: "f32 via split-bf16 X3 (2 planes, opt-in)",
               6: "f32 via exact-split bf16 X6", 9: "f32 via exact-split bf16 X9"}
 
@@ -580,6 +597,26 @@ def main():
             "cpu_baseline": None,
             "cpu_baseline_other": None,
         }
+        if bf16 and not k1_ms and kernel_ms.get("gemm_fwd"):
+            # DCN_FWD_AUTO ran the fused forward: K1 does not exist as a
+            # launch; the dominant forward kernel is the fused one (gather + GEMM + bias)
+            fl = 2.0 * B * Ho * Wo * N * C * O_
+            ms = kernel_ms["gemm_fwd"]
+            tr, tr_src = load_fused_traffic()
+            res["roofline"] = {
+                "kernel": "dcn::fwd_fused_bf16 (f2: bilinear gather into bf16 MFMA + bias, "
+                          "columns stored for the backward)",
+                "bound": "mfma",
+                "achieved": round(fl / (ms * 1e-3) / 1e12, 1),
+                "peak": 2500.0,
+                "unit": "TFLOP/s",
+                "frac": round(fl / (ms * 1e-3) / 1e12 / 2500.0, 4),
+                "traffic": tr,
+                "traffic_source": tr_src,
+                "algorithmic_flop": fl,
+                "avg_launch_ms": ms,
+                "note": "HIP events around the launch (wf_to_frag16 swizzle included)",
+            }
         if world == 1 and not bf16 and not args.no_host_path:
             res["host_path"] = host_path_rate(cfg, args.config)
         if world == 1 and not args.no_cpu_baseline:
