@@ -115,15 +115,17 @@ __device__ __forceinline__ v4u blend8(float4 wv, v4u ua, v4u ub, v4u uc, v4u ud)
 }
 
 // wfr[ob][ks][lane][8] = Wf[16·ob + (lane & 15)][32·ks + 8·(lane >> 4) + e]: the A fragment of
-// v_mfma_f32_16x16x32_bf16 for output-channel block ob and k step ks, one 16-B load per lane
+// v_mfma_f32_16x16x32_bf16 for output-channel block ob and k step ks, one 16-B load per lane;
+// one thread per fragment (the 8 elements are contiguous in Wf: one 16-B load and store)
 __global__ __launch_bounds__(256) void wf_to_frag16(const bf16_t* __restrict__ w,
                                                     bf16_t* __restrict__ wfr, int O, int K) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long)O * K) return;
-  const int e = (int)(i & 7), l = (int)((i >> 3) & 63);
-  const long rest = i >> 9;
+  const long f = (long)blockIdx.x * 256 + threadIdx.x;  // fragment = (ob, ks, lane)
+  if (f >= (long)O * K / 8) return;
+  const int l = (int)(f & 63);
+  const long rest = f >> 6;
   const int NKS = K / 32, ob = (int)(rest / NKS), ks = (int)(rest - (long)ob * NKS);
-  wfr[i] = w[(size_t)(16 * ob + (l & 15)) * K + 32 * ks + 8 * (l >> 4) + e];
+  *reinterpret_cast<uint4*>(wfr + f * 8) = *reinterpret_cast<const uint4*>(
+      w + (size_t)(16 * ob + (l & 15)) * K + 32 * ks + 8 * (l >> 4));
 }
 
 template <bool STORE>
@@ -321,22 +323,42 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
     }
   }
 
-  // ---- epilogue: out[b][o][h][w] = bf16(acc + bias[o]); C/D: col = lane & 15, row = 4(lane>>4)+r
-  const int wcol = w0 + (lane & 15);
-  if (wcol < g.Wo) {
+  // ---- epilogue: out[b][o][h][w] = bf16(acc + bias[o]) (launch_bias_to_bf16's rounding).
+  // The tile goes through LDS as [o][slot] (the window / B / record regions are free now) so
+  // that each thread stores 8 consecutive pixels of one (o, h) as two 8-B runs instead of
+  // 112 scattered 2-B stores per lane (r03: 15 us of the kernel's 140). C/D map: slot =
+  // 16·pb + (lane & 15), o = 16·i + 4·(lane >> 4) + r.
+  constexpr int kEP = kSlots * 2 + 16;  // bytes per output-channel row of the staged tile
+  static_assert(kOT * kEP <= kLdsOvfT, "staged output tile fits the freed LDS");
+  __syncthreads();  // every wave is past its last B-tile read
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int o = o0 + 16 * i + 4 * (lane >> 4) + r;
-        const float bv = bias ? bias[o] : 0.f;
-        bf16_t* op = out + ((size_t)b * g.O + o) * g.HW + wcol;
+    for (int r = 0; r < 4; ++r) {
+      const int ol = 64 * wave + 16 * i + 4 * (lane >> 4) + r;
+      const float bv = bias ? bias[o0 - 64 * wave + ol] : 0.f;
 #pragma unroll
-        for (int pb = 0; pb < kPB; ++pb) {
-          const int h = h0 + pb;
-          if (h < g.Ho) op[(size_t)h * g.Wo] = f2bf(acc[i][pb][r] + bv);
-        }
-      }
+      for (int pb = 0; pb < kPB; ++pb)
+        *reinterpret_cast<bf16_t*>(lds + ol * kEP + (16 * pb + (lane & 15)) * 2) =
+            f2bf(acc[i][pb][r] + bv);
+    }
+  __syncthreads();
+  // 8-pixel runs: (output channel, tile row, half row)
+  const int ob0 = blk.z * kOT;
+  for (int u = tid; u < kOT * kTH * 2; u += 256) {
+    const int half = u & 1, rest = u >> 1;
+    const int th = rest % kTH, ol = rest / kTH;
+    const int h = h0 + th, wc = w0 + 8 * half;
+    if (h >= g.Ho || wc >= g.Wo) continue;
+    const uint4 v = *reinterpret_cast<const uint4*>(lds + ol * kEP + (16 * th + 8 * half) * 2);
+    bf16_t* op = out + ((size_t)b * g.O + ob0 + ol) * g.HW + (size_t)h * g.Wo + wc;
+    if (wc + 8 <= g.Wo && ((reinterpret_cast<uintptr_t>(op) & 7) == 0)) {
+      *reinterpret_cast<uint2*>(op) = make_uint2(v.x, v.y);
+      *reinterpret_cast<uint2*>(op + 4) = make_uint2(v.z, v.w);
+    } else {
+      const unsigned e[4] = {v.x, v.y, v.z, v.w};
+      for (int j = 0; j < 8 && wc + j < g.Wo; ++j)
+        op[j] = (bf16_t)((e[j >> 1] >> (16 * (j & 1))) & 0xffffu);
     }
   }
 }
@@ -656,8 +678,8 @@ hipError_t launch_fused_fwd_bf16(const Geo& g, const bf16_t* xT, const float* of
                                  bf16_t* colT, hipStream_t s) {
   if (!fused_fwd_bf16_ok(g)) return hipErrorInvalidValue;
   const long nw = (long)g.O * g.K;
-  hipLaunchKernelGGL(wf_to_frag16, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, w, wfr,
-                     g.O, g.K);
+  hipLaunchKernelGGL(wf_to_frag16, dim3((unsigned)((nw / 8 + 255) / 256)), dim3(256), 0, s, w,
+                     wfr, g.O, g.K);
   const int th_n = (g.Ho + kTH - 1) / kTH, tw_n = (g.Wo + kTW - 1) / kTW;
   const dim3 grid(th_n * tw_n, g.B, g.O / kOT);
   if (colT)
