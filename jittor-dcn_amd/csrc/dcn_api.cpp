@@ -541,13 +541,19 @@ int forward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x,
     if (has_bias) cb.add(b, F32(L.b32), (size_t)g.O, false);
     HIP_TRY(dcn::launch_convert_multi(cb, st));
   }
-  {
+  // f3: the offset conv stages its windows from the NCHW x and writes xT itself (one pass
+  // over x, no transpose launch) wherever its row kernel applies with stride 1
+  const bool fold = dcn::offset_fwd_bf16_fold_ok(g) && !dcn::get_force_generic();
+  if (!fold) {
     ProfScope ps(h, DCN_K_XPOSE);
     HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(x, xT, g.B, g.C, g.HWi, st));
   }
   {
     ProfScope ps(h, DCN_K_OFFSET_FWD);
-    if (dcn::offset_fwd_mfma_bf16_ok(g)) {
+    if (fold) {
+      HIP_TRY(dcn::launch_offset_conv_fwd_bf16(g, xT, w_off, F32(L.boff32), off32, off,
+                                               BF(L.wb16), st, x));
+    } else if (dcn::offset_fwd_mfma_bf16_ok(g)) {
       // bf16 MFMA straight from the bf16 xT: the offsets, rounded to bf16 (off) and as
       // fp32 values (off32, what the sampling uses)
       HIP_TRY(dcn::launch_offset_conv_fwd_bf16(g, xT, w_off, F32(L.boff32), off32, off,

@@ -100,9 +100,12 @@ hipError_t launch_offset_conv_fwd(const Geo& g, const float* x, const float* w_o
 // bf16-rounded offsets (off) and their fp32 values (off32). Needs offset_fwd_mfma_bf16_ok.
 bool offset_fwd_mfma_bf16_ok(const Geo& g);
 size_t offset_fwd_bf16_wb_elems(const Geo& g);
+// x_nchw != NULL (needs offset_fwd_bf16_fold_ok): f3, the window staged from the NCHW x and
+// xT WRITTEN by the same blocks (no separate transpose launch, one pass over x).
+bool offset_fwd_bf16_fold_ok(const Geo& g);
 hipError_t launch_offset_conv_fwd_bf16(const Geo& g, const bf16_t* xT, const bf16_t* w_off,
                                        const float* b_off, float* off32, bf16_t* off, bf16_t* wb,
-                                       hipStream_t s);
+                                       hipStream_t s, const bf16_t* x_nchw = nullptr);
 // DCN_BF16 offset-conv backward on bf16 MFMA (stride 1, C % 64 == 0, H·W % 8 == 0): gx is
 // the bf16 NCHW grad_x = transpose(gxT_in) + the offset-conv route. part: the goffT scratch;
 // wc: offset_bwd_bf16_wc_elems(g) bf16 values.

@@ -1018,11 +1018,15 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16(
 // checks), then reads its A fragments from LDS: each x byte leaves L2 once per block, not
 // once per tap and pixel, and the global loads touch whole lines (the register-direct
 // kernel's 16-B-per-pixel gathers touched 32 lines per load instruction).
-template <int SPT>
+// FOLD (f3): the window is staged from the NCHW bf16 x instead of xT, and the
+// block writes its own input row (window row ph: stride 1, Ho == H) to xT — the channels-last
+// copy K1 / the fused forward / K5 read — so x is read in one pass and the separate transpose
+// launch disappears, as offset_conv_fwd_mfma_xt does for fp32 (offset_fwd_bf16_fold_ok).
+template <int SPT, bool FOLD = false>
 __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
     Geo g, const bf16_t* __restrict__ xT, const bf16_t* __restrict__ wb, int Cp,
     const float* __restrict__ b_off, float* __restrict__ off32, bf16_t* __restrict__ off,
-    int tpr, int SWc) {
+    int tpr, int SWc, const bf16_t* __restrict__ x_nchw = nullptr, bf16_t* __restrict__ xT_out = nullptr) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_row[];
   constexpr int P = 16 * SPT + 8;  // LDS pixel pitch (bf16)
   const int lane = threadIdx.x & 63;
@@ -1033,7 +1037,42 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
   const int KH = g.kh, KK = g.kh * g.kw;
   bf16_t* L = reinterpret_cast<bf16_t*>(smem_row) + (size_t)w * KH * SWc * P;
   const int cw = w * SPT * 16;  // this wave's first channel
-  {
+  if constexpr (FOLD) {
+    // zero the slice (image borders and the channel padding past C stay zero), then the
+    // in-image part from NCHW rows: item = (channel pair, window row, 4-pixel chunk), two
+    // 8-B loads (channels c, c+1) -> four 32-bit LDS stores of (c, c+1) per pixel
+    const int nz = KH * SWc * P / 8;
+    for (int i = lane; i < nz; i += 64) reinterpret_cast<uint4*>(L)[i] = make_uint4(0u, 0u, 0u, 0u);
+    __builtin_amdgcn_wave_barrier();
+    const int NQ = g.W / 4, x0 = -g.pw;  // wo0 == 0 (tpr == 1)
+    const int nit = 8 * SPT * KH * NQ;
+    const bf16_t* xb = x_nchw + (size_t)b * g.C * g.HWi;
+    for (int it = lane; it < nit; it += 64) {
+      const int q = it % NQ, rest = it / NQ;
+      const int i = rest % KH, cp = rest / KH;
+      const int y = ho - g.ph + i, c = cw + 2 * cp;
+      if (y < 0 || y >= g.H || c >= g.C) continue;
+      const bf16_t* p0 = xb + ((size_t)c * g.H + y) * g.W + 4 * q;
+      const uint2 u0 = *reinterpret_cast<const uint2*>(p0);
+      const uint2 u1 = *reinterpret_cast<const uint2*>(p0 + g.HWi);
+      unsigned* d = reinterpret_cast<unsigned*>(L + (i * SWc + 4 * q - x0) * P + 2 * cp);
+      constexpr int PW = P / 2;  // pixel pitch in 32-bit words
+      d[0] = (u0.x & 0xffffu) | (u1.x << 16);
+      d[PW] = (u0.x >> 16) | (u1.x & 0xffff0000u);
+      d[2 * PW] = (u0.y & 0xffffu) | (u1.y << 16);
+      d[3 * PW] = (u0.y >> 16) | (u1.y & 0xffff0000u);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // input row ho (window row ph) -> xT[b][ho][px][cw ..]: 16-B runs of 8 channels
+    const int ir = g.ph;
+    const int nch = min(16 * SPT, g.C - cw);
+    for (int it = lane; it < g.W * (16 * SPT / 8); it += 64) {
+      const int ch8 = it % (16 * SPT / 8), px = it / (16 * SPT / 8);
+      if (8 * ch8 >= nch) continue;
+      const uint4 v = *reinterpret_cast<const uint4*>(L + (ir * SWc + px - x0) * P + 8 * ch8);
+      *reinterpret_cast<uint4*>(xT_out + (((size_t)b * g.H + ho) * g.W + px) * g.C + cw + 8 * ch8) = v;
+    }
+  } else {
     const auto rx = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<bf16_t*>(xT + (size_t)b * g.HWi * g.C), 0, (int)((size_t)g.HWi * g.C * 2),
         0x00020000);
@@ -1142,10 +1181,18 @@ size_t offset_fwd_bf16_wb_elems(const Geo& g) {
 }
 
 // xT: channels-last bf16 x; wb: scratch of offset_fwd_bf16_wb_elems(g) bf16 values.
+bool offset_fwd_bf16_fold_ok(const Geo& g) {
+  int SWc = 0;
+  return offset_fwd_mfma_bf16_ok(g) && fwd_bf16_row_lds(g, &SWc) && g.sh == 1 && g.sw == 1 &&
+         g.dh == 1 && g.dw == 1 && g.Ho == g.H && g.Wo == g.W && g.W <= 32 && g.W % 4 == 0 &&
+         g.ph >= 0 && g.ph < g.kh && g.pw >= 0 && g.pw < g.kw && g.C % 8 == 0;
+}
+
 hipError_t launch_offset_conv_fwd_bf16(const Geo& g, const bf16_t* xT, const bf16_t* w_off,
                                        const float* b_off, float* off32, bf16_t* off, bf16_t* wb,
-                                       hipStream_t s) {
+                                       hipStream_t s, const bf16_t* x_nchw) {
   if (!offset_fwd_mfma_bf16_ok(g)) return hipErrorInvalidValue;
+  if (x_nchw && !offset_fwd_bf16_fold_ok(g)) return hipErrorInvalidValue;
   const int KK = g.kh * g.kw, Cp = (g.C + 63) / 64 * 64;
   const int n = KK * 32 * Cp;
   hipLaunchKernelGGL(woff_to_tjc_bf16, dim3((n + 255) / 256), dim3(256), 0, s, w_off, wb, g.J,
@@ -1157,8 +1204,16 @@ hipError_t launch_offset_conv_fwd_bf16(const Geo& g, const bf16_t* xT, const bf1
     const int tpr = (g.Wo + 31) / 32;
     dim3 grid(tpr * g.Ho, 1, g.B);
     auto go = [&](auto kern) {
-      hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g, xT, wb, Cp, b_off, off32, off, tpr, SWc);
+      hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g, xT, wb, Cp, b_off, off32, off, tpr, SWc,
+                         x_nchw, const_cast<bf16_t*>(xT));
     };
+    if (x_nchw) {  // f3: x read once, xT written by the same blocks
+      if (spt == 1) go(offset_conv_fwd_mfma_bf16_row<1, true>);
+      else if (spt == 2) go(offset_conv_fwd_mfma_bf16_row<2, true>);
+      else if (spt == 3) go(offset_conv_fwd_mfma_bf16_row<3, true>);
+      else go(offset_conv_fwd_mfma_bf16_row<4, true>);
+      return hipGetLastError();
+    }
     if (spt == 1) go(offset_conv_fwd_mfma_bf16_row<1>);
     else if (spt == 2) go(offset_conv_fwd_mfma_bf16_row<2>);
     else if (spt == 3) go(offset_conv_fwd_mfma_bf16_row<3>);

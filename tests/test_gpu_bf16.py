@@ -254,3 +254,27 @@ def test_bf16_backward_with_attached_comm_single_rank(gpu_handle):
     for name in ref[2]:
         np.testing.assert_array_equal(got[2][name], ref[2][name], err_msg=name)
 
+
+
+@pytest.mark.parametrize("C,H,W", [(256, 28, 28), (64, 20, 20), (192, 13, 16)])
+def test_bf16_offset_conv_fold_vs_separate_transpose(gpu_handle, C, H, W):
+    """f3: where it applies the bf16 offset conv stages its windows from the
+    NCHW x and writes the channels-last xT itself (no transpose launch). Against the
+    separate-transpose schedule (dcn_debug_force_generic also turns the fold off; both runs
+    unfused, so their columns and GEMMs are the same): offsets and out bit for bit, which
+    needs every xT element right, and the forward against the oracle."""
+    bits, v, s = _case(71 + C, B=2, C=C, O_=64, H=H, W=W, off_scale=1.5)
+    gpu_handle.set_fwd_path(rt.DCN_FWD_UNFUSED)
+    try:
+        out_a, off_a, _ = _device(gpu_handle, bits, s)
+        rt.check(gpu_handle.lib.dcn_debug_force_generic(1))
+        try:
+            out_b, off_b, _ = _device(gpu_handle, bits, s)
+        finally:
+            rt.check(gpu_handle.lib.dcn_debug_force_generic(0))
+    finally:
+        gpu_handle.set_fwd_path(rt.DCN_FWD_AUTO)
+    np.testing.assert_array_equal(off_a.view(np.uint32), off_b.view(np.uint32))
+    np.testing.assert_array_equal(out_a.view(np.uint32), out_b.view(np.uint32))
+    ro, _, _ = O.forward(v["x"], v["w_off"], v["b_off"], v["w"], v["b"], s, (1, 1), offsets=off_a)
+    assert_bf16_close(out_a, ro, "out (fold)")
