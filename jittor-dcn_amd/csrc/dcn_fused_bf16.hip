@@ -105,7 +105,6 @@ __device__ __forceinline__ bf16x8_t as_frag(uint4 u) { return __builtin_bit_cast
 // scratch memory)
 __device__ __forceinline__ bf16x8_t as_frag(v4u u) { return __builtin_bit_cast(bf16x8_t, u); }
 __device__ __forceinline__ v4u as_v(uint4 u) { return __builtin_bit_cast(v4u, u); }
-__device__ __forceinline__ uint4 as_u(v4u u) { return __builtin_bit_cast(uint4, u); }
 __device__ __forceinline__ v4u ld16v_if(const bf16_t* p, bool ok) {
   return ok ? *reinterpret_cast<const v4u*>(p) : v4u{0u, 0u, 0u, 0u};
 }
@@ -388,7 +387,6 @@ constexpr int kDSl = 128;                     // pixel slots per tile, padded to
 constexpr int kDRow = kDSl * 2 + 16;          // bytes per [tap][channel] row of the col tile
 constexpr int kDT = 512;
 constexpr int kDOB = 2;
-constexpr int kDPairs = (kSlots / 2) * kMaxN * 2;  // (slot pair, tap, 8-channel group)
 constexpr int kDLWin = 0;
 constexpr int kDLCol = kDLWin + 2 * kDWPix * kDWPitch;
 constexpr int kDLRecW = kDLCol + 2 * kMaxN * kDC * kDRow;
