@@ -278,3 +278,20 @@ def test_bf16_offset_conv_fold_vs_separate_transpose(gpu_handle, C, H, W):
     np.testing.assert_array_equal(out_a.view(np.uint32), out_b.view(np.uint32))
     ro, _, _ = O.forward(v["x"], v["w_off"], v["b_off"], v["w"], v["b"], s, (1, 1), offsets=off_a)
     assert_bf16_close(out_a, ro, "out (fold)")
+
+
+def test_bf16_fused_forward_with_attached_comm_single_rank(gpu_handle):
+    """The config-4 data-parallel step on one rank: DCN_FWD_AUTO's fused bf16 forward (C=256,
+    its columns stored for the backward) with the RCCL communicator attached — the overlapped
+    gradient exchange must leave every tensor as the run without a communicator."""
+    import dcn_dp
+    bits, v, s = _case(43, B=4, C=256, O_=256, H=28, W=28)
+    ref = _device(gpu_handle, bits, s)
+    comm = dcn_dp.RcclComm(gpu_handle, 1, 0, dcn_dp.RcclComm.unique_id())
+    try:
+        got = _device(gpu_handle, bits, s, comm=comm)
+    finally:
+        comm.close()
+    np.testing.assert_array_equal(got[0], ref[0])
+    for name in ref[2]:
+        np.testing.assert_array_equal(got[2][name], ref[2][name], err_msg=name)
