@@ -330,7 +330,8 @@ int dcn_get_math(dcn_handle* h, int* math);
  * backward; DCN_FWD_FUSED_NOCOL never writes a column (forward-only callers: no_grad /
  * inference, deform_conv.py:56 under jt.no_grad); a DCN_BWD_COL_IN_WS backward on the
  * workspace of such a forward recomputes the columns. Both need C % 64 == 0, O % 256 == 0,
- * deform_groups 1, kh*kw <= 9; elsewhere they take the unfused schedule. Same columns bit
+ * deform_groups 1, kh*kw <= 9; elsewhere they take the unfused schedule. DCN_FWD_AUTO picks
+ * DCN_FWD_FUSED for DCN_BF16 when O == 256 (measured faster there). Same columns bit
  * for bit as K1; out to fp32 rounding of a different summation order before the bf16
  * rounding.
  * DCN_F32: DCN_FWD_FUSED (and _NOCOL, which for fp32 still writes the columns) runs the

@@ -664,10 +664,11 @@ bool fused_fwd_bf16_ok(const Geo& g) {
          g.Ho >= 2 && g.Wo >= 2 && (long)g.O * g.K < lim && (long)g.HW * g.K < (1l << 31);
 }
 
-// r03 at config 4 (C = O = 256, 28x28): the fused forward with its column stores 0.150 ms
-// against K1 0.069 + hipBLASLt 0.082 + bias 0.017 ms (step 0.686-0.701 vs 0.695-0.703 ms,
-// DESIGN.md §4.7); measured only with 256 input channels
-bool fused_fwd_bf16_pays(const Geo& g) { return g.C >= 256; }
+// r03 (tools/r03_fb_geo.py, fwd+bwd per step): fused faster wherever all
+// output channels are one 256-channel tile — C = 64 / 128 / 192 / 256 at 28x28 (6-9 %), C = 256
+// at 56x56 (6 %) — and slower with two tiles (O = 512, B = 16: 0.40 vs 0.37 ms), whose
+// workgroups each repeat the gather
+bool fused_fwd_bf16_pays(const Geo& g) { return g.O == kOT; }
 
 size_t fused_fwd_bf16_wfr_elems(const Geo& g) { return (size_t)g.O * g.K; }
 
