@@ -237,6 +237,117 @@ def load_fused_traffic(bf16_cfg4_glob="r*_pmc_hbm_config4.json"):
     return None, None
 
 
+class Workload:
+    """One BASELINE configuration's replicated parameters and packed gradient buffer on
+    `dev` (synthetic, SURVEY §8(d): offset conv σ = 1/sqrt(C·9) so Δ ~ N(0,1) px; the same
+    seed on every rank)."""
+
+    def __init__(self, cfg, rt, torch, dev, dcn_dp, seed=1234):
+        self.cfg = cfg
+        self.C, self.O, self.H, self.W = cfg["C"], cfg["O"], cfg["H"], cfg["W"]
+        self.k, self.s, self.p = cfg["k"], cfg["s"], cfg["p"]
+        self.dil, self.G = cfg.get("dil", 1), cfg.get("G", 1)
+        self.fwd_only = cfg.get("fwd_only", False)
+        self.bf16 = cfg["dtype"] == "bf16"
+        self.tdt = torch.bfloat16 if self.bf16 else torch.float32
+        self.N = self.k * self.k
+        self.J = 2 * self.N * self.G
+        self._rt = rt
+        C, O_, k, N, J, tdt = self.C, self.O, self.k, self.N, self.J, self.tdt
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed)
+        self.w_off = (torch.randn(J, C, k, k, device=dev, generator=g)
+                      / float(np.sqrt(C * N))).to(tdt)
+        self.b_off = (torch.rand(J, device=dev, generator=g) - 0.5).to(tdt)
+        self.w = (torch.randn(O_, C, k, k, device=dev, generator=g)
+                  * float(np.sqrt(2.0 / (C * N)))).to(tdt)
+        self.b = (torch.randn(O_, device=dev, generator=g) * 0.1).to(tdt)
+        # all parameter grads packed in ONE buffer -> one all-reduce per step (dcn_dp)
+        self.gbuf = dcn_dp.GradBuffer(dcn_dp.param_shapes(C, O_, k, k, deform_groups=self.G),
+                                      lambda n: torch.empty(n, device=dev, dtype=tdt))
+        self.gflat = self.gbuf.flat
+        self.grads = tuple(self.gbuf[n] for n in dcn_dp.PARAM_ORDER)
+        # ∂W and ∂b lead the packed buffer (dcn_dp.PARAM_ORDER)
+        self.n_dw = self.grads[0].numel() + self.grads[1].numel()
+
+    def desc(self, nb):
+        rt = self._rt
+        return rt.make_desc(nb, self.C, self.H, self.W, self.O, (self.k, self.k),
+                            (self.s, self.s), (self.p, self.p), (self.dil, self.dil), self.G,
+                            dtype=rt.DCN_BF16 if self.bf16 else rt.DCN_F32)
+
+
+def fused_roofline(kernel_ms, B, Ho, Wo, N, C, O_):
+    """The bf16 fused forward (gather + MFMA GEMM + bias, DCN_K_GEMM_FWD scope) against the
+    dense bf16 MFMA peak, with its PMC traffic from the newest committed config-4 summary."""
+    fl = 2.0 * B * Ho * Wo * N * C * O_
+    ms = kernel_ms["gemm_fwd"]
+    tr, tr_src = load_fused_traffic()
+    return {
+        "kernel": "dcn::fwd_fused_bf16 (f2: bilinear gather into bf16 MFMA + bias, "
+                  "columns stored for the backward)",
+        "bound": "mfma",
+        "achieved": round(fl / (ms * 1e-3) / 1e12, 1),
+        "peak": 2500.0,
+        "unit": "TFLOP/s",
+        "frac": round(fl / (ms * 1e-3) / 1e12 / 2500.0, 4),
+        "traffic": tr,
+        "traffic_source": tr_src,
+        "algorithmic_flop": fl,
+        "avg_launch_ms": ms,
+        "note": "HIP events around the launch (wf_to_frag16 swizzle included)",
+    }
+
+
+def config4_leg(args, world, rank, wl, rt, make_step, timed, kernel_times, fwd_path_split,
+                sync):
+    """BASELINE config 4 per GPU (bf16, 64 images, C=O=256, 28x28, fwd+bwd; at N > 1 with
+    the gradient all-reduce) timed like `value`; returns the `config4` object of the line.
+    `wl` is the config-4 Workload; `sync()` synchronises the device."""
+    cfg = wl.cfg
+    B = cfg["B"]
+    step, bufs = make_step(wl, B, 3000 + rank)
+    for _ in range(args.warmup):
+        step()
+    sync()
+    el = timed(step, args.steps)
+    km = kernel_times(step, args.steps)
+    Ho, Wo = rt.out_shape(wl.desc(B))
+    N, C, O_, J = wl.N, wl.C, wl.O, wl.J
+    paths = (fwd_path_split(step, args.warmup, args.steps)
+             if world == 1 and args.fwd_path == 0 else None)
+    res = {
+        "workload": f"config4: B={B}/GPU C={C}->O={O_} {cfg['H']}x{cfg['W']} k{cfg['k']} "
+                    f"s{cfg['s']} p{cfg['p']} bf16 DeformConv2d fwd+bwd"
+                    + (" + grad all-reduce" if world > 1 or args.exchange else ""),
+        "dtype": "bf16",
+        "value": round(B * world * Ho * Wo * N * args.steps / el / 1e9, 5),
+        "unit": "Gsamples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 4),
+        "scaling": "weak",
+        "global_batch": B * world,
+        "kernel_ms": km,
+        "fwd_paths_ms_per_step": paths,
+        "rooflines_other": other_rooflines(km, B, C, O_, cfg["H"], cfg["W"], N, Ho, Wo, J, True,
+                                           False),
+    }
+    if km.get("gemm_fwd") and not km.get("im2col"):
+        res["roofline"] = fused_roofline(km, B, Ho, Wo, N, C, O_)
+    else:  # the unfused schedule ran (K1 bf16 is the forward's HBM kernel)
+        k1_ms = km.get("im2col")
+        k1_b = k1_bytes(B, C, cfg["H"], cfg["W"], N, Ho, Wo, elem=2, J=J)
+        ach = k1_b / (k1_ms * 1e-3) / 1e9 if k1_ms else None
+        res["roofline"] = {"kernel": "dcn::im2col_lds_b8 (K1 bf16)", "bound": "hbm",
+                           "achieved": round(ach, 1) if ach else None, "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
+                           "algorithmic_bytes": k1_b, "avg_launch_ms": k1_ms}
+    del step, bufs
+    return res
+
+
 MATH_NAMES = {0: "f32 MFMA (rocBLAS/hipBLASLt)", 3: "f32 via split-bf16 X3 (2 planes, opt-in)",
               6: "f32 via exact-split bf16 X6", 9: "f32 via exact-split bf16 X9"}
 
@@ -277,6 +388,9 @@ def main():
     ap.add_argument("--no-strong", action="store_true",
                     help="skip the secondary fixed-global-batch (512) measurement that "
                          "multi-GPU weak runs of configs 3 and 4 add under strong_scaling")
+    ap.add_argument("--no-config4", action="store_true",
+                    help="skip the BASELINE config-4 leg (bf16, 64 images per GPU, 28x28) that "
+                         "the default config-3 run times beside the headline under `config4`")
     ap.add_argument("--exchange", action="store_true",
                     help="run the gradient exchange even at N=1 (a 1-rank RCCL group), to "
                          "exercise the overlapped all-reduce path on one GPU")
@@ -321,29 +435,12 @@ def main():
     if strong:  # fixed global batch split over the ranks (SURVEY §8(e) strong scaling)
         B = shard_sizes(args.global_batch, world)[rank]
     bf16 = cfg["dtype"] == "bf16"
-    tdt = torch.bfloat16 if bf16 else torch.float32
     N = k * k
     dil, G = cfg.get("dil", 1), cfg.get("G", 1)
     fwd_only = cfg.get("fwd_only", False)
-    mk_desc = lambda nb: rt.make_desc(nb, C, H, W, O_, (k, k), (s, s), (p, p), (dil, dil), G,
-                                      dtype=rt.DCN_BF16 if bf16 else rt.DCN_F32)
-    desc = mk_desc(B)
-    Ho, Wo = rt.out_shape(desc)
+    wl_main = Workload(cfg, rt, torch, dev, dcn_dp)
+    Ho, Wo = rt.out_shape(wl_main.desc(B))
     J = 2 * N * G
-
-    # synthetic inputs: x ~ N(0,1); offset conv σ = 1/sqrt(C·9) so Δ ~ N(0,1) px;
-    # replicated parameters (same seed on every rank), per-rank batch shard
-    g = torch.Generator(device=dev)
-    g.manual_seed(1234)
-    w_off = (torch.randn(J, C, k, k, device=dev, generator=g) / float(np.sqrt(C * N))).to(tdt)
-    b_off = (torch.rand(J, device=dev, generator=g) - 0.5).to(tdt)
-    w = (torch.randn(O_, C, k, k, device=dev, generator=g) * float(np.sqrt(2.0 / (C * N)))).to(tdt)
-    b = (torch.randn(O_, device=dev, generator=g) * 0.1).to(tdt)
-    # all parameter grads packed in ONE buffer -> one all-reduce per step (dcn_dp)
-    gbuf = dcn_dp.GradBuffer(dcn_dp.param_shapes(C, O_, k, k, deform_groups=G),
-                             lambda n: torch.empty(n, device=dev, dtype=tdt))
-    gflat = gbuf.flat
-    gw, gb, gwo, gbo = (gbuf[n] for n in dcn_dp.PARAM_ORDER)
 
     h = rt.Handle(local_rank)
     stream = torch.cuda.current_stream(dev)
@@ -354,7 +451,6 @@ def main():
     P = lambda t: t.data_ptr()
     comm = None
     gs = None
-    n_dw = gw.numel() + gb.numel()  # ∂W and ∂b lead the packed buffer (dcn_dp.PARAM_ORDER)
     if exch and args.comm == "libdcn":
         # libdcn's own communicator attached to the handle: dcn_backward returns summed
         # gradients, the ∂W/∂b part overlapped with ∂col/col2im/offset-conv backward, the
@@ -377,35 +473,73 @@ def main():
             dcn_dp.allreduce_torch(t32)
             t.copy_(t32)
 
-    def make_step(nb, seed):
-        """One DeformConv2d fwd + bwd (+ the gradient exchange) over a resident shard of
-        nb images; returns the step and the buffers it keeps alive."""
-        d = mk_desc(nb)
+    def make_step(wl, nb, seed):
+        """One DeformConv2d fwd + bwd (+ the gradient exchange) of workload `wl` over a
+        resident shard of nb images; returns the step and the buffers it keeps alive."""
+        d = wl.desc(nb)
+        Ho_, Wo_ = rt.out_shape(d)
+        tdt_ = wl.tdt
         gen = torch.Generator(device=dev)
         gen.manual_seed(seed)
-        x = torch.randn(nb, C, H, W, device=dev, generator=gen).to(tdt)
-        gout = torch.randn(nb, O_, Ho, Wo, device=dev, generator=gen).to(tdt)
-        out = torch.empty(nb, O_, Ho, Wo, device=dev, dtype=tdt)
-        off = torch.empty(nb, J, Ho, Wo, device=dev, dtype=tdt)
+        x = torch.randn(nb, wl.C, wl.H, wl.W, device=dev, generator=gen).to(tdt_)
+        gout = torch.randn(nb, wl.O, Ho_, Wo_, device=dev, generator=gen).to(tdt_)
+        out = torch.empty(nb, wl.O, Ho_, Wo_, device=dev, dtype=tdt_)
+        off = torch.empty(nb, wl.J, Ho_, Wo_, device=dev, dtype=tdt_)
         gx = torch.empty_like(x)
         goff = torch.empty_like(off)
         wsb = rt.workspace_bytes(d, True)
         ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        gw, gb, gwo, gbo = wl.grads
 
         def step():
-            rt.check(L.dcn_forward(h.h, d, P(x), P(w_off), P(b_off), P(w), P(b), P(out), P(off),
-                                   P(ws), wsb), "dcn_forward")
-            if fwd_only:
+            rt.check(L.dcn_forward(h.h, d, P(x), P(wl.w_off), P(wl.b_off), P(wl.w), P(wl.b),
+                                   P(out), P(off), P(ws), wsb), "dcn_forward")
+            if wl.fwd_only:
                 return
-            rt.check(L.dcn_backward(h.h, d, P(x), P(off), P(w_off), P(w), P(gout), P(gx), P(gw),
-                                    P(gb), P(gwo), P(gbo), P(goff), P(ws), wsb,
+            rt.check(L.dcn_backward(h.h, d, P(x), P(off), P(wl.w_off), P(wl.w), P(gout), P(gx),
+                                    P(gw), P(gb), P(gwo), P(gbo), P(goff), P(ws), wsb,
                                     rt.DCN_BWD_COL_IN_WS), "dcn_backward")
             if gs is not None:
                 with torch.cuda.stream(gs):
-                    reduce_fp32(gflat[:n_dw])  # starts once ∂W/∂b are final (dcn_set_grad_stream)
-                reduce_fp32(gflat[n_dw:])      # ∂W_off/∂b_off after the whole backward
+                    # starts once ∂W/∂b are final (dcn_set_grad_stream)
+                    reduce_fp32(wl.gflat[:wl.n_dw])
+                reduce_fp32(wl.gflat[wl.n_dw:])  # ∂W_off/∂b_off after the whole backward
                 stream.wait_stream(gs)
         return step, (x, gout, out, off, gx, goff, ws)
+
+    def kernel_times(step, steps):
+        """Average HIP-event duration per libdcn kernel class: a separate pass of `steps`
+        steps with events around every launch on `stream` (outside any timed region)."""
+        h.prof_enable(steps)
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize(dev)
+        km = {}
+        for name in rt.KERNEL_IDS:
+            tot, cnt = h.prof_read(name)
+            if cnt:
+                km[name] = round(tot / cnt, 4)
+        h.prof_enable(0)
+        return km
+
+    def fwd_path_split(step, warmup, steps):
+        """DCN_BF16: the same step under each forward schedule (include/dcn.h dcn_fwd_path),
+        reported beside the headline, never as `value`."""
+        res = {}
+        for name, pth in (("unfused (K1 + hipBLASLt + bias)", 1),
+                          ("fused, columns stored (DCN_FWD_FUSED)", 2),
+                          ("fused, no column matrix (DCN_FWD_FUSED_NOCOL: recomputed dW)", 3)):
+            h.set_fwd_path(pth)
+            for _ in range(max(2, warmup)):
+                step()
+            torch.cuda.synchronize(dev)
+            tp = time.perf_counter()
+            for _ in range(steps):
+                step()
+            torch.cuda.synchronize(dev)
+            res[name] = round((time.perf_counter() - tp) / steps * 1e3, 4)
+        h.set_fwd_path(args.fwd_path)
+        return res
 
     def timed(run, steps):
         """Barrier + synchronize on both sides of exactly `steps` steps; max over ranks."""
@@ -425,7 +559,7 @@ def main():
             el_ = float(t.item())
         return el_
 
-    step, bufs = make_step(B, 1000 + rank)
+    step, bufs = make_step(wl_main, B, 1000 + rank)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -454,15 +588,7 @@ def main():
 
     # per-kernel durations: a second, separate pass of the same steps with HIP events
     # around every libdcn launch on `stream` (kept out of the timed region above)
-    h.prof_enable(args.steps)
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    kernel_ms = {}
-    for name in rt.KERNEL_IDS:
-        tot, cnt = h.prof_read(name)
-        if cnt:
-            kernel_ms[name] = round(tot / cnt, 4)
+    kernel_ms = kernel_times(step, args.steps)
     # the same step under another GEMM arithmetic (split-bf16 X6 by default), reported
     # beside the headline, never as `value`
     alt = None
@@ -496,21 +622,7 @@ def main():
     # timed like the alt arithmetic, reported beside the headline, never as `value`
     fwd_paths = None
     if world == 1 and bf16 and args.fwd_path == 0 and not args.graph and not fwd_only:
-        h.prof_enable(0)
-        fwd_paths = {}
-        for name, pth in (("unfused (K1 + hipBLASLt + bias)", 1),
-                          ("fused, columns stored (DCN_FWD_FUSED)", 2),
-                          ("fused, no column matrix (DCN_FWD_FUSED_NOCOL: recomputed dW)", 3)):
-            h.set_fwd_path(pth)
-            for _ in range(max(2, args.warmup)):
-                step()
-            torch.cuda.synchronize(dev)
-            tp = time.perf_counter()
-            for _ in range(args.steps):
-                step()
-            torch.cuda.synchronize(dev)
-            fwd_paths[name] = round((time.perf_counter() - tp) / args.steps * 1e3, 4)
-        h.set_fwd_path(0)
+        fwd_paths = fwd_path_split(step, args.warmup, args.steps)
     k1_ms = kernel_ms.get("im2col")
     k1_b = k1_bytes(B, C, H, W, N, Ho, Wo, elem=2 if bf16 else 4, J=J)
     k1_name = K1_KERNEL if (G == 1 and C % 4 == 0) else "dcn::im2col_cl"
@@ -529,7 +641,7 @@ def main():
         torch.cuda.synchronize(dev)
         torch.cuda.empty_cache()
         shards = shard_sizes(STRONG_GLOBAL_BATCH, world)
-        step2, bufs2 = make_step(shards[rank], 2000 + rank)
+        step2, bufs2 = make_step(wl_main, shards[rank], 2000 + rank)
         for _ in range(2):
             step2()
         st_steps = max(1, min(args.steps, 10))
@@ -542,6 +654,20 @@ def main():
             "note": "fixed global batch of 512 images split over the ranks, timed like value "
                     "(barrier + synchronize, max over ranks); `value` is the weak curve"}
         del step2, bufs2
+        torch.cuda.empty_cache()
+    # BASELINE config 4 (bf16, B = 64 per GPU, 28², the multi-GPU target's per-GPU shard)
+    # beside the fp32 headline in the default run: same steps / warmup, same timed() (barrier
+    # + synchronize, max over ranks; at N > 1 with the gradient all-reduce on every rank).
+    # Reported under `config4`, never as `value`.
+    cfg4_res = None
+    if args.config == 3 and not strong and not args.no_config4 and not args.graph:
+        h.prof_enable(0)
+        torch.cuda.synchronize(dev)
+        torch.cuda.empty_cache()
+        wl4 = Workload(CONFIGS[4], rt, torch, dev, dcn_dp, seed=4321)
+        cfg4_res = config4_leg(args, world, rank, wl4, rt, make_step, timed, kernel_times,
+                               fwd_path_split, lambda: torch.cuda.synchronize(dev))
+        del wl4
         torch.cuda.empty_cache()
     if rank == 0:
         achieved = k1_b / (k1_ms * 1e-3) / 1e9 if k1_ms else None
@@ -594,29 +720,14 @@ def main():
             "alt": alt,
             "fwd_paths_ms_per_step": fwd_paths,
             "strong_scaling": strong_res,
+            "config4": cfg4_res,
             "cpu_baseline": None,
             "cpu_baseline_other": None,
         }
         if bf16 and not k1_ms and kernel_ms.get("gemm_fwd"):
             # DCN_FWD_AUTO ran the fused forward: K1 does not exist as a
             # launch; the dominant forward kernel is the fused one (gather + GEMM + bias)
-            fl = 2.0 * B * Ho * Wo * N * C * O_
-            ms = kernel_ms["gemm_fwd"]
-            tr, tr_src = load_fused_traffic()
-            res["roofline"] = {
-                "kernel": "dcn::fwd_fused_bf16 (f2: bilinear gather into bf16 MFMA + bias, "
-                          "columns stored for the backward)",
-                "bound": "mfma",
-                "achieved": round(fl / (ms * 1e-3) / 1e12, 1),
-                "peak": 2500.0,
-                "unit": "TFLOP/s",
-                "frac": round(fl / (ms * 1e-3) / 1e12 / 2500.0, 4),
-                "traffic": tr,
-                "traffic_source": tr_src,
-                "algorithmic_flop": fl,
-                "avg_launch_ms": ms,
-                "note": "HIP events around the launch (wf_to_frag16 swizzle included)",
-            }
+            res["roofline"] = fused_roofline(kernel_ms, B, Ho, Wo, N, C, O_)
         if world == 1 and not bf16 and not args.no_host_path:
             res["host_path"] = host_path_rate(cfg, args.config)
         if world == 1 and not args.no_cpu_baseline:

@@ -36,8 +36,10 @@
 extern "C" {
 #endif
 
-#define DCN_ABI_VERSION 4 /* 2: dcn_allreduce_grads takes a dtype; dcn_set_comm, dcn_set_grad_stream;
-                             3: dcn_backward_host_ex; 4: dcn_host_state, dcn_host_alloc */
+#define DCN_ABI_VERSION 5 /* 2: dcn_allreduce_grads takes a dtype; dcn_set_comm, dcn_set_grad_stream;
+                             3: dcn_backward_host_ex; 4: dcn_host_state, dcn_host_alloc;
+                             5: dcn_forward_ex (DCN_FWD_NO_COLUMNS), dcn_get_fwd_path,
+                                dcn_workspace_bytes(DCN_WS_FORWARD_NO_COLUMNS) */
 
 typedef enum {
   DCN_OK = 0,
@@ -104,7 +106,12 @@ int dcn_memset_zero(dcn_handle* h, void* dst, size_t bytes);
 /* Output size, deform_conv.py:34-35 (dilation-aware for the extension). */
 int dcn_out_shape(const dcn_desc* d, int* Ho, int* Wo);
 /* Device workspace needed by dcn_forward (with_backward=0) or by the pair
- * dcn_forward + dcn_backward sharing one workspace (with_backward=1). */
+ * dcn_forward + dcn_backward sharing one workspace (with_backward=1).
+ * with_backward=DCN_WS_FORWARD_NO_COLUMNS (2): a forward that writes no columns
+ * (dcn_forward_ex with DCN_FWD_NO_COLUMNS, or DCN_FWD_FUSED_NOCOL) needs no column region
+ * where that applies (DCN_BF16 geometries of the fused forward: 231 MB less at config 4);
+ * elsewhere the same as 0. */
+#define DCN_WS_FORWARD_NO_COLUMNS 2
 int dcn_workspace_bytes(const dcn_desc* d, int with_backward, size_t* bytes);
 
 /* ---- hot-path kernels (device pointers, stream-ordered) -------------------- */
@@ -139,8 +146,21 @@ int dcn_forward(dcn_handle* h, const dcn_desc* d, const float* x,
                 const float* w_off, const float* b_off, const float* w,
                 const float* b, float* out, float* off, void* ws,
                 size_t ws_bytes);
+/* dcn_forward with per-call flags (ABI 5). DCN_FWD_NO_COLUMNS: no backward will read this
+ * forward's columns (inference, jt.no_grad: deform_conv.py:56 under train.py:430), so a
+ * DCN_BF16 fused geometry writes none, whatever path the handle is set to; the handle's
+ * state is not touched (thread-safe with respect to other callers' paths). ws may then be
+ * sized by dcn_workspace_bytes(d, DCN_WS_FORWARD_NO_COLUMNS). fp32, and bf16 geometries
+ * outside the fused forward, write their columns as usual. flags = 0 is dcn_forward. */
+#define DCN_FWD_NO_COLUMNS 1
+int dcn_forward_ex(dcn_handle* h, const dcn_desc* d, const float* x,
+                   const float* w_off, const float* b_off, const float* w,
+                   const float* b, float* out, float* off, void* ws,
+                   size_t ws_bytes, int flags);
 
-#define DCN_BWD_COL_IN_WS 1 /* ws still holds forward's columns */
+#define DCN_BWD_COL_IN_WS 1 /* ws still holds forward's columns. The library remembers,
+                              per workspace, a DCN_BF16 forward that wrote none (NO_COLUMNS /
+                              FUSED_NOCOL): a backward on that workspace recomputes them. */
 
 /* Autodiff of DeformConv2d.execute as triggered by optimizer.backward
  * (train.py:414). Overwrites grad_x, grad_w, grad_b (if has_bias),
@@ -327,11 +347,12 @@ int dcn_get_math(dcn_handle* h, int* math);
  * DCN_BF16 (dcn_fused_bf16.hip): DCN_FWD_FUSED gathers the bilinear samples from an LDS
  * window of the channels-last x straight into the B operand of bf16 MFMAs (bias and the
  * bf16 rounding in the epilogue) and still writes the columns for a DCN_BWD_COL_IN_WS
- * backward; DCN_FWD_FUSED_NOCOL never writes a column (forward-only callers: no_grad /
- * inference, deform_conv.py:56 under jt.no_grad); a DCN_BWD_COL_IN_WS backward on the
- * workspace of such a forward recomputes the columns. Both need C % 64 == 0, O % 256 == 0,
- * deform_groups 1, kh*kw <= 9; elsewhere they take the unfused schedule. DCN_FWD_AUTO picks
- * DCN_FWD_FUSED for DCN_BF16 when O == 256 (measured faster there). Same columns bit
+ * backward; DCN_FWD_FUSED_NOCOL never writes a column, and its backward recomputes
+ * the columns inside the ∂W MFMA kernel (no column matrix in the step); a DCN_BWD_COL_IN_WS
+ * backward on the workspace of a forward without columns recomputes them (tracked per
+ * workspace). Both need C % 64 == 0, O % 256 == 0, deform_groups 1, kh*kw <= 9; elsewhere
+ * they take the unfused schedule. DCN_FWD_AUTO picks DCN_FWD_FUSED for DCN_BF16 when O == 256
+ * and Ho*Wo >= 784 (measured faster there). Same columns bit
  * for bit as K1; out to fp32 rounding of a different summation order before the bf16
  * rounding.
  * DCN_F32: DCN_FWD_FUSED (and _NOCOL, which for fp32 still writes the columns) runs the
@@ -348,13 +369,7 @@ typedef enum {
   DCN_FWD_FUSED_NOCOL = 3
 } dcn_fwd_path;
 int dcn_set_fwd_path(dcn_handle* h, int path);
-
-/* ---- development A/B knobs ------------------------------------------------------ *
- * Env DCN_EXP="v0,v1,..." (read once per process) is the hook for speed experiments
- * during development: a candidate kernel is put behind exp_flag(i), A/B-measured against
- * the default, and then either made the default or deleted. No slot selects anything in
- * this build: every alternative measured slower was removed (DESIGN.md §4 keeps the
- * measurements), so the shipped path is the one the parity tests run. */
+int dcn_get_fwd_path(dcn_handle* h, int* path);
 
 /* ---- testing ------------------------------------------------------------------ */
 /* One fp32 GEMM through the handle's engine under its current math mode, BLAS

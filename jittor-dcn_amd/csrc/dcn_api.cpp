@@ -121,7 +121,9 @@ struct WsLayout {
   size_t total = 0;
 };
 
-WsLayout ws_layout(const Geo& g, bool bwd) {
+// cols = false: the forward-only layout of a forward that writes no columns (a
+// DCN_BF16 fused forward under DCN_FWD_NO_COLUMNS / DCN_FWD_FUSED_NOCOL): no `col` region
+WsLayout ws_layout(const Geo& g, bool bwd, bool cols = true) {
   WsLayout L;
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -132,7 +134,7 @@ WsLayout ws_layout(const Geo& g, bool bwd) {
   L.xT = take((size_t)g.B * g.HWi * g.C * sizeof(float));
   L.wt = take(dcn::offset_conv_wt_floats(g) * sizeof(float));
   L.part = take(dcn::offset_conv_fpart_floats(g) * sizeof(float));
-  L.col = take((size_t)g.B * g.HW * g.K * sizeof(float));
+  L.col = take(cols ? (size_t)g.B * g.HW * g.K * sizeof(float) : 0);
   const size_t f = sizeof(float);
   if (g.dt == DCN_BF16) {
     // DCN_BF16 forward copies, at the same offsets in the forward-only and the
@@ -190,9 +192,11 @@ struct dcn_handle {
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   dcn::GemmEngine* gemm = nullptr;
   int fwd_path = DCN_FWD_AUTO;  // dcn_set_fwd_path
-  // workspace of the last DCN_BF16 forward that left no columns in it (DCN_FWD_FUSED_NOCOL):
-  // a DCN_BWD_COL_IN_WS backward on it recomputes them instead of reading stale ones
-  const void* nocol_ws = nullptr;
+  // workspaces whose last DCN_BF16 forward left no columns in them (DCN_FWD_FUSED_NOCOL or
+  // DCN_FWD_NO_COLUMNS): a DCN_BWD_COL_IN_WS backward on one of them recomputes the columns
+  // instead of reading whatever its col region holds. One entry per workspace (any number of
+  // modules may share the handle); a forward that writes columns into a workspace drops it.
+  std::vector<const void*> nocol_ws;
   // data-parallel gradient exchange (dcn_set_comm / dcn_set_grad_stream): the ∂W/∂b
   // all-reduce runs on comm_stream as soon as they are final (dw_main / dw_aux), beside the
   // rest of the backward; the stream waits for comm_done before anything later
@@ -243,24 +247,6 @@ namespace {
 void state_free(dcn_host_state* s);
 }  // namespace
 
-namespace dcn {
-int exp_flag(int i) {
-  static int v[16] = {0};
-  static bool init = false;
-  if (!init) {
-    init = true;
-    if (const char* e = std::getenv("DCN_EXP")) {
-      for (int k = 0; k < 16 && *e; ++k) {
-        v[k] = std::atoi(e);
-        while (*e && *e != ',') ++e;
-        if (*e == ',') ++e;
-      }
-    }
-  }
-  return (i >= 0 && i < 16) ? v[i] : 0;
-}
-}  // namespace dcn
-
 namespace {
 
 struct ProfScope {
@@ -285,6 +271,21 @@ int set_device(dcn_handle* h) {
   if (!h) return fail(DCN_ERR_INVALID, "null handle");
   HIP_TRY(hipSetDevice(h->device));
   return DCN_OK;
+}
+
+bool ws_is_nocol(const dcn_handle* h, const void* ws) {
+  return std::find(h->nocol_ws.begin(), h->nocol_ws.end(), ws) != h->nocol_ws.end();
+}
+void ws_mark_nocol(dcn_handle* h, const void* ws, bool nocol) {
+  auto it = std::find(h->nocol_ws.begin(), h->nocol_ws.end(), ws);
+  if (nocol && it == h->nocol_ws.end()) h->nocol_ws.push_back(ws);
+  if (!nocol && it != h->nocol_ws.end()) h->nocol_ws.erase(it);
+}
+
+// Does a DCN_BF16 forward under this path / these flags skip the columns?
+bool fwd_skips_columns(const dcn_handle* h, const Geo& g, int flags) {
+  return g.dt == DCN_BF16 && dcn::fused_fwd_bf16_ok(g) && !dcn::get_force_generic() &&
+         (h->fwd_path == DCN_FWD_FUSED_NOCOL || (flags & DCN_FWD_NO_COLUMNS) != 0);
 }
 
 // ---- forward / backward cores ---------------------------------------------------
@@ -531,7 +532,7 @@ using dcn::bf16_t;
 
 int forward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x,
                  const bf16_t* w_off, const bf16_t* b_off, const bf16_t* w, const bf16_t* b,
-                 bf16_t* out, bf16_t* off, char* base, const WsLayout& L) {
+                 bf16_t* out, bf16_t* off, char* base, const WsLayout& L, bool nocol) {
   hipStream_t st = h->stream;
   bf16_t* xT = BF(L.xT);  // channels-last bf16 x: K1, K5 and the offset conv read it
   float *off32 = F32(L.off32), *out32 = F32(L.out32);
@@ -568,8 +569,8 @@ int forward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x,
     }
   }
   const bool fused_ok = dcn::fused_fwd_bf16_ok(g) && !dcn::get_force_generic();
-  const bool nocol = fused_ok && h->fwd_path == DCN_FWD_FUSED_NOCOL;
-  h->nocol_ws = nocol ? base : (h->nocol_ws == base ? nullptr : h->nocol_ws);
+  // this workspace holds this forward's columns unless it runs without them
+  ws_mark_nocol(h, base, nocol);
   if (fused_ok && (h->fwd_path == DCN_FWD_FUSED || nocol ||
                    (h->fwd_path == DCN_FWD_AUTO && dcn::fused_fwd_bf16_pays(g)))) {
     // f2: the bilinear gather feeds the bf16 MFMAs straight from an LDS window of xT; bias
@@ -918,7 +919,13 @@ int dcn_workspace_bytes(const dcn_desc* d, int with_backward, size_t* bytes) {
   if (!bytes) return fail(DCN_ERR_INVALID, "null out pointer");
   Geo g;
   DCN_TRY(make_geo(d, &g));
-  *bytes = ws_layout(g, with_backward != 0).total;
+  if (with_backward < 0 || with_backward > DCN_WS_FORWARD_NO_COLUMNS)
+    return fail(DCN_ERR_INVALID, "dcn_workspace_bytes: with_backward must be 0, 1 or 2");
+  // DCN_WS_FORWARD_NO_COLUMNS: no col region where the forward skips the columns (DCN_BF16
+  // fused geometries); elsewhere the forward writes them and needs the forward layout
+  const bool cols = !(with_backward == DCN_WS_FORWARD_NO_COLUMNS && g.dt == DCN_BF16 &&
+                      dcn::fused_fwd_bf16_ok(g));
+  *bytes = ws_layout(g, with_backward == 1, cols).total;
   return DCN_OK;
 }
 
@@ -994,10 +1001,18 @@ int dcn_col2im_coord_bwd(dcn_handle* h, const dcn_desc* d, const float* x, const
 int dcn_forward(dcn_handle* h, const dcn_desc* d, const float* x, const float* w_off,
                 const float* b_off, const float* w, const float* b, float* out, float* off,
                 void* ws, size_t ws_bytes) {
+  return dcn_forward_ex(h, d, x, w_off, b_off, w, b, out, off, ws, ws_bytes, 0);
+}
+
+int dcn_forward_ex(dcn_handle* h, const dcn_desc* d, const float* x, const float* w_off,
+                   const float* b_off, const float* w, const float* b, float* out, float* off,
+                   void* ws, size_t ws_bytes, int flags) {
   Geo g;
   DCN_TRY(make_geo(d, &g));
   DCN_TRY(set_device(h));
-  const WsLayout L = ws_layout(g, false);
+  if (flags & ~DCN_FWD_NO_COLUMNS) return fail(DCN_ERR_INVALID, "dcn_forward_ex: unknown flags");
+  const bool nocol = fwd_skips_columns(h, g, flags);
+  const WsLayout L = ws_layout(g, false, !nocol);
   if (!ws || ws_bytes < L.total) return fail(DCN_ERR_WORKSPACE, "workspace too small for dcn_forward");
   if (d->has_bias && !b) return fail(DCN_ERR_INVALID, "has_bias set but bias is NULL");
   char* base = static_cast<char*>(ws);
@@ -1007,7 +1022,7 @@ int dcn_forward(dcn_handle* h, const dcn_desc* d, const float* x, const float* w
                         reinterpret_cast<const bf16_t*>(w_off),
                         reinterpret_cast<const bf16_t*>(b_off), reinterpret_cast<const bf16_t*>(w),
                         reinterpret_cast<const bf16_t*>(b), reinterpret_cast<bf16_t*>(out),
-                        reinterpret_cast<bf16_t*>(off), base, L);
+                        reinterpret_cast<bf16_t*>(off), base, L, nocol);
   }
   float* xT = reinterpret_cast<float*>(base + L.xT);
   if (dcn::offset_fwd_mfma_xt_ok(g)) {
@@ -1053,7 +1068,7 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
     auto C = [](const float* p) { return reinterpret_cast<const bf16_t*>(p); };
     auto M = [](float* p) { return reinterpret_cast<bf16_t*>(p); };
     // a DCN_FWD_FUSED_NOCOL forward left no columns in this workspace: recompute them
-    const bool col_valid = (flags & DCN_BWD_COL_IN_WS) != 0 && h->nocol_ws != ws;
+    const bool col_valid = (flags & DCN_BWD_COL_IN_WS) != 0 && !ws_is_nocol(h, ws);
     return backward_bf16(h, g, d->has_bias != 0, C(x), C(off), C(w_off), C(w), C(grad_out),
                          M(grad_x), M(grad_w), M(grad_b), M(grad_w_off), M(grad_b_off),
                          M(grad_off_out), base, L, col_valid);
@@ -1734,6 +1749,12 @@ int dcn_set_fwd_path(dcn_handle* h, int path) {
       path != DCN_FWD_FUSED_NOCOL)
     return fail(DCN_ERR_INVALID, "dcn_set_fwd_path: unknown path " + std::to_string(path));
   h->fwd_path = path;
+  return DCN_OK;
+}
+
+int dcn_get_fwd_path(dcn_handle* h, int* path) {
+  if (!h || !path) return fail(DCN_ERR_INVALID, "dcn_get_fwd_path: null argument");
+  *path = h->fwd_path;
   return DCN_OK;
 }
 

@@ -25,6 +25,8 @@
 //   * Epilogue: bf16(acc + bias[o]) straight to NCHW out (launch_bias_to_bf16's rounding).
 #include <algorithm>
 #include <climits>
+#include <mutex>
+#include <vector>
 
 #include "dcn_device.h"
 
@@ -667,8 +669,9 @@ bool fused_fwd_bf16_ok(const Geo& g) {
 // r03 (tools/r03_fb_geo.py, fwd+bwd per step): fused faster wherever all
 // output channels are one 256-channel tile — C = 64 / 128 / 192 / 256 at 28x28 (6-9 %), C = 256
 // at 56x56 (6 %) — and slower with two tiles (O = 512, B = 16: 0.40 vs 0.37 ms), whose
-// workgroups each repeat the gather
-bool fused_fwd_bf16_pays(const Geo& g) { return g.O == kOT; }
+// workgroups each repeat the gather. Only the measured range takes it: output maps of at least
+// 28 x 28 pixels (small maps fill only part of each 7 x 16 tile and were not measured)
+bool fused_fwd_bf16_pays(const Geo& g) { return g.O == kOT && g.HW >= 28 * 28; }
 
 size_t fused_fwd_bf16_wfr_elems(const Geo& g) { return (size_t)g.O * g.K; }
 
@@ -701,12 +704,24 @@ int fused_dw_bf16_groups(const Geo& g) { return std::min(16, g.B); }
 hipError_t launch_fused_dw_bf16(const Geo& g, const bf16_t* xT, const float* off,
                                 const bf16_t* gout, float* parts, hipStream_t s) {
   if (!fused_dw_bf16_ok(g)) return hipErrorInvalidValue;
-  static bool attr = false;
-  if (!attr) {
-    attr = true;
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dw_fused_bf16<0>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, kDLds);
+  // the >64 KB dynamic-LDS attribute is per device: set once per device id, recorded only
+  // after it succeeded (a failure is returned and retried on the next call)
+  static std::mutex mu;
+  static std::vector<char> attr_set;
+  int dev = 0;
+  {
+    const hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
+  }
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if ((int)attr_set.size() <= dev) attr_set.resize(dev + 1, 0);
+    if (!attr_set[dev]) {
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dw_fused_bf16<0>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, kDLds);
+      if (e != hipSuccess) return e;
+      attr_set[dev] = 1;
+    }
   }
   const int ng = fused_dw_bf16_groups(g);
   const int tw_n = (g.Wo + kTW - 1) / kTW;

@@ -237,9 +237,6 @@ hipError_t launch_gemm_split(int math, const GemmSpec& s, const float* A, const 
 // Selection of the im2col / col2im implementation (tests force the generic
 // global-memory kernels to cross-check the channels-last ones).
 void set_force_generic(int on);
-// Development A/B knobs for speed experiments: DCN_EXP="a,b,..." (16 slots) -> exp_flag(i), 0 when
-// unset. Never changes results, only which of several equivalent kernels runs.
-int exp_flag(int i);
 int get_force_generic();
 
 }  // namespace dcn

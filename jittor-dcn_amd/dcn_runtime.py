@@ -15,10 +15,12 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DCN_LIB", os.path.join(HERE, "lib", "libdcn.so"))
 
-ABI_VERSION = 4  # include/dcn.h DCN_ABI_VERSION
+ABI_VERSION = 5  # include/dcn.h DCN_ABI_VERSION
 HOST_REUSE_FWD = 2  # include/dcn.h DCN_HOST_REUSE_FWD
 DCN_F32, DCN_BF16 = 0, 1
 DCN_BWD_COL_IN_WS = 1
+DCN_FWD_NO_COLUMNS = 1  # dcn_forward_ex flag
+DCN_WS_FORWARD_NO_COLUMNS = 2  # dcn_workspace_bytes(with_backward=2)
 DCN_FWD_AUTO, DCN_FWD_UNFUSED, DCN_FWD_FUSED, DCN_FWD_FUSED_NOCOL = 0, 1, 2, 3
 DCN_MATH_F32, DCN_MATH_F32_BF16X3, DCN_MATH_F32_BF16X6, DCN_MATH_F32_BF16X9 = 0, 3, 6, 9
 KERNEL_IDS = {
@@ -72,6 +74,7 @@ SIGNATURES = {
     "dcn_im2col_fwd": [_vp, _dp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int],
     "dcn_col2im_coord_bwd": [_vp, _dp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int],
     "dcn_forward": [_vp, _dp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz],
+    "dcn_forward_ex": [_vp, _dp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, ctypes.c_int],
     "dcn_backward": [_vp, _dp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz,
                      ctypes.c_int],
     "dcn_forward_host": [_vp, _dp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
@@ -97,6 +100,7 @@ SIGNATURES = {
     "dcn_set_math": [_vp, ctypes.c_int],
     "dcn_get_math": [_vp, _ip],
     "dcn_set_fwd_path": [_vp, ctypes.c_int],
+    "dcn_get_fwd_path": [_vp, _ip],
     "dcn_debug_fused_workgroups": [ctypes.c_int],
     "dcn_debug_gemm": [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                        _vp, ctypes.c_int, ctypes.c_long, _vp, ctypes.c_int, ctypes.c_long, _vp,
@@ -188,7 +192,8 @@ def out_shape(desc: Desc):
     return ho.value, wo.value
 
 
-def workspace_bytes(desc: Desc, with_backward: bool) -> int:
+def workspace_bytes(desc: Desc, with_backward) -> int:
+    """dcn_workspace_bytes: with_backward False / True, or DCN_WS_FORWARD_NO_COLUMNS (2)."""
     n = ctypes.c_size_t()
     check(load().dcn_workspace_bytes(ctypes.byref(desc), int(with_backward), ctypes.byref(n)),
           "dcn_workspace_bytes")
@@ -262,6 +267,11 @@ class Handle:
         """0 DCN_FWD_AUTO (measured-faster schedule), 1 DCN_FWD_UNFUSED, 2 DCN_FWD_FUSED,
         3 DCN_FWD_FUSED_NOCOL (DCN_BF16: no columns written)."""
         check(self.lib.dcn_set_fwd_path(self.h, int(path)), "dcn_set_fwd_path")
+
+    def get_fwd_path(self) -> int:
+        p = ctypes.c_int()
+        check(self.lib.dcn_get_fwd_path(self.h, ctypes.byref(p)), "dcn_get_fwd_path")
+        return p.value
 
     # --- data-parallel gradient exchange (include/dcn.h) ---------------------------
     def set_comm(self, comm):

@@ -6,8 +6,9 @@ conv, gauss-initialised weight) over GPU-resident torch tensors. Forward and bac
 are dcn_forward / dcn_backward on torch's current HIP stream, so there are no host
 copies. Each module keeps its workspace, so the backward reuses the forward's columns
 (DCN_BWD_COL_IN_WS); a bf16 forward that no backward will follow (torch.no_grad, or no
-input needing a gradient: the reference's jt.no_grad inference, train.py:430) runs
-DCN_FWD_FUSED_NOCOL, which never writes the column matrix. torch is only the tensor container
+input needing a gradient: the reference's jt.no_grad inference, train.py:430) calls
+dcn_forward_ex with DCN_FWD_NO_COLUMNS, which writes no column matrix and leaves the shared
+handle's forward path alone. torch is only the tensor container
 here: every kernel is libdcn's, and a missing libdcn.so or HIP device raises (no fallback).
 """
 from __future__ import annotations
@@ -69,15 +70,11 @@ class DeformConv2dFunction(torch.autograd.Function):
         wsb = rt.workspace_bytes(desc, True)
         buf = ws.get(wsb, x.device)
         P = lambda t: None if t is None else t.data_ptr()
-        nocol = nocol and x.dtype == torch.bfloat16
-        if nocol:  # forward-only: no columns for a backward
-            h.set_fwd_path(rt.DCN_FWD_FUSED_NOCOL)
-        try:
-            rt.check(h.lib.dcn_forward(h.h, desc, P(x), P(w_off), P(b_off), P(w), P(b), P(out),
-                                       P(off), P(buf), wsb), "dcn_forward")
-        finally:
-            if nocol:
-                h.set_fwd_path(rt.DCN_FWD_AUTO)
+        # forward-only (no backward will read the columns): a per-call flag,
+        # so the handle shared by every module on this device keeps the caller's path
+        flags = rt.DCN_FWD_NO_COLUMNS if nocol else 0
+        rt.check(h.lib.dcn_forward_ex(h.h, desc, P(x), P(w_off), P(b_off), P(w), P(b), P(out),
+                                      P(off), P(buf), wsb, flags), "dcn_forward_ex")
         ctx.save_for_backward(x, off, w_off, w)
         ctx.desc, ctx.ws, ctx.wsb, ctx.has_bias = desc, ws, wsb, b is not None
         ws.fwd_count += 1

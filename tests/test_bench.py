@@ -113,3 +113,54 @@ def test_dry_weak_scaling_shards_per_rank():
     rc, line, err = _run_bench("--gpus", "2", "--dry")
     assert rc == 0, err
     assert line["scaling"] == "weak" and line["shards"] == [64, 64]
+
+
+def test_config4_leg_is_wired(bench):
+    """The default config-3 run times BASELINE config 4 beside the headline (VERDICT r03 next
+    item 2): bf16, 64 images per GPU, C=O=256, 28x28, fwd+bwd, through the same timed() /
+    warmup / steps, reported under `config4` with its kernel times, the dominant kernel's
+    roofline (the fused forward against the bf16 MFMA peak when AUTO runs it, K1 bf16 against
+    HBM otherwise) and the forward-schedule split. Stubbed device: only the wiring runs."""
+    import argparse
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "jittor-dcn_amd"))
+    torch = pytest.importorskip("torch")
+    import dcn_dp
+    import dcn_runtime as rt
+    c4 = bench.CONFIGS[4]
+    assert (c4["B"], c4["C"], c4["O"], c4["H"], c4["W"], c4["k"], c4["dtype"]) == \
+        (64, 256, 256, 28, 28, 3, "bf16")
+    wl = bench.Workload(c4, rt, torch, torch.device("cpu"), dcn_dp, seed=4321)
+    assert wl.w.dtype == torch.bfloat16 and wl.desc(64).dtype == rt.DCN_BF16
+    calls = {}
+
+    def make_step(w, nb, seed):
+        calls["make_step"] = (w.cfg is c4, nb)
+        return (lambda: calls.__setitem__("steps", calls.get("steps", 0) + 1)), ()
+
+    def timed(step, steps):
+        calls["timed"] = steps
+        return 0.7e-3 * steps
+
+    for km, kind in (({"gemm_fwd": 0.14, "gemm_dw": 0.12, "gemm_dcol": 0.1, "col2im": 0.11},
+                      "mfma"),
+                     ({"im2col": 0.07, "gemm_fwd": 0.08, "gemm_dw": 0.12}, "hbm")):
+        args = argparse.Namespace(warmup=2, steps=5, fwd_path=0, exchange=False)
+        res = bench.config4_leg(args, 1, 0, wl, rt, make_step, timed, lambda s, n: km,
+                                lambda s, w, n: {"fused": 0.7}, lambda: None)
+        assert calls["make_step"] == (True, 64) and calls["timed"] == 5
+        assert res["dtype"] == "bf16" and res["unit"] == "Gsamples/s"
+        assert res["workload"].startswith("config4: B=64/GPU C=256->O=256 28x28 k3")
+        assert abs(res["ms_per_step"] - 0.7) < 1e-9
+        # 64·28·28·9 samples per 0.7 ms
+        assert abs(res["value"] - 64 * 28 * 28 * 9 / 0.7e-3 / 1e9) < 1e-4
+        assert res["kernel_ms"] is km and res["fwd_paths_ms_per_step"] == {"fused": 0.7}
+        assert res["roofline"]["bound"] == kind
+        for key in ("achieved", "peak", "unit", "frac"):
+            assert key in res["roofline"]
+    # at N > 1 the leg reports the whole job (every rank's 64 images), no schedule split
+    res = bench.config4_leg(argparse.Namespace(warmup=1, steps=2, fwd_path=0, exchange=False),
+                            8, 0, wl, rt, make_step, timed, lambda s, n: {"gemm_fwd": 0.14},
+                            lambda s, w, n: {"x": 1}, lambda: None)
+    assert res["n_gpus"] == 8 and res["global_batch"] == 512 and res["fwd_paths_ms_per_step"] is None
+    assert "all-reduce" in res["workload"]

@@ -33,6 +33,7 @@ torch = pytest.importorskip("torch")
 import torch.nn.functional as F  # noqa: E402
 
 import dcn_oracle as O  # noqa: E402
+import dcn_runtime as rt  # noqa: E402
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                 "examples"))
@@ -171,19 +172,25 @@ def test_torch_module_surface_and_bf16():
 
 def test_torch_bf16_no_grad_forward_writes_no_columns():
     """A bf16 forward under torch.no_grad (the reference's jt.no_grad inference,
-    train.py:430) runs DCN_FWD_FUSED_NOCOL: same output bits as the grad-enabled forward
-    (which DCN_FWD_AUTO runs fused with its columns stored at C >= 256), and the gradients of
-    a forward followed by a no-grad forward of the same module stay bit for bit: the no-grad
-    call advanced the workspace token, so the backward recomputes the columns."""
+    train.py:430) runs dcn_forward_ex(DCN_FWD_NO_COLUMNS): same output bits as the
+    grad-enabled forward (which DCN_FWD_AUTO runs fused with its columns stored when O is one
+    256-channel tile and the map has at least 28 x 28 pixels), the handle's forward path is
+    left as the caller set it, and the gradients of a forward followed by a no-grad forward of
+    the same module stay bit for bit: the no-grad call advanced the workspace token, so the
+    backward recomputes the columns."""
     import torch_dcn
     torch.manual_seed(3)
     m = torch_dcn.DeformConv2d(256, 256, 3, 1, 1).cuda().to(torch.bfloat16)
     with torch.no_grad():
         m.offset_conv.weight.normal_(0, 1.0 / 48)
         m.offset_conv.bias.uniform_(-0.5, 0.5)
-    x = torch.randn(2, 256, 14, 14, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(2, 256, 28, 28, device="cuda", dtype=torch.bfloat16)
+    h = torch_dcn._handle(x.device)
+    h.set_fwd_path(rt.DCN_FWD_FUSED)  # a path the caller chose: the no-grad call keeps it
     with torch.no_grad():
         y0 = m(x)
+    assert h.get_fwd_path() == rt.DCN_FWD_FUSED
+    h.set_fwd_path(rt.DCN_FWD_AUTO)
     xg = x.clone().requires_grad_(True)
     y1 = m(xg)
     assert torch.equal(y0.view(torch.int16), y1.detach().view(torch.int16))

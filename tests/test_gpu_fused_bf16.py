@@ -16,12 +16,14 @@ that reuses them (DCN_FWD_FUSED) or never (DCN_FWD_FUSED_NOCOL).
   area and, past its 48 entries, the in-line global corner reads;
 * config 4 at full size: forward twice in one process, bit for bit.
 """
+import ctypes
+
 import numpy as np
 import pytest
 
 import dcn_oracle as O
 import dcn_runtime as rt
-from test_gpu_bf16 import _case, _device, assert_bf16_close
+from test_gpu_bf16 import Buf, _case, _device, assert_bf16_close
 
 pytestmark = pytest.mark.gpu
 
@@ -127,3 +129,114 @@ def test_fused_bf16_nocol_config4_full_size(gpu_handle):
             _near(r1[2][k], ru[2][k], "config 4 nocol ∂W")
         else:
             np.testing.assert_array_equal(r1[2][k], ru[2][k], err_msg=f"config 4 nocol ∂{k}")
+
+
+def _upload_case(D, c):
+    bits, _, s = c
+    B, C, H, W = bits["x"].shape
+    O_, _, kh, kw = bits["w"].shape
+    J = bits["w_off"].shape[0]
+    desc = rt.make_desc(B, C, H, W, O_, (kh, kw), s, (1, 1), dtype=rt.DCN_BF16)
+    Ho, Wo = rt.out_shape(desc)
+    p = {k: D.up(v) for k, v in bits.items()}
+    p["out"], p["off"] = D.zeros(B * O_ * Ho * Wo * 2), D.zeros(B * J * Ho * Wo * 2)
+    p["g"] = {k: D.zeros(v.nbytes) for k, v in bits.items() if k != "grad_out"}
+    p["goff"] = D.zeros(B * J * Ho * Wo * 2)
+    return desc, (B, O_, Ho, Wo), p
+
+
+def _fwd(h, desc, p, ws, wsb, flags=0):
+    vp = ctypes.c_void_p
+    rt.check(h.lib.dcn_forward_ex(h.h, desc, vp(p["x"]), vp(p["w_off"]), vp(p["b_off"]),
+                                  vp(p["w"]), vp(p["b"]), vp(p["out"]), vp(p["off"]), vp(ws),
+                                  wsb, flags), "dcn_forward_ex")
+
+
+def _bwd(h, desc, p, ws, wsb):
+    vp = ctypes.c_void_p
+    g = p["g"]
+    rt.check(h.lib.dcn_backward(h.h, desc, vp(p["x"]), vp(p["off"]), vp(p["w_off"]), vp(p["w"]),
+                                vp(p["grad_out"]), vp(g["x"]), vp(g["w"]), vp(g["b"]),
+                                vp(g["w_off"]), vp(g["b_off"]), vp(p["goff"]), vp(ws), wsb,
+                                rt.DCN_BWD_COL_IN_WS), "dcn_backward")
+
+
+def _grads(D, c, p):
+    bits = c[0]
+    g = p["g"]
+    return {"x": D.down(g["x"], bits["x"].shape), "weight": D.down(g["w"], bits["w"].shape),
+            "bias": D.down(g["b"], bits["b"].shape),
+            "offset_conv.weight": D.down(g["w_off"], bits["w_off"].shape),
+            "offset_conv.bias": D.down(g["b_off"], bits["b_off"].shape)}
+
+
+@pytest.mark.parametrize("path", [rt.DCN_FWD_FUSED_NOCOL, rt.DCN_FWD_AUTO])
+def test_nocol_state_is_per_workspace(gpu_handle, path):
+    """Several modules on one handle (a stack: all forwards, then all backwards), each with its
+    own workspace, every backward with DCN_BWD_COL_IN_WS. Forwards without columns
+    (DCN_FWD_FUSED_NOCOL on the handle, or DCN_FWD_NO_COLUMNS per call) are remembered per
+    workspace, so every backward recomputes its columns instead of reading another step's;
+    a column-storing forward in between on one of them makes that one read its columns again.
+    Every module's gradients equal the unfused schedule's (∂W within one bf16 rounding where
+    it is recomputed inside dw_fused_bf16, everything else bit for bit). deform_conv.py:41-80
+    and its autodiff."""
+    h = gpu_handle
+    cases = [_case(930 + i, B=2, C=64, O_=256, H=28, W=28, off_scale=1.5) for i in range(3)]
+    ref = [_run(h, c, rt.DCN_FWD_UNFUSED)[2] for c in cases]
+    D = Buf(h)
+    try:
+        mods = [_upload_case(D, c) for c in cases]
+        wsb = rt.workspace_bytes(mods[0][0], True)
+        wss = [D.zeros(wsb) for _ in mods]
+        h.set_fwd_path(path)
+        flags = rt.DCN_FWD_NO_COLUMNS if path == rt.DCN_FWD_AUTO else 0
+        for (desc, _, p), ws in zip(mods, wss):
+            _fwd(h, desc, p, ws, wsb, flags)
+        # module 1 runs a column-storing forward again (AUTO, no flag): its backward reads them
+        h.set_fwd_path(rt.DCN_FWD_AUTO)
+        _fwd(h, mods[1][0], mods[1][2], wss[1], wsb, 0)
+        h.set_fwd_path(path)
+        for (desc, _, p), ws in reversed(list(zip(mods, wss))):
+            _bwd(h, desc, p, ws, wsb)
+        for i, (c, (_, _, p)) in enumerate(zip(cases, mods)):
+            got = _grads(D, c, p)
+            for k in got:
+                recomputed = k == "weight" and path == rt.DCN_FWD_FUSED_NOCOL and i != 1
+                if recomputed:
+                    _near(got[k], ref[i][k], f"module {i} ∂W (recomputed columns)")
+                else:
+                    np.testing.assert_array_equal(got[k], ref[i][k], err_msg=f"module {i} ∂{k}")
+    finally:
+        h.set_fwd_path(rt.DCN_FWD_AUTO)
+        D.free()
+
+
+def test_forward_no_columns_flag_small_workspace(gpu_handle):
+    """dcn_forward_ex(DCN_FWD_NO_COLUMNS) in a workspace of dcn_workspace_bytes(d,
+    DCN_WS_FORWARD_NO_COLUMNS) bytes (no column region: smaller by B·HW·K floats of the
+    layout): out bit for bit the fused forward's, the handle's path untouched; a workspace
+    one byte short is refused."""
+    h = gpu_handle
+    c = _case(940, B=2, C=128, O_=256, H=28, W=28)
+    out_f, _, _ = _run(h, c, rt.DCN_FWD_FUSED)
+    D = Buf(h)
+    try:
+        desc, oshape, p = _upload_case(D, c)
+        full = rt.workspace_bytes(desc, False)
+        small = rt.workspace_bytes(desc, rt.DCN_WS_FORWARD_NO_COLUMNS)
+        B, C = c[0]["x"].shape[:2]
+        assert full - small >= B * 28 * 28 * 9 * C * 4
+        ws = D.zeros(small)
+        h.set_fwd_path(rt.DCN_FWD_UNFUSED)
+        _fwd(h, desc, p, ws, small, rt.DCN_FWD_NO_COLUMNS)
+        assert h.get_fwd_path() == rt.DCN_FWD_UNFUSED
+        out = D.down(p["out"], oshape)
+        np.testing.assert_array_equal(out.view(np.uint32), out_f.view(np.uint32))
+        vp = ctypes.c_void_p
+        rc = h.lib.dcn_forward_ex(h.h, desc, vp(p["x"]), vp(p["w_off"]), vp(p["b_off"]),
+                                  vp(p["w"]), vp(p["b"]), vp(p["out"]), vp(p["off"]), vp(ws),
+                                  small - 1, rt.DCN_FWD_NO_COLUMNS)
+        assert rc == -5  # DCN_ERR_WORKSPACE
+    finally:
+        h.set_fwd_path(rt.DCN_FWD_AUTO)
+        D.free()
