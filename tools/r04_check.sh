@@ -7,6 +7,10 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 TAG=${1:-r04a}
+echo "== fused bf16 parity first (new kernels, short limit)" && \
+timeout -k 10 240 python -u -m pytest tests/test_gpu_fused_bf16.py -x -q --timeout 100 --timeout-method thread > gpurun_out/fused_first_$TAG.log 2>&1; rc=$?
+tail -4 gpurun_out/fused_first_$TAG.log
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || { echo "fused tests aborted rc=$rc"; exit $rc; }
 echo "== launch_diag" && \
 timeout -k 10 300 python -u tools/launch_diag.py --reps ${REPS:-200} --out gpurun_out/launch_diag_$TAG.json > gpurun_out/launch_diag_$TAG.log 2>&1; rc=$?
 tail -3 gpurun_out/launch_diag_$TAG.log
