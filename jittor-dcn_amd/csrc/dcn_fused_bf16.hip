@@ -84,6 +84,24 @@ __device__ __forceinline__ unsigned blend2(float4 wv, unsigned a, unsigned b, un
   v = __builtin_elementwise_fma(f32x2v{wv.w, wv.w}, unpack2(d), v);
   return (unsigned)f2bf(v.x) | ((unsigned)f2bf(v.y) << 16);
 }
+// the same roundings in scalar fp32 (v_mul_f32 / v_fma_f32): beside MFMAs on the same SIMD a
+// packed v_pk_fma_f32 costs far more than its issue slot (MI355X_MICROARCH.md, filler prices)
+__device__ __forceinline__ unsigned blend2s(float4 wv, unsigned a, unsigned b, unsigned c,
+                                            unsigned d) {
+  float lo = wv.x * __uint_as_float(a << 16);
+  float hi = wv.x * __uint_as_float(a & 0xffff0000u);
+  lo = fmaf(wv.y, __uint_as_float(b << 16), lo);
+  hi = fmaf(wv.y, __uint_as_float(b & 0xffff0000u), hi);
+  lo = fmaf(wv.z, __uint_as_float(c << 16), lo);
+  hi = fmaf(wv.z, __uint_as_float(c & 0xffff0000u), hi);
+  lo = fmaf(wv.w, __uint_as_float(d << 16), lo);
+  hi = fmaf(wv.w, __uint_as_float(d & 0xffff0000u), hi);
+  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+}
+__device__ __forceinline__ uint4 blend8s(float4 wv, uint4 ua, uint4 ub, uint4 uc, uint4 ud) {
+  return make_uint4(blend2s(wv, ua.x, ub.x, uc.x, ud.x), blend2s(wv, ua.y, ub.y, uc.y, ud.y),
+                    blend2s(wv, ua.z, ub.z, uc.z, ud.z), blend2s(wv, ua.w, ub.w, uc.w, ud.w));
+}
 __device__ __forceinline__ uint4 blend8(float4 wv, uint4 ua, uint4 ub, uint4 uc, uint4 ud) {
   return make_uint4(blend2(wv, ua.x, ub.x, uc.x, ud.x), blend2(wv, ua.y, ub.y, uc.y, ud.y),
                     blend2(wv, ua.z, ub.z, uc.z, ud.z), blend2(wv, ua.w, ub.w, uc.w, ud.w));
@@ -410,7 +428,8 @@ __global__ __launch_bounds__(kXT, 2) void fwd_fused_bf16_ws(Geo g, const bf16_t*
                                                             const bf16_t* __restrict__ wfr,
                                                             const float* __restrict__ bias,
                                                             bf16_t* __restrict__ out,
-                                                            bf16_t* __restrict__ colT, int tw_n) {
+                                                            bf16_t* __restrict__ colT, int tw_n,
+                                                            int dbg) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* const win = lds + kXLdsWin;
   char* const bt = lds + kXLdsB;
@@ -500,6 +519,11 @@ __global__ __launch_bounds__(kXT, 2) void fwd_fused_bf16_ws(Geo g, const bf16_t*
 #pragma unroll
       for (int pb = 0; pb < kPB; ++pb) {
         const bf16x8_t bv = as_frag(*reinterpret_cast<const uint4*>(bb + pb * 16 * kXPitch));
+        if (dbg & 2) {
+          acc[0][pb][0] += __builtin_bit_cast(float, __builtin_bit_cast(uint4, bv).x) +
+                           __builtin_bit_cast(float, a[0].x);
+          continue;
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           acc[i][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a[i]), bv, acc[i][pb], 0, 0, 0);
@@ -597,14 +621,15 @@ __global__ __launch_bounds__(kXT, 2) void fwd_fused_bf16_ws(Geo g, const bf16_t*
         const int slot = it * 16 + pw * 4 + grp;
         const int meta = recm[slot * kMaxN + n];
         uint4 o = make_uint4(0u, 0u, 0u, 0u);
-        if (meta >= 0) {
+        if (dbg & 1) {
+        } else if (meta >= 0) {
           const float4 wv = recw[slot * kMaxN + n];
           const char* wp = win + meta * kXPitch + chunk * 16;
           const uint4 ua = *reinterpret_cast<const uint4*>(wp);
           const uint4 ub = *reinterpret_cast<const uint4*>(wp + kXPitch);
           const uint4 uc = *reinterpret_cast<const uint4*>(wp + kWQ * kXPitch);
           const uint4 ud = *reinterpret_cast<const uint4*>(wp + (kWQ + 1) * kXPitch);
-          o = blend8(wv, ua, ub, uc, ud);
+          o = (dbg & 4) ? blend8s(wv, ua, ub, uc, ud) : blend8(wv, ua, ub, uc, ud);
         } else if (meta != kMZero) {
           const int j = -2 - meta;
           if (j < kXOvf) {
@@ -622,10 +647,14 @@ __global__ __launch_bounds__(kXT, 2) void fwd_fused_bf16_ws(Geo g, const bf16_t*
             unsigned* dst = reinterpret_cast<unsigned*>(
                 colT + ((size_t)b * g.HW + (size_t)h * g.Wo + w) * g.K + n * g.C + kXS * cs +
                 8 * chunk);
-            __builtin_nontemporal_store(o.x, dst);
-            __builtin_nontemporal_store(o.y, dst + 1);
-            __builtin_nontemporal_store(o.z, dst + 2);
-            __builtin_nontemporal_store(o.w, dst + 3);
+            if (dbg & 8) {
+              __builtin_nontemporal_store(as_v(o), reinterpret_cast<v4u*>(dst));
+            } else {
+              __builtin_nontemporal_store(o.x, dst);
+              __builtin_nontemporal_store(o.y, dst + 1);
+              __builtin_nontemporal_store(o.z, dst + 2);
+              __builtin_nontemporal_store(o.w, dst + 3);
+            }
           }
         }
       }
@@ -996,7 +1025,7 @@ __global__ __launch_bounds__(kXT, 2) void dw_fused_bf16_ws(Geo g, const bf16_t* 
                                                            const float* __restrict__ off,
                                                            const bf16_t* __restrict__ gout,
                                                            float* __restrict__ parts, int tw_n,
-                                                           int ngrp) {
+                                                           int ngrp, int dbg) {
   extern __shared__ __attribute__((aligned(16))) char dl[];
   char* const win = dl + kYLdsWin;
   char* const bt = dl + kYLdsB;
@@ -1087,6 +1116,10 @@ __global__ __launch_bounds__(kXT, 2) void dw_fused_bf16_ws(Geo g, const bf16_t* 
         const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
             (lds_s16x4_p)(base + (s0 + 4) * kXPitch + 16 * ychunk(s0 + 4, c)));
         const s16x8_t bv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if (dbg & 2) {
+          acc[0][cb][0] += (float)bv[0] + __builtin_bit_cast(float, a[0].x);
+          continue;
+        }
 #pragma unroll
         for (int ob = 0; ob < 4; ++ob)
           acc[ob][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
@@ -1254,14 +1287,15 @@ __global__ __launch_bounds__(kXT, 2) void dw_fused_bf16_ws(Geo g, const bf16_t* 
         const int slot = it * 16 + pw * 4 + sg;
         const int meta = recm[(i & 1) * kSlots + slot];
         uint4 o = make_uint4(0u, 0u, 0u, 0u);
-        if (meta >= 0) {
+        if (dbg & 1) {
+        } else if (meta >= 0) {
           const float4 wv = recw[(i & 1) * kSlots + slot];
           const char* wp = win + meta * kXPitch + chunk * 16;
           const uint4 ua = *reinterpret_cast<const uint4*>(wp);
           const uint4 ub = *reinterpret_cast<const uint4*>(wp + kXPitch);
           const uint4 uc = *reinterpret_cast<const uint4*>(wp + kWQ * kXPitch);
           const uint4 ud = *reinterpret_cast<const uint4*>(wp + (kWQ + 1) * kXPitch);
-          o = blend8(wv, ua, ub, uc, ud);
+          o = (dbg & 4) ? blend8s(wv, ua, ub, uc, ud) : blend8(wv, ua, ub, uc, ud);
         } else if (meta != kMZero) {
           const int j = -2 - meta;
           if (j < kYOvf) {
@@ -1311,6 +1345,16 @@ __global__ __launch_bounds__(kXT, 2) void dw_fused_bf16_ws(Geo g, const bf16_t* 
 }
 
 }  // namespace
+
+// r04 diagnosis (temporary): DCN_WS_DBG bits: 1 producers skip the gather, 2 consumers skip the
+// MFMAs, 4 scalar blend, 8 16-B column stores
+int ws_dbg() {
+  static const int v = [] {
+    const char* e = std::getenv("DCN_WS_DBG");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
 
 // The > 64 KB dynamic-LDS attribute of a kernel, per device: set once per (kernel, device id),
 // recorded only after it succeeded (a failure is returned and retried on the next call).
@@ -1362,10 +1406,10 @@ hipError_t launch_fused_fwd_bf16(const Geo& g, const bf16_t* xT, const float* of
     if (e != hipSuccess) return e;
     if (colT)
       hipLaunchKernelGGL(fwd_fused_bf16_ws<true>, grid, dim3(kXT), kXLds, s, g, xT, off, wfr, bias,
-                         out, colT, tw_n);
+                         out, colT, tw_n, ws_dbg());
     else
       hipLaunchKernelGGL(fwd_fused_bf16_ws<false>, grid, dim3(kXT), kXLds, s, g, xT, off, wfr,
-                         bias, out, colT, tw_n);
+                         bias, out, colT, tw_n, ws_dbg());
     return hipGetLastError();
   }
   if (colT)
@@ -1416,7 +1460,7 @@ hipError_t launch_fused_dw_bf16(const Geo& g, const bf16_t* xT, const float* off
     const int nslices = (g.C + kXS - 1) / kXS;
     const dim3 grid(nslices * g.N, ng, g.O / kOT);
     hipLaunchKernelGGL(dw_fused_bf16_ws, grid, dim3(kXT), kYLds, s, g, xT, off, gout, parts, tw_n,
-                       ng);
+                       ng, ws_dbg());
     return hipGetLastError();
   }
   const int ng = std::min(16, g.B);

@@ -1,0 +1,24 @@
+#!/bin/bash
+# r04: diagnosis of the warp-specialised bf16 kernels (temporary DCN_WS_DBG knob: 1 producers skip
+# the gather, 2 consumers skip the MFMAs, 4 scalar blend, 8 16-B column stores) at config 4,
+# after their parity tests. Stops at the first failure.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+T=${1:-ws2}
+echo "== fused bf16 parity" && \
+timeout -k 10 240 python -u -m pytest tests/test_gpu_fused_bf16.py -x -q --timeout 100 --timeout-method thread > gpurun_out/${T}_pytest.log 2>&1 || { tail -30 gpurun_out/${T}_pytest.log; exit 1; }
+tail -2 gpurun_out/${T}_pytest.log
+run() {  # name env... -- bench args
+  local name=$1; shift
+  env "$@" timeout -k 10 120 python bench.py --config 4 --steps 20 --warmup 5 --no-cpu-baseline --no-strong --no-host-path $BARGS > gpurun_out/${T}_$name.json 2> gpurun_out/${T}_$name.err || { tail -5 gpurun_out/${T}_$name.err; exit 1; }
+  python -c "import json,sys; d=json.loads(open('gpurun_out/${T}_$name.json').read().splitlines()[-1]); print('$name', d['ms_per_step'], {k: d['kernel_ms'].get(k) for k in ('gemm_fwd','gemm_dw')})"
+}
+for fp in 2 3; do
+  BARGS="--fwd-path $fp"
+  run old_p$fp DCN_FWD_WS=0 DCN_DW_WS=0
+  for v in 0 1 2 3 4 8 12; do run ws_p${fp}_d$v DCN_WS_DBG=$v; done
+  run old2_p$fp DCN_FWD_WS=0 DCN_DW_WS=0
+done
+echo done
