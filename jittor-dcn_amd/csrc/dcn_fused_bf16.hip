@@ -519,11 +519,6 @@ __global__ __launch_bounds__(kXT, 2) void fwd_fused_bf16_ws(Geo g, const bf16_t*
 #pragma unroll
       for (int pb = 0; pb < kPB; ++pb) {
         const bf16x8_t bv = as_frag(*reinterpret_cast<const uint4*>(bb + pb * 16 * kXPitch));
-        if (dbg & 2) {
-          acc[0][pb][0] += __builtin_bit_cast(float, __builtin_bit_cast(uint4, bv).x) +
-                           __builtin_bit_cast(float, a[0].x);
-          continue;
-        }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           acc[i][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a[i]), bv, acc[i][pb], 0, 0, 0);
@@ -533,6 +528,7 @@ __global__ __launch_bounds__(kXT, 2) void fwd_fused_bf16_ws(Geo g, const bf16_t*
     auto consume = [&]() {
       if (consumed >= produced) return;
       const int mc = consumed++;  // from buffer mc & 1
+      if (dbg & 2) return;
       const int cw = min(kXS, g.C - kXS * (mc / N));
       const int mn = min(mc + 1, M - 1);
       kstep(mc & 1, 0, a0);
@@ -664,7 +660,9 @@ __global__ __launch_bounds__(kXT, 2) void fwd_fused_bf16_ws(Geo g, const bf16_t*
         stage_window(m / N);
         __syncthreads();
       }
-      if (m < M) produce(m);  // gather phase m
+      if (m < M) {  // gather phase m
+        produce(m);
+      }
       __syncthreads();
     }
   }
@@ -1116,10 +1114,6 @@ __global__ __launch_bounds__(kXT, 2) void dw_fused_bf16_ws(Geo g, const bf16_t* 
         const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
             (lds_s16x4_p)(base + (s0 + 4) * kXPitch + 16 * ychunk(s0 + 4, c)));
         const s16x8_t bv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        if (dbg & 2) {
-          acc[0][cb][0] += (float)bv[0] + __builtin_bit_cast(float, a[0].x);
-          continue;
-        }
 #pragma unroll
         for (int ob = 0; ob < 4; ++ob)
           acc[ob][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
@@ -1134,7 +1128,7 @@ __global__ __launch_bounds__(kXT, 2) void dw_fused_bf16_ws(Geo g, const bf16_t* 
     __syncthreads();  // prologue 2: window and overflow of tile 0
     // phase i: the producers gather tile i; the consumers run the MFMAs of tile i - 1
     for (int i = 0; i <= T; ++i) {
-      const int ic = i - 1;
+      const int ic = (dbg & 2) ? -1 : i - 1;
       if (ic >= 0) {
         a_load(ic, 2, aC);
         kstep(ic & 1, 0, aA);
