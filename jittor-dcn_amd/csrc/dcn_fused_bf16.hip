@@ -606,52 +606,80 @@ __global__ __launch_bounds__(kXT, 2) void fwd_fused_bf16_ws(Geo g, const bf16_t*
           *reinterpret_cast<uint4*>(ovfd + idx * 16) = ov[k];
       }
     };
-    // gather macro step m (slice cs, tap n) into buffer m & 1 (and the column rows)
+    // gather macro step m (slice cs, tap n) into buffer m & 1 (and the column rows). The 7
+    // samples of a thread go in two batches (4 + 3): every record read of a batch, then every
+    // corner read, then the blends and stores, branch-free (an overflow sample's staged slice is
+    // read in the first corner's place, a sample outside the image blends to zero), so the LDS
+    // round trips of a batch overlap instead of chaining through each sample's B-tile store.
+    // A sample past the overflow area is rare: it is redone from global memory afterwards.
     auto produce = [&](int m) {
       const int cs = m / N, n = m - cs * N;
       const int cw8 = min(kXS, g.C - kXS * cs) / 8;
       char* bb = bt + (m & 1) * kSlots * kXPitch;
       const bool cok = chunk < cw8;
+      constexpr int NU = kSlots / 16, GU = 4;
+      bool slow = false;
 #pragma unroll
-      for (int it = 0; it < kSlots / 16; ++it) {
-        const int slot = it * 16 + pw * 4 + grp;
-        const int meta = recm[slot * kMaxN + n];
-        uint4 o = make_uint4(0u, 0u, 0u, 0u);
-        if (dbg & 1) {
-        } else if (meta >= 0) {
-          const float4 wv = recw[slot * kMaxN + n];
-          const char* wp = win + meta * kXPitch + chunk * 16;
-          const uint4 ua = *reinterpret_cast<const uint4*>(wp);
-          const uint4 ub = *reinterpret_cast<const uint4*>(wp + kXPitch);
-          const uint4 uc = *reinterpret_cast<const uint4*>(wp + kWQ * kXPitch);
-          const uint4 ud = *reinterpret_cast<const uint4*>(wp + (kWQ + 1) * kXPitch);
-          o = (dbg & 4) ? blend8s(wv, ua, ub, uc, ud) : blend8(wv, ua, ub, uc, ud);
-        } else if (meta != kMZero) {
-          const int j = -2 - meta;
-          if (j < kXOvf) {
-            o = *reinterpret_cast<const uint4*>(ovfd + j * kXPitch + chunk * 16);
-          } else if (cok) {  // more overflow samples than the area holds: global corners
-            const int h = h0 + slot / kTW, w = w0 + slot % kTW;
-            const Tap t = sample_tap(g, off, b, 0, n, h * g.Wo + w);
-            o = gather_global(g, xb, t.r0, t.c0, kXS * cs + 8 * chunk, recw[slot * kMaxN + n]);
+      for (int g0 = 0; g0 < NU; g0 += GU) {
+        int meta[GU];
+        float4 wv[GU];
+        uint4 ua[GU], ub[GU], uc[GU], ud[GU];
+#pragma unroll
+        for (int k = 0; k < GU; ++k) {
+          if (g0 + k < NU) {
+            const int slot = (g0 + k) * 16 + pw * 4 + grp;
+            meta[k] = recm[slot * kMaxN + n];
+            wv[k] = recw[slot * kMaxN + n];
           }
         }
-        *reinterpret_cast<uint4*>(bb + slot * kXPitch + 16 * (chunk ^ (slot & 15))) = o;
-        if (STORE && cok) {
-          const int h = h0 + slot / kTW, w = w0 + slot % kTW;
-          if (h < g.Ho && w < g.Wo) {
-            unsigned* dst = reinterpret_cast<unsigned*>(
-                colT + ((size_t)b * g.HW + (size_t)h * g.Wo + w) * g.K + n * g.C + kXS * cs +
-                8 * chunk);
-            if (dbg & 8) {
-              __builtin_nontemporal_store(as_v(o), reinterpret_cast<v4u*>(dst));
-            } else {
-              __builtin_nontemporal_store(o.x, dst);
-              __builtin_nontemporal_store(o.y, dst + 1);
-              __builtin_nontemporal_store(o.z, dst + 2);
-              __builtin_nontemporal_store(o.w, dst + 3);
+#pragma unroll
+        for (int k = 0; k < GU; ++k) {
+          if (g0 + k < NU) {
+            const int mt = meta[k];
+            const int j = min(max(-2 - mt, 0), kXOvf - 1);
+            const char* wq = win + max(mt, 0) * kXPitch + chunk * 16;
+            ua[k] = *reinterpret_cast<const uint4*>(mt >= 0 ? wq : ovfd + j * kXPitch + chunk * 16);
+            ub[k] = *reinterpret_cast<const uint4*>(wq + kXPitch);
+            uc[k] = *reinterpret_cast<const uint4*>(wq + kWQ * kXPitch);
+            ud[k] = *reinterpret_cast<const uint4*>(wq + (kWQ + 1) * kXPitch);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < GU; ++k) {
+          if (g0 + k < NU) {
+            const int slot = (g0 + k) * 16 + pw * 4 + grp;
+            const int mt = meta[k];
+            uint4 o = (dbg & 4) ? blend8s(wv[k], ua[k], ub[k], uc[k], ud[k])
+                                : blend8(wv[k], ua[k], ub[k], uc[k], ud[k]);
+            if (mt < 0) o = (mt == kMZero || -2 - mt >= kXOvf) ? make_uint4(0u, 0u, 0u, 0u) : ua[k];
+            if (dbg & 1) o = make_uint4(0u, 0u, 0u, 0u);
+            slow |= mt != kMZero && -2 - mt >= kXOvf;
+            *reinterpret_cast<uint4*>(bb + slot * kXPitch + 16 * (chunk ^ (slot & 15))) = o;
+            if (STORE && cok) {
+              const int h = h0 + slot / kTW, w = w0 + slot % kTW;
+              if (h < g.Ho && w < g.Wo)
+                __builtin_nontemporal_store(
+                    as_v(o), reinterpret_cast<v4u*>(colT + ((size_t)b * g.HW + (size_t)h * g.Wo + w) * g.K +
+                                                    n * g.C + kXS * cs + 8 * chunk));
             }
           }
+        }
+      }
+      if (__any(slow)) {  // more overflow samples than the area holds: global corners
+#pragma unroll 1
+        for (int it = 0; it < NU; ++it) {
+          const int slot = it * 16 + pw * 4 + grp;
+          const int mt = recm[slot * kMaxN + n];
+          if (mt == kMZero || -2 - mt < kXOvf || !cok) continue;
+          const int h = h0 + slot / kTW, w = w0 + slot % kTW;
+          const Tap t = sample_tap(g, off, b, 0, n, h * g.Wo + w);
+          const uint4 o = gather_global(g, xb, t.r0, t.c0, kXS * cs + 8 * chunk,
+                                        recw[slot * kMaxN + n]);
+          *reinterpret_cast<uint4*>(bb + slot * kXPitch + 16 * (chunk ^ (slot & 15))) = o;
+          if (STORE && h < g.Ho && w < g.Wo)
+            __builtin_nontemporal_store(
+                as_v(o), reinterpret_cast<v4u*>(colT + ((size_t)b * g.HW + (size_t)h * g.Wo + w) * g.K +
+                                                n * g.C + kXS * cs + 8 * chunk));
         }
       }
     };
@@ -1271,37 +1299,68 @@ __global__ __launch_bounds__(kXT, 2) void dw_fused_bf16_ws(Geo g, const bf16_t* 
           *reinterpret_cast<uint4*>(ovfd + idx * 16) = blend8(ov[k].wv, ov[k].a, ov[k].b, ov[k].c, ov[k].d);
       }
     };
-    // the column tile of tile i into buffer i & 1: sample (slot) per 16 lanes, chunk per lane
+    // the column tile of tile i into buffer i & 1: sample (slot) per 16 lanes, chunk per lane;
+    // batched and branch-free like the forward's producers (two batches of samples: record
+    // reads, corner reads, blends + stores), the rare samples past the overflow area redone
+    // from global memory afterwards
     auto produce = [&](int i) {
       const TileId q = tile_id(i);
       const bf16_t* xb = xT + (size_t)q.b * g.HWi * g.C;
       char* bb = bt + (i & 1) * kYSl * kXPitch;
+      const int* rm = recm + (i & 1) * kSlots;
+      const float4* rw = recw + (i & 1) * kSlots;
+      constexpr int NU = kSlots / 16, GU = 2;
+      bool slow = false;
 #pragma unroll
-      for (int it = 0; it < kSlots / 16; ++it) {
-        const int slot = it * 16 + pw * 4 + sg;
-        const int meta = recm[(i & 1) * kSlots + slot];
-        uint4 o = make_uint4(0u, 0u, 0u, 0u);
-        if (dbg & 1) {
-        } else if (meta >= 0) {
-          const float4 wv = recw[(i & 1) * kSlots + slot];
-          const char* wp = win + meta * kXPitch + chunk * 16;
-          const uint4 ua = *reinterpret_cast<const uint4*>(wp);
-          const uint4 ub = *reinterpret_cast<const uint4*>(wp + kXPitch);
-          const uint4 uc = *reinterpret_cast<const uint4*>(wp + kWQ * kXPitch);
-          const uint4 ud = *reinterpret_cast<const uint4*>(wp + (kWQ + 1) * kXPitch);
-          o = (dbg & 4) ? blend8s(wv, ua, ub, uc, ud) : blend8(wv, ua, ub, uc, ud);
-        } else if (meta != kMZero) {
-          const int j = -2 - meta;
-          if (j < kYOvf) {
-            o = *reinterpret_cast<const uint4*>(ovfd + j * kXPitch + chunk * 16);
-          } else if (cok) {  // past the overflow area: corners from global memory
-            const int h = q.h0 + slot / kTW, w = q.w0 + slot % kTW;
-            const Tap t = sample_tap(g, off, q.b, 0, n, h * g.Wo + w);
-            o = gather_global(g, xb, t.r0, t.c0, kXS * cs + 8 * chunk,
-                              recw[(i & 1) * kSlots + slot]);
+      for (int g0 = 0; g0 < NU; g0 += GU) {
+        int meta[GU];
+        float4 wv[GU];
+        uint4 ua[GU], ub[GU], uc[GU], ud[GU];
+#pragma unroll
+        for (int k = 0; k < GU; ++k) {
+          if (g0 + k < NU) {
+            const int slot = (g0 + k) * 16 + pw * 4 + sg;
+            meta[k] = rm[slot];
+            wv[k] = rw[slot];
           }
         }
-        *reinterpret_cast<uint4*>(bb + slot * kXPitch + 16 * ychunk(slot, chunk)) = o;
+#pragma unroll
+        for (int k = 0; k < GU; ++k) {
+          if (g0 + k < NU) {
+            const int mt = meta[k];
+            const int j = min(max(-2 - mt, 0), kYOvf - 1);
+            const char* wq = win + max(mt, 0) * kXPitch + chunk * 16;
+            ua[k] = *reinterpret_cast<const uint4*>(mt >= 0 ? wq : ovfd + j * kXPitch + chunk * 16);
+            ub[k] = *reinterpret_cast<const uint4*>(wq + kXPitch);
+            uc[k] = *reinterpret_cast<const uint4*>(wq + kWQ * kXPitch);
+            ud[k] = *reinterpret_cast<const uint4*>(wq + (kWQ + 1) * kXPitch);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < GU; ++k) {
+          if (g0 + k < NU) {
+            const int slot = (g0 + k) * 16 + pw * 4 + sg;
+            const int mt = meta[k];
+            uint4 o = (dbg & 4) ? blend8s(wv[k], ua[k], ub[k], uc[k], ud[k])
+                                : blend8(wv[k], ua[k], ub[k], uc[k], ud[k]);
+            if (mt < 0) o = (mt == kMZero || -2 - mt >= kYOvf) ? make_uint4(0u, 0u, 0u, 0u) : ua[k];
+            if (dbg & 1) o = make_uint4(0u, 0u, 0u, 0u);
+            slow |= mt != kMZero && -2 - mt >= kYOvf;
+            *reinterpret_cast<uint4*>(bb + slot * kXPitch + 16 * ychunk(slot, chunk)) = o;
+          }
+        }
+      }
+      if (__any(slow)) {  // past the overflow area: corners from global memory
+#pragma unroll 1
+        for (int it = 0; it < NU; ++it) {
+          const int slot = it * 16 + pw * 4 + sg;
+          const int mt = rm[slot];
+          if (mt == kMZero || -2 - mt < kYOvf || !cok) continue;
+          const int h = q.h0 + slot / kTW, w = q.w0 + slot % kTW;
+          const Tap t = sample_tap(g, off, q.b, 0, n, h * g.Wo + w);
+          *reinterpret_cast<uint4*>(bb + slot * kXPitch + 16 * ychunk(slot, chunk)) =
+              gather_global(g, xb, t.r0, t.c0, kXS * cs + 8 * chunk, rw[slot]);
+        }
       }
     };
     uint4 wr[IT];

@@ -18,7 +18,7 @@ run() {  # name env... -- bench args
 for fp in 2 3; do
   BARGS="--fwd-path $fp"
   run old_p$fp DCN_FWD_WS=0 DCN_DW_WS=0
-  for v in 0 1 2 3 4 8 12; do run ws_p${fp}_d$v DCN_WS_DBG=$v; done
+  for v in 0 4 1 2 5; do run ws_p${fp}_d$v DCN_WS_DBG=$v; done
   run old2_p$fp DCN_FWD_WS=0 DCN_DW_WS=0
 done
 echo done
