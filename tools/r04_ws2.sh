@@ -21,4 +21,10 @@ for fp in 2 3; do
   for v in 0 4 1 2 5; do run ws_p${fp}_d$v DCN_WS_DBG=$v; done
   run old2_p$fp DCN_FWD_WS=0 DCN_DW_WS=0
 done
-echo done
+echo variants done
+echo "== pytest -m gpu" && \
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${T}_pytest_all.log 2>&1 || { tail -30 gpurun_out/${T}_pytest_all.log; exit 1; }
+tail -3 gpurun_out/${T}_pytest_all.log
+echo "== launch_diag" && \
+timeout -k 10 240 python -u tools/launch_diag.py --reps 200 --reps3 40 --out gpurun_out/${T}_diag.json > gpurun_out/${T}_diag.log 2>&1 || { tail -3 gpurun_out/${T}_diag.log | cut -c1-800; exit 1; }
+echo diag ok
