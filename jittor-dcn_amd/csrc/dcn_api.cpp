@@ -159,12 +159,7 @@ WsLayout ws_layout(const Geo& g, bool bwd, bool cols = true) {
   }
   if (bwd) {
     // ∂W partials; first also the ∂b tile sums of the fused ∂out transpose
-    // (DCN_BF16: also the recomputed-column ∂W kernel's group partials, whose group count may
-    // exceed B for small batches)
-    const size_t nparts = g.dt == DCN_BF16 && dcn::fused_dw_bf16_ok(g)
-                              ? std::max<size_t>(g.B, dcn::fused_dw_bf16_groups(g))
-                              : (size_t)g.B;
-    L.parts = take(std::max(nparts * g.O * g.K, dcn::xpose_chsum_floats(g.B, g.O, g.HW)) *
+    L.parts = take(std::max((size_t)g.B * g.O * g.K, dcn::xpose_chsum_floats(g.B, g.O, g.HW)) *
                    sizeof(float));
     L.goff = take((size_t)g.B * g.J * g.HW * sizeof(float));
     L.goffT = take(dcn::offset_conv_goffT_floats(g) * sizeof(float));

@@ -173,6 +173,46 @@ __device__ __forceinline__ float wave_sum(float v) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
+// The 64-lane sums of eight values at once, in wave_sum's association order (lane pairs,
+// quads, half rows, rows, then (row 0 + row 1) + (row 2 + row 3)), so each sum has wave_sum's
+// bits. The first three levels also halve the values held per lane: a lane keeps one value of
+// each pair and receives its partner's share of it (two selects and one DPP add per kept
+// value). Which one it keeps follows lane bits b0 ^ b2, b1 ^ b2, b2 at the three levels: each
+// level's partners (lane ^ 1, lane ^ 2, then row_half_mirror's k and 7 - k, all three bits
+// flipped) differ in that level's selector and agree in the earlier ones, so they hold the
+// same values. The last three levels fold the one value left (row_ror:8 = lane ^ 8,
+// then v_permlane16_swap and v_permlane32_swap of the value with itself). 28 VALU for the eight
+// sums where wave_sum takes about 17 per sum. wave_sum8_lane(k) names a lane holding sum k.
+template <int CTRL>
+__device__ __forceinline__ float half_fold(bool hi, float a, float b) {
+  // lanes with hi keep b, the others a; each adds its partner's copy of what it keeps
+  return (hi ? b : a) + dpp_f<CTRL>(hi ? a : b);
+}
+__device__ __forceinline__ float swap_fold16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float swap_fold32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float wave_sum8(const float (&v)[8], int lane) {
+  const bool b0 = lane & 1, b1 = (lane >> 1) & 1, b2 = (lane >> 2) & 1;
+  const bool h1 = b0 ^ b2, h2 = b1 ^ b2;
+  const float p0 = half_fold<0xB1>(h1, v[0], v[4]), p1 = half_fold<0xB1>(h1, v[1], v[5]);
+  const float p2 = half_fold<0xB1>(h1, v[2], v[6]), p3 = half_fold<0xB1>(h1, v[3], v[7]);
+  const float q0 = half_fold<0x4E>(h2, p0, p2), q1 = half_fold<0x4E>(h2, p1, p3);
+  float d = half_fold<0x141>(b2, q0, q1);  // row_half_mirror
+  d += dpp_f<0x128>(d);                    // row_ror:8 (wave_sum: row_mirror, same sums)
+  return swap_fold32(swap_fold16(d));
+}
+// lane bits of sum k: b2 = bit 0 of k, b1 ^ b2 = bit 1, b0 ^ b2 = bit 2
+__host__ __device__ constexpr int wave_sum8_lane(int k) {
+  return (((k >> 2) ^ k) & 1) | ((((k >> 1) ^ k) & 1) << 1) | ((k & 1) << 2);
+}
+
 // Workgroup barrier that orders LDS only: __syncthreads()'s fence would also drain every
 // outstanding global load and store (vmcnt(0)), i.e. the prefetch pipelines kept in flight
 // across the barrier (fused forward: the column stores of a k step; K5: the ∂col rows).

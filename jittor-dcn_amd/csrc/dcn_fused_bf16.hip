@@ -25,9 +25,7 @@
 //   * Epilogue: bf16(acc + bias[o]) straight to NCHW out (launch_bias_to_bf16's rounding).
 #include <algorithm>
 #include <climits>
-#include <cstdlib>
 #include <mutex>
-#include <utility>
 #include <vector>
 
 #include "dcn_device.h"
@@ -37,8 +35,6 @@ namespace {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
-typedef short s16x4_t __attribute__((ext_vector_type(4)));
-typedef short s16x8_t __attribute__((ext_vector_type(8)));
 
 constexpr int kTH = 7, kTW = 16;  // output tile rows (h) × columns (w)
 constexpr int kPB = kTH * kTW / 16;  // 16-slot MFMA column blocks
@@ -83,24 +79,6 @@ __device__ __forceinline__ unsigned blend2(float4 wv, unsigned a, unsigned b, un
   v = __builtin_elementwise_fma(f32x2v{wv.z, wv.z}, unpack2(c), v);
   v = __builtin_elementwise_fma(f32x2v{wv.w, wv.w}, unpack2(d), v);
   return (unsigned)f2bf(v.x) | ((unsigned)f2bf(v.y) << 16);
-}
-// the same roundings in scalar fp32 (v_mul_f32 / v_fma_f32): beside MFMAs on the same SIMD a
-// packed v_pk_fma_f32 costs far more than its issue slot (MI355X_MICROARCH.md, filler prices)
-__device__ __forceinline__ unsigned blend2s(float4 wv, unsigned a, unsigned b, unsigned c,
-                                            unsigned d) {
-  float lo = wv.x * __uint_as_float(a << 16);
-  float hi = wv.x * __uint_as_float(a & 0xffff0000u);
-  lo = fmaf(wv.y, __uint_as_float(b << 16), lo);
-  hi = fmaf(wv.y, __uint_as_float(b & 0xffff0000u), hi);
-  lo = fmaf(wv.z, __uint_as_float(c << 16), lo);
-  hi = fmaf(wv.z, __uint_as_float(c & 0xffff0000u), hi);
-  lo = fmaf(wv.w, __uint_as_float(d << 16), lo);
-  hi = fmaf(wv.w, __uint_as_float(d & 0xffff0000u), hi);
-  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
-}
-__device__ __forceinline__ uint4 blend8s(float4 wv, uint4 ua, uint4 ub, uint4 uc, uint4 ud) {
-  return make_uint4(blend2s(wv, ua.x, ub.x, uc.x, ud.x), blend2s(wv, ua.y, ub.y, uc.y, ud.y),
-                    blend2s(wv, ua.z, ub.z, uc.z, ud.z), blend2s(wv, ua.w, ub.w, uc.w, ud.w));
 }
 __device__ __forceinline__ uint4 blend8(float4 wv, uint4 ua, uint4 ub, uint4 uc, uint4 ud) {
   return make_uint4(blend2(wv, ua.x, ub.x, uc.x, ud.x), blend2(wv, ua.y, ub.y, uc.y, ud.y),
@@ -386,335 +364,6 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
   }
 }
 
-
-// ---------------------------------------------------------------------------------------
-// Warp-specialised form (r04). Same product and the same per-sample arithmetic as
-// fwd_fused_bf16 (the columns bit for bit K1's), reorganised so that the gather and the MFMAs
-// run in different waves of the same SIMD and overlap instead of adding up (r03 phase skips:
-// gather and MFMA costs added, and 45 % of the LDS cycles were bank conflicts):
-//   * 8 waves: waves 0-3 consume (wave w: output channels 64w..64w+63 × the 112 slots, 28
-//     accumulators of v_mfma_f32_16x16x32_bf16), waves 4-7 produce (gather). One workgroup
-//     per CU; each SIMD holds one consumer and one producer wave.
-//   * A macro step is (128-channel slice cs, tap n): the producers gather the [112 slots]
-//     [128 channels] B tile of macro step m into buffer m & 1 while the consumers run the four
-//     32-channel k steps of macro step m - 1 from the other buffer; one barrier per macro step
-//     (18 per tile at C = 256, instead of 72).
-//   * Conflict-free LDS: the window holds 128 channels per pixel at a 256-B pitch and 16
-//     consecutive lanes gather the 16 8-channel chunks of one sample, so every ds_read_b128 of
-//     a corner covers 16 distinct 16-B bank groups whatever the sampled pixels are (r03: four
-//     random pixels per lane group). The B tile is [slot][16 chunks] at 256 B per slot with
-//     chunk ^ (slot & 15): the producers' 16-B stores and the consumers' fragment reads are
-//     both conflict-free.
-//   * Column stores (STORE): 16 lanes store one sample's 256 contiguous bytes of its column
-//     row (whole 128-B lines) instead of 64-B pieces.
-constexpr int kXS = 128;                    // channels per slice (macro step)
-constexpr int kXChunks = kXS / 8;           // 16 × 8-channel chunks
-constexpr int kXPitch = kXS * 2;            // 256 B per window pixel / B-tile slot
-constexpr int kXOvf = 32;                   // overflow samples per tile with a staged slice
-constexpr int kXT = 512;                    // threads: 4 consumer + 4 producer waves
-constexpr int kXLdsWin = 0;
-constexpr int kXLdsB = kXLdsWin + kWPix * kXPitch;           // 56,320
-constexpr int kXLdsRecW = kXLdsB + 2 * kSlots * kXPitch;     // + 57,344
-constexpr int kXLdsRecM = kXLdsRecW + kSlots * kMaxN * 16;
-constexpr int kXLdsOvfT = kXLdsRecM + kSlots * kMaxN * 4;
-constexpr int kXLdsOvfD = kXLdsOvfT + kXOvf * 16;
-constexpr int kXLdsCnt = kXLdsOvfD + kXOvf * kXPitch;
-constexpr int kXLds = kXLdsCnt + 16;
-static_assert(kXLds <= 160 * 1024, "one workgroup per CU");
-
-template <bool STORE>
-__global__ __launch_bounds__(kXT, 2) void fwd_fused_bf16_ws(Geo g, const bf16_t* __restrict__ xT,
-                                                            const float* __restrict__ off,
-                                                            const bf16_t* __restrict__ wfr,
-                                                            const float* __restrict__ bias,
-                                                            bf16_t* __restrict__ out,
-                                                            bf16_t* __restrict__ colT, int tw_n,
-                                                            int dbg) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  char* const win = lds + kXLdsWin;
-  char* const bt = lds + kXLdsB;
-  float4* const recw = reinterpret_cast<float4*>(lds + kXLdsRecW);
-  int* const recm = reinterpret_cast<int*>(lds + kXLdsRecM);
-  int4* const ovft = reinterpret_cast<int4*>(lds + kXLdsOvfT);
-  char* const ovfd = lds + kXLdsOvfD;
-  int* const cnt = reinterpret_cast<int*>(lds + kXLdsCnt);
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool consumer = wave < 4;
-  const Block3 blk = xcd_block();
-  const int b = blk.y;
-  const int th_i = blk.x / tw_n, tw_i = blk.x - th_i * tw_n;
-  const int h0 = th_i * kTH, w0 = tw_i * kTW;
-  const int rlo = (int)floorf((float)w0 * (float)(g.H - 1) / (float)(g.Wo - 1)) - kMar;
-  const int qlo = (int)floorf((float)h0 * (float)(g.W - 1) / (float)(g.Ho - 1)) - kMar;
-  const bf16_t* const xb = xT + (size_t)b * g.HWi * g.C;
-  const int N = g.N;
-
-  // ---- records (all waves): the reference coordinate chain per (slot, tap) ----
-  if (tid == 0) cnt[0] = 0;
-  __syncthreads();
-  for (int s = tid; s < kSlots * N; s += kXT) {
-    const int p = s / N, n = s - p * N;
-    const int h = h0 + p / kTW, w = w0 + p % kTW;
-    int meta = kMZero;
-    float4 wv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (h < g.Ho && w < g.Wo) {
-      const Tap t = sample_tap(g, off, b, 0, n, h * g.Wo + w);
-      if (t.ok) {
-        const float gr = 1.0f - t.fr, gc = 1.0f - t.fc;
-        wv = make_float4(gr * gc, gr * t.fc, t.fr * gc, t.fr * t.fc);
-        const int rr = t.r0 - rlo, qq = t.c0 - qlo;
-        if (rr >= 0 && rr + 1 < kWR && qq >= 0 && qq + 1 < kWQ) {
-          meta = rr * kWQ + qq;
-        } else {
-          const int j = atomicAdd(cnt, 1);  // any order: each entry is computed on its own
-          meta = -2 - j;
-          if (j < kXOvf) ovft[j] = make_int4(t.r0, t.c0, p * kMaxN + n, 0);
-        }
-      }
-    }
-    recm[p * kMaxN + n] = meta;
-    recw[p * kMaxN + n] = wv;
-  }
-  __syncthreads();
-  const int novf = min(cnt[0], kXOvf);
-  const int nslices = (g.C + kXS - 1) / kXS;
-  const int M = nslices * N;  // macro steps
-  // Phases, one barrier each, the same sequence in both roles: before each slice a window
-  // phase (the producers stage the slice's window), then per macro step m a gather phase (the
-  // producers gather m into buffer m & 1), and a final phase. In every phase the consumers
-  // run the MFMAs of the oldest macro step gathered but not yet consumed, so the window
-  // staging overlaps the previous slice's last MFMAs.
-
-  if (consumer) {
-    // ================= consumer waves: 64 output channels × 112 slots =================
-    const int o0 = blk.z * kOT + 64 * wave;
-    const int NKS = g.K / 32;
-    f32x4 acc[4][kPB];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < kPB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // A fragments of macro step m, k step j (ks = (n·C + 128·cs) / 32 + j), rows o0 + 16i
-    auto load_a = [&](int m, int j, uint4 (&a)[4]) {
-      const int cs = m / N, n = m - cs * N;
-      const int cw = min(kXS, g.C - kXS * cs);
-      const int jj = min(j, cw / 32 - 1);  // past a 64-channel slice: reload a valid step
-      const int ks = (n * g.C + kXS * cs) / 32 + jj;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        a[i] = *reinterpret_cast<const uint4*>(
-            wfr + ((size_t)(((o0 >> 4) + i) * NKS + ks) * 64 + lane) * 8);
-    };
-    uint4 a0[4], a1[4], a2[4], a3[4];
-    load_a(0, 0, a0);
-    load_a(0, 1, a1);
-    load_a(0, 2, a2);
-    load_a(0, 3, a3);
-    auto kstep = [&](int buf, int j, const uint4 (&a)[4]) {
-      // lane: slot 16·pb + (lane & 15), chunk 4j + (lane >> 4), stored at chunk ^ (slot & 15)
-      const char* bb = bt + buf * kSlots * kXPitch + (lane & 15) * kXPitch +
-                       16 * ((4 * j + (lane >> 4)) ^ (lane & 15));
-#pragma unroll
-      for (int pb = 0; pb < kPB; ++pb) {
-        const bf16x8_t bv = as_frag(*reinterpret_cast<const uint4*>(bb + pb * 16 * kXPitch));
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          acc[i][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a[i]), bv, acc[i][pb], 0, 0, 0);
-      }
-    };
-    int produced = 0, consumed = 0;
-    auto consume = [&]() {
-      if (consumed >= produced) return;
-      const int mc = consumed++;  // from buffer mc & 1
-      if (dbg & 2) return;
-      const int cw = min(kXS, g.C - kXS * (mc / N));
-      const int mn = min(mc + 1, M - 1);
-      kstep(mc & 1, 0, a0);
-      load_a(mn, 0, a0);
-      kstep(mc & 1, 1, a1);
-      load_a(mn, 1, a1);
-      if (cw > 64) {
-        kstep(mc & 1, 2, a2);
-        kstep(mc & 1, 3, a3);
-      }
-      load_a(mn, 2, a2);
-      load_a(mn, 3, a3);
-    };
-    for (int m = 0; m <= M; ++m) {
-      if (m < M && m % N == 0) {  // window phase of slice m / N
-        consume();
-        __syncthreads();
-      }
-      consume();  // gather phase m (final phase at m == M)
-      __syncthreads();
-      if (m < M) ++produced;
-    }
-    // ---- epilogue: bf16(acc + bias[o]) staged as [o][slot] in the freed LDS ----
-    constexpr int kEP = kSlots * 2 + 16;
-    static_assert(kOT * kEP <= kXLdsRecW, "staged output tile fits the freed LDS");
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ol = 64 * wave + 16 * i + 4 * (lane >> 4) + r;
-        const float bv = bias ? bias[blk.z * kOT + ol] : 0.f;
-#pragma unroll
-        for (int pb = 0; pb < kPB; ++pb)
-          *reinterpret_cast<bf16_t*>(lds + ol * kEP + (16 * pb + (lane & 15)) * 2) =
-              f2bf(acc[i][pb][r] + bv);
-      }
-  } else {
-    // ================= producer waves: the B tiles, the window, the column rows ===========
-    const int pt = tid - 256, pw = pt >> 6;
-    const int chunk = lane & 15, grp = lane >> 4;
-    // window of slice cs: kWPix pixels × 16 chunks (only the slice's chunks are loaded)
-    auto stage_window = [&](int cs) {
-      const int cw8 = min(kXS, g.C - kXS * cs) / 8;
-      constexpr int TOT = kWPix * kXChunks, IT = (TOT + 255) / 256;
-      uint4 v[IT];
-#pragma unroll
-      for (int k = 0; k < IT; ++k) {
-        const int idx = pt + k * 256;
-        const int pix = idx >> 4, ch = idx & 15;
-        const int rr = pix / kWQ, qq = pix - rr * kWQ;
-        const int r = rlo + rr, q = qlo + qq;
-        const bool ok = idx < TOT && ch < cw8 && r >= 0 && r < g.H && q >= 0 && q < g.W;
-        v[k] = ld16_if(xb + ((size_t)r * g.W + q) * g.C + kXS * cs + 8 * ch, ok);
-      }
-      // overflow: novf entries × 16 chunks
-      uint4 ov[2];
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int idx = pt + 256 * k;
-        ov[k] = make_uint4(0u, 0u, 0u, 0u);
-        if (idx < novf * kXChunks && (idx & 15) < cw8) {
-          const int4 e = ovft[idx >> 4];
-          ov[k] = gather_global(g, xb, e.x, e.y, kXS * cs + 8 * (idx & 15), recw[e.z]);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < IT; ++k) {
-        const int idx = pt + k * 256;
-        if (idx < TOT) *reinterpret_cast<uint4*>(win + idx * 16) = v[k];
-      }
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int idx = pt + 256 * k;
-        if (idx < novf * kXChunks)
-          *reinterpret_cast<uint4*>(ovfd + idx * 16) = ov[k];
-      }
-    };
-    // gather macro step m (slice cs, tap n) into buffer m & 1 (and the column rows). The 7
-    // samples of a thread go in two batches (4 + 3): every record read of a batch, then every
-    // corner read, then the blends and stores, branch-free (an overflow sample's staged slice is
-    // read in the first corner's place, a sample outside the image blends to zero), so the LDS
-    // round trips of a batch overlap instead of chaining through each sample's B-tile store.
-    // A sample past the overflow area is rare: it is redone from global memory afterwards.
-    auto produce = [&](int m) {
-      const int cs = m / N, n = m - cs * N;
-      const int cw8 = min(kXS, g.C - kXS * cs) / 8;
-      char* bb = bt + (m & 1) * kSlots * kXPitch;
-      const bool cok = chunk < cw8;
-      constexpr int NU = kSlots / 16, GU = 4;
-      bool slow = false;
-#pragma unroll
-      for (int g0 = 0; g0 < NU; g0 += GU) {
-        int meta[GU];
-        float4 wv[GU];
-        uint4 ua[GU], ub[GU], uc[GU], ud[GU];
-#pragma unroll
-        for (int k = 0; k < GU; ++k) {
-          if (g0 + k < NU) {
-            const int slot = (g0 + k) * 16 + pw * 4 + grp;
-            meta[k] = recm[slot * kMaxN + n];
-            wv[k] = recw[slot * kMaxN + n];
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < GU; ++k) {
-          if (g0 + k < NU) {
-            const int mt = meta[k];
-            const int j = min(max(-2 - mt, 0), kXOvf - 1);
-            const char* wq = win + max(mt, 0) * kXPitch + chunk * 16;
-            ua[k] = *reinterpret_cast<const uint4*>(mt >= 0 ? wq : ovfd + j * kXPitch + chunk * 16);
-            ub[k] = *reinterpret_cast<const uint4*>(wq + kXPitch);
-            uc[k] = *reinterpret_cast<const uint4*>(wq + kWQ * kXPitch);
-            ud[k] = *reinterpret_cast<const uint4*>(wq + (kWQ + 1) * kXPitch);
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < GU; ++k) {
-          if (g0 + k < NU) {
-            const int slot = (g0 + k) * 16 + pw * 4 + grp;
-            const int mt = meta[k];
-            uint4 o = (dbg & 4) ? blend8s(wv[k], ua[k], ub[k], uc[k], ud[k])
-                                : blend8(wv[k], ua[k], ub[k], uc[k], ud[k]);
-            if (mt < 0) o = (mt == kMZero || -2 - mt >= kXOvf) ? make_uint4(0u, 0u, 0u, 0u) : ua[k];
-            if (dbg & 1) o = make_uint4(0u, 0u, 0u, 0u);
-            slow |= mt != kMZero && -2 - mt >= kXOvf;
-            *reinterpret_cast<uint4*>(bb + slot * kXPitch + 16 * (chunk ^ (slot & 15))) = o;
-            if (STORE && cok) {
-              const int h = h0 + slot / kTW, w = w0 + slot % kTW;
-              if (h < g.Ho && w < g.Wo)
-                __builtin_nontemporal_store(
-                    as_v(o), reinterpret_cast<v4u*>(colT + ((size_t)b * g.HW + (size_t)h * g.Wo + w) * g.K +
-                                                    n * g.C + kXS * cs + 8 * chunk));
-            }
-          }
-        }
-      }
-      if (__any(slow)) {  // more overflow samples than the area holds: global corners
-#pragma unroll 1
-        for (int it = 0; it < NU; ++it) {
-          const int slot = it * 16 + pw * 4 + grp;
-          const int mt = recm[slot * kMaxN + n];
-          if (mt == kMZero || -2 - mt < kXOvf || !cok) continue;
-          const int h = h0 + slot / kTW, w = w0 + slot % kTW;
-          const Tap t = sample_tap(g, off, b, 0, n, h * g.Wo + w);
-          const uint4 o = gather_global(g, xb, t.r0, t.c0, kXS * cs + 8 * chunk,
-                                        recw[slot * kMaxN + n]);
-          *reinterpret_cast<uint4*>(bb + slot * kXPitch + 16 * (chunk ^ (slot & 15))) = o;
-          if (STORE && h < g.Ho && w < g.Wo)
-            __builtin_nontemporal_store(
-                as_v(o), reinterpret_cast<v4u*>(colT + ((size_t)b * g.HW + (size_t)h * g.Wo + w) * g.K +
-                                                n * g.C + kXS * cs + 8 * chunk));
-        }
-      }
-    };
-    for (int m = 0; m <= M; ++m) {
-      if (m < M && m % N == 0) {  // window phase: every gather of the old slice is done
-        stage_window(m / N);
-        __syncthreads();
-      }
-      if (m < M) {  // gather phase m
-        produce(m);
-      }
-      __syncthreads();
-    }
-  }
-  __syncthreads();  // the consumers' staged output tile is complete
-  // 8-pixel runs: (output channel, tile row, half row), all 512 threads
-  constexpr int kEP = kSlots * 2 + 16;
-  const int ob0 = blk.z * kOT;
-  for (int u = tid; u < kOT * kTH * 2; u += kXT) {
-    const int half = u & 1, rest = u >> 1;
-    const int th = rest % kTH, ol = rest / kTH;
-    const int h = h0 + th, wc = w0 + 8 * half;
-    if (h >= g.Ho || wc >= g.Wo) continue;
-    const uint4 v = *reinterpret_cast<const uint4*>(lds + ol * kEP + (16 * th + 8 * half) * 2);
-    bf16_t* op = out + ((size_t)b * g.O + ob0 + ol) * g.HW + (size_t)h * g.Wo + wc;
-    if (wc + 8 <= g.Wo && ((reinterpret_cast<uintptr_t>(op) & 7) == 0)) {
-      *reinterpret_cast<uint2*>(op) = make_uint2(v.x, v.y);
-      *reinterpret_cast<uint2*>(op + 4) = make_uint2(v.z, v.w);
-    } else {
-      const unsigned e[4] = {v.x, v.y, v.z, v.w};
-      for (int j = 0; j < 8 && wc + j < g.Wo; ++j)
-        op[j] = (bf16_t)((e[j >> 1] >> (16 * (j & 1))) & 0xffffu);
-    }
-  }
-}
 
 // ---------------------------------------------------------------------------------------
 // ∂W with the columns recomputed (f2's backward half): ∂Wf[o][n·C + c] = Σ_p ∂out[o][p] ·
@@ -1009,421 +658,7 @@ __global__ __launch_bounds__(kDT) void dw_fused_bf16(Geo g, const bf16_t* __rest
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// ∂W with the columns recomputed, warp-specialised (r04; the same product as dw_fused_bf16:
-// ∂Wf[o][n·C + c] = Σ_p ∂out[o][p] · col[p][n·C + c], the autodiff of deform_conv.py:76).
-// r03's form re-staged a window and 1,008 sample records per 7 × 16 tile for only 16
-// channels (its waves waited 48 % of their cycles). Here a workgroup owns one column block
-// (128-channel slice cs, tap n) × 256 output channels and walks its share of the batch's
-// tiles; 8 waves:
-//   * consumers (waves 0-3, 64 output channels each, 4 × 8 accumulators of
-//     v_mfma_f32_16x16x32_bf16 over 128 columns): per tile 4 k steps of 32 pixel slots, the
-//     A fragments (8 consecutive slots of ∂out per lane) from global memory two k steps ahead,
-//     the B fragments from the [slot][channel] column tile by two ds_read_b64_tr_b16 (gfx950's
-//     transposing LDS read: the gather's natural 16-B stores, no register transpose);
-//   * producers (waves 4-7): the column tile of tile i (16 lanes per sample, one 8-channel
-//     chunk each: every corner read covers 16 distinct bank groups), while loading tile i+1's
-//     window and overflow corners and tile i+2's offsets into registers; after the mid-tile
-//     barrier they write those and compute tile i+2's sample records.
-// Two barriers per tile; the consumers split their 4 k steps around them. Per image group the
-// partial ∂W is written once (parts[grp]) and summed in a fixed order afterwards.
-constexpr int kYSl = 128;                                   // slots per tile, 4 k steps
-constexpr int kYOvf = 32;
-constexpr int kYLdsWin = 0;
-constexpr int kYLdsB = kYLdsWin + kWPix * kXPitch;          // 56,320
-constexpr int kYLdsRecW = kYLdsB + 2 * kYSl * kXPitch;      // + 65,536
-constexpr int kYLdsRecM = kYLdsRecW + 2 * kSlots * 16;
-constexpr int kYLdsOvfT = kYLdsRecM + 2 * kSlots * 4;
-constexpr int kYLdsOvfD = kYLdsOvfT + 2 * kYOvf * 16;
-constexpr int kYLdsCnt = kYLdsOvfD + kYOvf * kXPitch;
-constexpr int kYLds = kYLdsCnt + 16;
-static_assert(kYLds <= 160 * 1024, "one workgroup per CU");
-
-// chunk position of 16-B chunk c of slot s in the ∂W column tile: the 8 slots a 32-lane half
-// of a transposed read touches (s0..s0+3, s0+8..s0+11) get 8 distinct even XOR masks, so the
-// 32 8-byte words it reads sit in 32 distinct bank pairs; 16 lanes storing one slot's 16
-// chunks stay a permutation
-__device__ __forceinline__ int ychunk(int s, int c) {
-  return c ^ (2 * ((s & 3) | ((s >> 1) & 4)));
-}
-
-__global__ __launch_bounds__(kXT, 2) void dw_fused_bf16_ws(Geo g, const bf16_t* __restrict__ xT,
-                                                           const float* __restrict__ off,
-                                                           const bf16_t* __restrict__ gout,
-                                                           float* __restrict__ parts, int tw_n,
-                                                           int ngrp, int dbg) {
-  extern __shared__ __attribute__((aligned(16))) char dl[];
-  char* const win = dl + kYLdsWin;
-  char* const bt = dl + kYLdsB;
-  float4* const recw = reinterpret_cast<float4*>(dl + kYLdsRecW);  // [2][kSlots]
-  int* const recm = reinterpret_cast<int*>(dl + kYLdsRecM);         // [2][kSlots]
-  int4* const ovft = reinterpret_cast<int4*>(dl + kYLdsOvfT);       // [2][kYOvf]
-  char* const ovfd = dl + kYLdsOvfD;
-  int* const cnt = reinterpret_cast<int*>(dl + kYLdsCnt);           // [2]
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool consumer = wave < 4;
-  const Block3 blk = xcd_block();
-  const int N = g.N;
-  const int cs = blk.x / N, n = blk.x - cs * N;  // column block: slice cs, tap n
-  const int grp = blk.y;
-  const int cw8 = min(kXS, g.C - kXS * cs) / 8;  // 8-channel chunks in this slice
-  const int tiles_img = ((g.Ho + kTH - 1) / kTH) * tw_n;
-  const long Ttot = (long)g.B * tiles_img;
-  const int t_lo = (int)(Ttot * grp / ngrp), t_hi = (int)(Ttot * (grp + 1) / ngrp);
-  const int T = t_hi - t_lo;
-
-  struct TileId {
-    int b, h0, w0, rlo, qlo;
-  };
-  auto tile_id = [&](int i) {
-    TileId q;
-    const int t = t_lo + i;
-    const int ti = t % tiles_img;
-    q.b = t / tiles_img;
-    q.h0 = (ti / tw_n) * kTH;
-    q.w0 = (ti % tw_n) * kTW;
-    q.rlo = (int)floorf((float)q.w0 * (float)(g.H - 1) / (float)(g.Wo - 1)) - kMar;
-    q.qlo = (int)floorf((float)q.h0 * (float)(g.W - 1) / (float)(g.Ho - 1)) - kMar;
-    return q;
-  };
-
-  // zero both column tiles once (slots 112..127 and the chunks past the slice stay zero)
-  for (int i = tid * 16; i < 2 * kYSl * kXPitch; i += kXT * 16)
-    *reinterpret_cast<v4u*>(bt + i) = v4u{0u, 0u, 0u, 0u};
-  if (tid < 2) cnt[tid] = 0;
-
-  if (consumer) {
-    // ================= consumers =================
-    const int o0 = blk.z * kOT + 64 * wave;
-    f32x4 acc[4][8];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // A fragments: ∂out[b][o0 + 16·ob + (lane & 15)][slots 32·ks + 8·(lane >> 4) .. +7]
-    auto a_load = [&](int i, int ks, v4u (&a)[4]) {
-      const TileId q = tile_id(min(i, T - 1));
-      const int sl = 32 * ks + 8 * (lane >> 4);  // 8 slots of one tile row (kTW = 16)
-      const int h = q.h0 + sl / kTW, w = q.w0 + sl % kTW;
-      const bool rowok = i < T && sl < kSlots && h < g.Ho;
-      const int nv = rowok ? min(8, g.Wo - w) : 0;
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob) {
-        const int o = o0 + 16 * ob + (lane & 15);
-        const bf16_t* src = gout + ((size_t)q.b * g.O + o) * g.HW + (size_t)h * g.Wo + w;
-        v4u v = {0u, 0u, 0u, 0u};
-        if (nv >= 8 && ((reinterpret_cast<uintptr_t>(src) & 7) == 0)) {
-          const uint2 lo = *reinterpret_cast<const uint2*>(src);
-          const uint2 hi = *reinterpret_cast<const uint2*>(src + 4);
-          v = v4u{lo.x, lo.y, hi.x, hi.y};
-        } else if (nv > 0) {
-          unsigned e[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) e[j] = j < nv ? (unsigned)src[j] : 0u;
-          v = v4u{e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16)};
-        }
-        a[ob] = v;
-      }
-    };
-    // k step ks of the column tile in buffer buf: per 16-channel block cb two transposed reads
-    // (slots 8·(lane >> 4) + 0..3 and + 4..7 of the step, channel 16·cb + (lane & 15))
-    typedef __attribute__((address_space(3))) s16x4_t* lds_s16x4_p;
-    auto kstep = [&](int buf, int ks, const v4u (&a)[4]) {
-      const int gq = lane & 15, q = gq >> 2, p = gq & 3;
-      const int s0 = 32 * ks + 8 * (lane >> 4) + q;
-      const char* base = bt + buf * kYSl * kXPitch + 8 * (p & 1);
-#pragma unroll
-      for (int cb = 0; cb < 8; ++cb) {
-        const int c = 2 * cb + (p >> 1);
-        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_s16x4_p)(base + s0 * kXPitch + 16 * ychunk(s0, c)));
-        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_s16x4_p)(base + (s0 + 4) * kXPitch + 16 * ychunk(s0 + 4, c)));
-        const s16x8_t bv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-        for (int ob = 0; ob < 4; ++ob)
-          acc[ob][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              as_frag(a[ob]), __builtin_bit_cast(bf16x8_t, bv), acc[ob][cb], 0, 0, 0);
-      }
-    };
-    v4u aA[4], aB[4], aC[4];
-    a_load(0, 0, aA);
-    a_load(0, 1, aB);
-    __syncthreads();  // prologue 0: the zeroed counters
-    __syncthreads();  // prologue 1: records of tiles 0 and 1
-    __syncthreads();  // prologue 2: window and overflow of tile 0
-    // phase i: the producers gather tile i; the consumers run the MFMAs of tile i - 1
-    for (int i = 0; i <= T; ++i) {
-      const int ic = (dbg & 2) ? -1 : i - 1;
-      if (ic >= 0) {
-        a_load(ic, 2, aC);
-        kstep(ic & 1, 0, aA);
-        a_load(ic, 3, aA);
-        kstep(ic & 1, 1, aB);
-      }
-      __syncthreads();  // mid-tile
-      if (ic >= 0) {
-        a_load(ic + 1, 0, aB);
-        kstep(ic & 1, 2, aC);
-        a_load(ic + 1, 1, aC);
-        kstep(ic & 1, 3, aA);
-        // rotate: tile ic + 1's k steps 0 / 1 are in aB / aC
-        v4u t[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          t[k] = aA[k];
-          aA[k] = aB[k];
-          aB[k] = aC[k];
-          aC[k] = t[k];
-        }
-      }
-      __syncthreads();  // end of phase i
-    }
-    // partial ∂Wf[o][n·C + 128·cs + 16·cb + (lane & 15)] of this group; C/D: col = lane & 15,
-    // row = 4·(lane >> 4) + r
-    float* pg = parts + (size_t)grp * g.O * g.K;
-#pragma unroll
-    for (int ob = 0; ob < 4; ++ob)
-#pragma unroll
-      for (int cb = 0; cb < 8; ++cb) {
-        const int c = kXS * cs + 16 * cb + (lane & 15);
-        if (16 * cb < 8 * cw8) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int o = o0 + 16 * ob + 4 * (lane >> 4) + r;
-            pg[(size_t)o * g.K + n * g.C + c] = acc[ob][cb][r];
-          }
-        }
-      }
-  } else {
-    // ================= producers =================
-    const int pt = tid - 256, pw = pt >> 6;
-    const int chunk = lane & 15, sg = lane >> 4;
-    const bool cok = chunk < cw8;
-    // offsets (Δx, Δy) of tile i's slot pt (tap n), loaded ahead
-    auto off_load = [&](int i, float& dx, float& dy) {
-      dx = dy = 0.f;
-      if (i < T && pt < kSlots) {
-        const TileId q = tile_id(i);
-        const int h = q.h0 + pt / kTW, w = q.w0 + pt % kTW;
-        if (h < g.Ho && w < g.Wo) {
-          const float* ob = off + (size_t)q.b * g.J * g.HW + (size_t)h * g.Wo + w;
-          dx = ob[(size_t)n * g.HW];
-          dy = ob[(size_t)(N + n) * g.HW];
-        }
-      }
-    };
-    // records of tile i into buffer i & 1 (slot pt): the reference coordinate chain
-    auto rec_store = [&](int i, float dx, float dy) {
-      if (i >= T || pt >= kSlots) return;
-      const TileId q = tile_id(i);
-      const int h = q.h0 + pt / kTW, w = q.w0 + pt % kTW;
-      int meta = kMZero;
-      float4 wv = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (h < g.Ho && w < g.Wo) {
-        float iy, ix;
-        ref_coord(h, w, dx, dy, g, iy, ix);
-        const Tap t = make_tap(iy, ix, g);
-        if (t.ok) {
-          const float gr = 1.0f - t.fr, gc = 1.0f - t.fc;
-          wv = make_float4(gr * gc, gr * t.fc, t.fr * gc, t.fr * t.fc);
-          const int rr = t.r0 - q.rlo, qq = t.c0 - q.qlo;
-          if (rr >= 0 && rr + 1 < kWR && qq >= 0 && qq + 1 < kWQ) {
-            meta = rr * kWQ + qq;
-          } else {
-            const int j = atomicAdd(&cnt[i & 1], 1);
-            meta = -2 - j;
-            if (j < kYOvf) ovft[(i & 1) * kYOvf + j] = make_int4(t.r0, t.c0, pt, 0);
-          }
-        }
-      }
-      recm[(i & 1) * kSlots + pt] = meta;
-      recw[(i & 1) * kSlots + pt] = wv;
-    };
-    constexpr int TOT = kWPix * kXChunks, IT = (TOT + 255) / 256;
-    auto win_load = [&](int i, uint4 (&v)[IT]) {
-      const TileId q = tile_id(min(i, T - 1));
-      const bf16_t* xb = xT + (size_t)q.b * g.HWi * g.C + kXS * cs;
-#pragma unroll
-      for (int k = 0; k < IT; ++k) {
-        const int idx = pt + k * 256;
-        const int pix = idx >> 4, ch = idx & 15;
-        const int rr = pix / kWQ, qq = pix - rr * kWQ;
-        const int r = q.rlo + rr, qc = q.qlo + qq;
-        const bool ok = i < T && idx < TOT && ch < cw8 && r >= 0 && r < g.H && qc >= 0 && qc < g.W;
-        v[k] = ld16_if(xb + ((size_t)r * g.W + qc) * g.C + 8 * ch, ok);
-      }
-    };
-    auto win_store = [&](const uint4 (&v)[IT]) {
-#pragma unroll
-      for (int k = 0; k < IT; ++k) {
-        const int idx = pt + k * 256;
-        if (idx < TOT) *reinterpret_cast<uint4*>(win + idx * 16) = v[k];
-      }
-    };
-    // overflow column slices of tile i: its novf entries × 16 chunks, two units per thread;
-    // the corners are loaded in one half of a phase (ovf_load) and blended into the overflow
-    // area in the other (ovf_store), so their latency hides under the gather
-    struct Ovf {
-      uint4 a, b, c, d;
-      float4 wv;
-    };
-    auto ovf_load = [&](int i, Ovf (&ov)[2]) {
-      const int novf = i < T ? min(cnt[i & 1], kYOvf) : 0;
-      const TileId q = tile_id(min(i, T - 1));
-      const bf16_t* xb = xT + (size_t)q.b * g.HWi * g.C;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int idx = pt + 256 * k;
-        const bool on = idx < novf * kXChunks && (idx & 15) < cw8;
-        const int4 e = on ? ovft[(i & 1) * kYOvf + (idx >> 4)] : make_int4(0, 0, 0, 0);
-        ov[k].wv = on ? recw[(i & 1) * kSlots + e.z] : make_float4(0.f, 0.f, 0.f, 0.f);
-        const int r0 = e.x, c0 = e.y;
-        const bool r0ok = r0 >= 0, r1ok = r0 + 1 < g.H, c0ok = c0 >= 0, c1ok = c0 + 1 < g.W;
-        const long rs = (long)g.W * g.C;
-        const bf16_t* p00 = xb + ((long)r0 * g.W + c0) * (long)g.C + kXS * cs + 8 * (idx & 15);
-        ov[k].a = ld16_if(p00, on && r0ok && c0ok);
-        ov[k].b = ld16_if(p00 + g.C, on && r0ok && c1ok);
-        ov[k].c = ld16_if(p00 + rs, on && r1ok && c0ok);
-        ov[k].d = ld16_if(p00 + rs + g.C, on && r1ok && c1ok);
-      }
-    };
-    auto ovf_store = [&](int i, const Ovf (&ov)[2]) {
-      const int novf = i < T ? min(cnt[i & 1], kYOvf) : 0;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int idx = pt + 256 * k;
-        if (idx < novf * kXChunks)
-          *reinterpret_cast<uint4*>(ovfd + idx * 16) = blend8(ov[k].wv, ov[k].a, ov[k].b, ov[k].c, ov[k].d);
-      }
-    };
-    // the column tile of tile i into buffer i & 1: sample (slot) per 16 lanes, chunk per lane;
-    // batched and branch-free like the forward's producers (two batches of samples: record
-    // reads, corner reads, blends + stores), the rare samples past the overflow area redone
-    // from global memory afterwards
-    auto produce = [&](int i) {
-      const TileId q = tile_id(i);
-      const bf16_t* xb = xT + (size_t)q.b * g.HWi * g.C;
-      char* bb = bt + (i & 1) * kYSl * kXPitch;
-      const int* rm = recm + (i & 1) * kSlots;
-      const float4* rw = recw + (i & 1) * kSlots;
-      constexpr int NU = kSlots / 16, GU = 2;
-      bool slow = false;
-#pragma unroll
-      for (int g0 = 0; g0 < NU; g0 += GU) {
-        int meta[GU];
-        float4 wv[GU];
-        uint4 ua[GU], ub[GU], uc[GU], ud[GU];
-#pragma unroll
-        for (int k = 0; k < GU; ++k) {
-          if (g0 + k < NU) {
-            const int slot = (g0 + k) * 16 + pw * 4 + sg;
-            meta[k] = rm[slot];
-            wv[k] = rw[slot];
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < GU; ++k) {
-          if (g0 + k < NU) {
-            const int mt = meta[k];
-            const int j = min(max(-2 - mt, 0), kYOvf - 1);
-            const char* wq = win + max(mt, 0) * kXPitch + chunk * 16;
-            ua[k] = *reinterpret_cast<const uint4*>(mt >= 0 ? wq : ovfd + j * kXPitch + chunk * 16);
-            ub[k] = *reinterpret_cast<const uint4*>(wq + kXPitch);
-            uc[k] = *reinterpret_cast<const uint4*>(wq + kWQ * kXPitch);
-            ud[k] = *reinterpret_cast<const uint4*>(wq + (kWQ + 1) * kXPitch);
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < GU; ++k) {
-          if (g0 + k < NU) {
-            const int slot = (g0 + k) * 16 + pw * 4 + sg;
-            const int mt = meta[k];
-            uint4 o = (dbg & 4) ? blend8s(wv[k], ua[k], ub[k], uc[k], ud[k])
-                                : blend8(wv[k], ua[k], ub[k], uc[k], ud[k]);
-            if (mt < 0) o = (mt == kMZero || -2 - mt >= kYOvf) ? make_uint4(0u, 0u, 0u, 0u) : ua[k];
-            if (dbg & 1) o = make_uint4(0u, 0u, 0u, 0u);
-            slow |= mt != kMZero && -2 - mt >= kYOvf;
-            *reinterpret_cast<uint4*>(bb + slot * kXPitch + 16 * ychunk(slot, chunk)) = o;
-          }
-        }
-      }
-      if (__any(slow)) {  // past the overflow area: corners from global memory
-#pragma unroll 1
-        for (int it = 0; it < NU; ++it) {
-          const int slot = it * 16 + pw * 4 + sg;
-          const int mt = rm[slot];
-          if (mt == kMZero || -2 - mt < kYOvf || !cok) continue;
-          const int h = q.h0 + slot / kTW, w = q.w0 + slot % kTW;
-          const Tap t = sample_tap(g, off, q.b, 0, n, h * g.Wo + w);
-          *reinterpret_cast<uint4*>(bb + slot * kXPitch + 16 * ychunk(slot, chunk)) =
-              gather_global(g, xb, t.r0, t.c0, kXS * cs + 8 * chunk, rw[slot]);
-        }
-      }
-    };
-    uint4 wr[IT];
-    Ovf ov[2];
-    float dx0, dy0, dx1, dy1;
-    off_load(0, dx0, dy0);
-    off_load(1, dx1, dy1);
-    __syncthreads();  // prologue 0: the zeroed counters
-    rec_store(0, dx0, dy0);
-    rec_store(1, dx1, dy1);
-    win_load(0, wr);
-    __syncthreads();  // prologue 1: records of tiles 0 and 1
-    ovf_load(0, ov);
-    win_store(wr);
-    ovf_store(0, ov);
-    __syncthreads();  // prologue 2: window and overflow of tile 0
-    for (int i = 0; i <= T; ++i) {
-      float dx2 = 0.f, dy2 = 0.f;
-      if (i < T) {
-        win_load(i + 1, wr);
-        ovf_load(i + 1, ov);
-        off_load(i + 2, dx2, dy2);
-        if (pt == 0) cnt[i & 1] = 0;  // tile i's count was last read by its overflow staging
-        produce(i);
-      }
-      __syncthreads();  // mid-tile: tile i's window, records and overflow no longer read
-      if (i < T) {
-        rec_store(i + 2, dx2, dy2);
-        win_store(wr);
-        ovf_store(i + 1, ov);
-      }
-      __syncthreads();  // end of phase i
-    }
-  }
-}
-
 }  // namespace
-
-// r04 diagnosis (temporary): DCN_WS_DBG bits: 1 producers skip the gather, 2 consumers skip the
-// MFMAs, 4 scalar blend, 8 16-B column stores
-int ws_dbg() {
-  static const int v = [] {
-    const char* e = std::getenv("DCN_WS_DBG");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
-}
-
-// The > 64 KB dynamic-LDS attribute of a kernel, per device: set once per (kernel, device id),
-// recorded only after it succeeded (a failure is returned and retried on the next call).
-hipError_t set_lds_attr(const void* fn, int bytes) {
-  static std::mutex mu;
-  static std::vector<std::pair<const void*, int>> done;
-  int dev = 0;
-  const hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  std::lock_guard<std::mutex> lk(mu);
-  for (const auto& d : done)
-    if (d.first == fn && d.second == dev) return hipSuccess;
-  const hipError_t r = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-  if (r == hipSuccess) done.emplace_back(fn, dev);
-  return r;
-}
 
 bool fused_fwd_bf16_ok(const Geo& g) {
   const long lim = 1l << 31;
@@ -1449,22 +684,6 @@ hipError_t launch_fused_fwd_bf16(const Geo& g, const bf16_t* xT, const float* of
                      wfr, g.O, g.K);
   const int th_n = (g.Ho + kTH - 1) / kTH, tw_n = (g.Wo + kTW - 1) / kTW;
   const dim3 grid(th_n * tw_n, g.B, g.O / kOT);
-  static const bool ws_form = [] {  // r04 A/B (temporary): DCN_FWD_WS=0 runs the r03 kernel
-    const char* e = std::getenv("DCN_FWD_WS");
-    return !(e && e[0] == '0');
-  }();
-  if (ws_form) {
-    const hipError_t e = set_lds_attr(reinterpret_cast<const void*>(
-        colT ? &fwd_fused_bf16_ws<true> : &fwd_fused_bf16_ws<false>), kXLds);
-    if (e != hipSuccess) return e;
-    if (colT)
-      hipLaunchKernelGGL(fwd_fused_bf16_ws<true>, grid, dim3(kXT), kXLds, s, g, xT, off, wfr, bias,
-                         out, colT, tw_n, ws_dbg());
-    else
-      hipLaunchKernelGGL(fwd_fused_bf16_ws<false>, grid, dim3(kXT), kXLds, s, g, xT, off, wfr,
-                         bias, out, colT, tw_n, ws_dbg());
-    return hipGetLastError();
-  }
   if (colT)
     hipLaunchKernelGGL(fwd_fused_bf16<true>, grid, dim3(256), 0, s, g, xT, off, wfr, bias, out,
                        colT, tw_n);
@@ -1480,43 +699,32 @@ bool fused_dw_bf16_ok(const Geo& g) {
          (long)g.B * g.O * g.HW < (1l << 40);
 }
 
-// image groups of the ∂W partials. The warp-specialised kernel splits the batch's tiles (not
-// images) into groups so that (slices × taps × groups) workgroups about fill the 256 CUs, one
-// per CU, every group at least one tile
-int fused_dw_bf16_groups(const Geo& g) {
-  static const bool ws_form = [] {
-    const char* e = std::getenv("DCN_DW_WS");
-    return !(e && e[0] == '0');
-  }();
-  if (!ws_form) return std::min(16, g.B);
-  const int cols = ((g.C + kXS - 1) / kXS) * g.N * (g.O / kOT);
-  const long tiles = (long)g.B * ((g.Ho + kTH - 1) / kTH) * ((g.Wo + kTW - 1) / kTW);
-  return (int)std::max(1L, std::min<long>(tiles, std::max(1, 256 / cols)));
-}
+int fused_dw_bf16_groups(const Geo& g) { return std::min(16, g.B); }
 
 hipError_t launch_fused_dw_bf16(const Geo& g, const bf16_t* xT, const float* off,
                                 const bf16_t* gout, float* parts, hipStream_t s) {
   if (!fused_dw_bf16_ok(g)) return hipErrorInvalidValue;
+  // the >64 KB dynamic-LDS attribute is per device: set once per device id, recorded only
+  // after it succeeded (a failure is returned and retried on the next call)
+  static std::mutex mu;
+  static std::vector<char> attr_set;
+  int dev = 0;
   {
-    const hipError_t e = set_lds_attr(reinterpret_cast<const void*>(&dw_fused_bf16<0>), kDLds);
+    const hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
   }
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if ((int)attr_set.size() <= dev) attr_set.resize(dev + 1, 0);
+    if (!attr_set[dev]) {
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dw_fused_bf16<0>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, kDLds);
+      if (e != hipSuccess) return e;
+      attr_set[dev] = 1;
+    }
+  }
+  const int ng = fused_dw_bf16_groups(g);
   const int tw_n = (g.Wo + kTW - 1) / kTW;
-  static const bool ws_form = [] {  // r04 A/B (temporary): DCN_DW_WS=0 runs the r03 kernel
-    const char* e = std::getenv("DCN_DW_WS");
-    return !(e && e[0] == '0');
-  }();
-  if (ws_form) {
-    const hipError_t e = set_lds_attr(reinterpret_cast<const void*>(&dw_fused_bf16_ws), kYLds);
-    if (e != hipSuccess) return e;
-    const int ng = fused_dw_bf16_groups(g);
-    const int nslices = (g.C + kXS - 1) / kXS;
-    const dim3 grid(nslices * g.N, ng, g.O / kOT);
-    hipLaunchKernelGGL(dw_fused_bf16_ws, grid, dim3(kXT), kYLds, s, g, xT, off, gout, parts, tw_n,
-                       ng, ws_dbg());
-    return hipGetLastError();
-  }
-  const int ng = std::min(16, g.B);
   const dim3 grid(g.C / kDC, ng, g.O / kOT);
   hipLaunchKernelGGL(dw_fused_bf16<0>, grid, dim3(kDT), kDLds, s, g, xT, off, gout, parts, tw_n,
                      ng);

@@ -14,6 +14,7 @@
 #include <algorithm>
 
 #include "dcn_device.h"
+#include <type_traits>
 
 namespace dcn {
 
@@ -764,6 +765,94 @@ __global__ __launch_bounds__(256) void offset_wgrad_mfma_m1(Geo g, const float* 
     v += __shfl_xor(v, 16);
     v += __shfl_xor(v, 32);
     if (r < NV && q == 0) pp[(size_t)(cw + n) * TJ + 160 + r] = v;
+  }
+}
+
+// The same ∂W_off partials on v_mfma_f32_32x32x2f32 (C % 128 == 0 besides m1's conditions): a
+// wave owns 32 channels (M = 32) over the 160 MFMA tap columns as 5 N-tiles of 32, K = 2
+// pixels per step, the last NV <= 2 columns on the VALU. Per step a wave reads 5 + 2 LDS
+// words per lane for 5 MFMAs (m1: 10 + 2 for 10 16x16x4 MFMAs of the same flops), and a
+// workgroup (4 waves, 128 channels) stages each ∂offset chunk for twice m1's channels. Lane
+// (i = l&31, k = l>>5): A = xT[pixel 2ks+k][channel cw+i]; tile T: B = ∂offset at tap column
+// 32T+i of pixel 2ks+k; D[row][col] in register r of lane col + 32·hi, row = drow(r, hi).
+__global__ __launch_bounds__(256) void offset_wgrad_mfma_m2(Geo g, const float* __restrict__ xT,
+                                                           const float* __restrict__ goff,
+                                                           float* __restrict__ part, int rowsB,
+                                                           int cpi, int grp0, int cpb) {
+  extern __shared__ float S[];
+  const int grp = grp0 + blockIdx.x;
+  const int SW = g.W + (g.kw - 1) * g.dw;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = lane & 31, k = lane >> 5;
+  const int TJ = g.J * g.kh * g.kw, NV = TJ - 160;
+  int bv0[5], vv0[2];
+#pragma unroll
+  for (int t = 0; t < 5; ++t) bv0[t] = k * g.J + g_toff(g, 32 * t + i, SW);
+#pragma unroll
+  for (int r = 0; r < 2; ++r) vv0[r] = k * g.J + g_toff(g, 160 + r, SW);  // 0 past TJ
+  const int cw = blockIdx.y * 128 + 32 * w;
+  f32x16 acc[5];
+#pragma unroll
+  for (int t = 0; t < 5; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  float va[2] = {0.f, 0.f};
+  for (int cc = 0; cc < cpb; ++cc) {
+    const int chunk = grp * cpb + cc;
+    const int b = chunk / cpi, y0 = (chunk - b * cpi) * rowsB;
+    const int nrows = min(rowsB, g.H - y0);
+    if (cc) __syncthreads();  // the previous chunk's LDS reads are done
+    stage_goff(g, goff, b, y0, nrows + (g.kh - 1) * g.dh, SW, S);
+    __syncthreads();
+    constexpr int kPf = 4;
+    const int nq = g.W / 2, nsteps = nrows * nq;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(xT + ((size_t)b * g.H + y0) * g.W * g.C), 0,
+        (int)((size_t)max(nrows, 1) * g.W * g.C * 4), 0x00020000);
+    const unsigned lane_x = (unsigned)((k * g.C + cw + i) * 4);
+    const int step_x = 8 * g.C, last = (nsteps - 1) * step_x;
+    auto ld = [&](int so) {
+      return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, lane_x, so, 0));
+    };
+    float ring[kPf];
+    int lo = 0;
+#pragma unroll
+    for (int d = 0; d < kPf; ++d, lo += step_x) ring[d] = ld(min(lo, last));
+    int sb = 0, sx = 0;
+    const int row_skip = (SW - g.W) * g.J;
+    for (int ks0 = 0; ks0 < nsteps; ks0 += kPf) {
+#pragma unroll
+      for (int d = 0; d < kPf; ++d) {
+        const unsigned keep = ks0 + d < nsteps ? 0xffffffffu : 0u;  // wave-uniform
+        const float a = __uint_as_float(__float_as_uint(ring[d]) & keep);
+        float bv[5], vb[2];
+#pragma unroll
+        for (int t = 0; t < 5; ++t) bv[t] = __uint_as_float(__float_as_uint(S[sb + bv0[t]]) & keep);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) vb[r] = __uint_as_float(__float_as_uint(S[sb + vv0[r]]) & keep);
+        sb += 2 * g.J;
+        if (++sx == nq) sx = 0, sb += row_skip;
+#pragma unroll
+        for (int t = 0; t < 5; ++t) acc[t] = mfma32(a, bv[t], acc[t]);
+        va[0] = fmaf(a, vb[0], va[0]);
+        va[1] = fmaf(a, vb[1], va[1]);
+        ring[d] = ld(min(lo, last));
+        lo += step_x;
+        __builtin_amdgcn_sched_barrier(0);  // the load stays kPf steps ahead (see m1)
+      }
+    }
+  }  // chunks
+  float* pp = part + (size_t)grp * g.C * TJ;
+#pragma unroll
+  for (int t = 0; t < 5; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) pp[(size_t)(cw + drow(r, k)) * TJ + 32 * t + i] = acc[t][r];
+  // the VALU columns: lane (i, k) holds channel cw+i over pixels ≡ k (mod 2)
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    float v = va[r];
+    v += __shfl_xor(v, 32);
+    if (r < NV && k == 0) pp[(size_t)(cw + i) * TJ + 160 + r] = v;
   }
 }
 
@@ -1737,11 +1826,13 @@ __global__ __launch_bounds__(256) void offset_bwd_generic(Geo g, const float* __
 // order: deterministic.
 // ---------------------------------------------------------------------------
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-constexpr int kXtCP = 20, kXtRWmax = 64, kXtWts = 9 * 64 * 4 + 9 * 4 * 8;  // floats
+constexpr int kXtCP = 20, kXtRWmax = 64, kXtWts = 9 * 64 * 4 + 3 * 64 * 2;  // floats
 
 // per 16-channel chunk cg, kXtWts floats: B[t][lane][s] = w_off[j = lane&15][c][t] with
-// c = 16cg + 4(lane>>4) + s, then V[t][g][2s + jj] = w_off[16 + jj][16cg + 4g + s][t]
-// (0 for j >= J)
+// c = 16cg + 4(lane>>4) + s, then the VALU weights of offset channels 16-17 one per lane:
+// V[ty][lane][r] = w_off[16 + jj][16cg + 4g + s][3ty + tx] for lane = 16g + i, vi = 16r + i =
+// 8tx + 2s + jj (0 for vi >= 24 or j >= J); the kernel broadcasts lane i of its 16-lane group
+// (DPP row_newbcast) instead of reading the same weights from LDS in every lane
 __global__ __launch_bounds__(256) void woff_to_f32frag(const float* __restrict__ w,
                                                        float* __restrict__ wf, int J, int C) {
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -1754,12 +1845,23 @@ __global__ __launch_bounds__(256) void woff_to_f32frag(const float* __restrict__
     j = lane & 15;
     c = 16 * cg + 4 * (lane >> 4) + s;
   } else {
-    const int v = k - 9 * 256, jj = v & 1, s = (v >> 1) & 3, gg = (v >> 3) & 3;
-    t = v >> 5;
-    j = 16 + jj;
-    c = 16 * cg + 4 * gg + s;
+    const int v = k - 9 * 256, r = v & 1, lane = (v >> 1) & 63, ty = v >> 7;
+    const int vi = 16 * r + (lane & 15), tx = vi >> 3, s = (vi >> 1) & 3, jj = vi & 1;
+    t = 3 * ty + tx;
+    j = vi < 24 ? 16 + jj : J;
+    c = 16 * cg + 4 * (lane >> 4) + s;
   }
   wf[i] = j < J ? w[((size_t)j * C + c) * 9 + t] : 0.f;
+}
+
+// weight VI of the lane's 16-lane group: lane VI % 16 of the group's row of vv (DPP
+// row_newbcast, gfx90a+), component VI / 16
+template <int VI>
+__device__ __forceinline__ float row_bcast_w(float2 vv) {
+  static_assert(VI >= 0 && VI < 32, "two weights per lane");
+  const float v = VI < 16 ? vv.x : vv.y;
+  return __int_as_float(
+      __builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + (VI & 15), 0xf, 0xf, true));
 }
 
 template <int ROWS>  // output rows per workgroup; 4 * ROWS waves
@@ -1880,28 +1982,34 @@ offset_conv_fwd_mfma_xt(Geo g, const float* __restrict__ x, const float* __restr
     }
     const float* LB = L + WIN;
     if (has_tile && live) {
-#pragma unroll 1
-      for (int ty = 0; ty < 3; ++ty)
 #pragma unroll
-      for (int tx = 0; tx < 3; ++tx) {
-        const int t = ty * 3 + tx;
-        const float4 bw = *reinterpret_cast<const float4*>(LB + (t * 64 + lane) * 4);
-        const float4 v0 = *reinterpret_cast<const float4*>(LB + 9 * 256 + (t * 4 + gq) * 8);
-        const float4 v1 = *reinterpret_cast<const float4*>(LB + 9 * 256 + (t * 4 + gq) * 8 + 4);
-        const float4 a =
-            *reinterpret_cast<const float4*>(L + ((ra + ty) * RW + ca + tx) * CP + 4 * gq);
-        acc = mfma16(a.x, bw.x, acc);
-        acc = mfma16(a.y, bw.y, acc);
-        acc = mfma16(a.z, bw.z, acc);
-        acc = mfma16(a.w, bw.w, acc);
-        e0 = fmaf(a.x, v0.x, e0);
-        e1 = fmaf(a.x, v0.y, e1);
-        e0 = fmaf(a.y, v0.z, e0);
-        e1 = fmaf(a.y, v0.w, e1);
-        e0 = fmaf(a.z, v1.x, e0);
-        e1 = fmaf(a.z, v1.y, e1);
-        e0 = fmaf(a.w, v1.z, e0);
-        e1 = fmaf(a.w, v1.w, e1);
+      for (int ty = 0; ty < 3; ++ty) {
+        // this row of taps' 24 VALU weights of the lane's group, lane i of the group holding
+        // weights i and 16 + i (one 8-B read per row of taps, not two 16-B reads per tap)
+        const float2 vv = *reinterpret_cast<const float2*>(LB + 9 * 256 + (ty * 64 + lane) * 2);
+        auto tap = [&](auto TX) __attribute__((always_inline)) {
+          constexpr int tx = decltype(TX)::value;
+          const int t = ty * 3 + tx;
+          const float4 bw = *reinterpret_cast<const float4*>(LB + (t * 64 + lane) * 4);
+          const float4 a =
+              *reinterpret_cast<const float4*>(L + ((ra + ty) * RW + ca + tx) * CP + 4 * gq);
+          acc = mfma16(a.x, bw.x, acc);
+          acc = mfma16(a.y, bw.y, acc);
+          acc = mfma16(a.z, bw.z, acc);
+          acc = mfma16(a.w, bw.w, acc);
+          // weight (s, jj) of tap tx: vi = 8tx + 2s + jj
+          e0 = fmaf(a.x, row_bcast_w<8 * tx + 0>(vv), e0);
+          e1 = fmaf(a.x, row_bcast_w<8 * tx + 1>(vv), e1);
+          e0 = fmaf(a.y, row_bcast_w<8 * tx + 2>(vv), e0);
+          e1 = fmaf(a.y, row_bcast_w<8 * tx + 3>(vv), e1);
+          e0 = fmaf(a.z, row_bcast_w<8 * tx + 4>(vv), e0);
+          e1 = fmaf(a.z, row_bcast_w<8 * tx + 5>(vv), e1);
+          e0 = fmaf(a.w, row_bcast_w<8 * tx + 6>(vv), e0);
+          e1 = fmaf(a.w, row_bcast_w<8 * tx + 7>(vv), e1);
+        };
+        tap(std::integral_constant<int, 0>());
+        tap(std::integral_constant<int, 1>());
+        tap(std::integral_constant<int, 2>());
       }
     }
     // unconditional: past the last chunk it stages a re-loaded chunk nobody reads
@@ -2068,9 +2176,14 @@ hipError_t launch_offset_bwd_chunk(const Geo& g, const void* xT, bool xT_bf16, c
     else w4 ? wg(offset_wgrad_mfma<3, true, bf16_t>, xb) : wg(offset_wgrad_mfma<3, false, bf16_t>, xb);
   } else if (wgrad_m1(g)) {
     const int cpb = wgrad_cpb(g, ms);
-    hipLaunchKernelGGL(offset_wgrad_mfma_m1, dim3(nb * ms.cpi / cpb, g.C / 64), dim3(256),
-                       ms.lds_w, s, g, static_cast<const float*>(xT), goff, goffT, ms.rowsB,
-                       ms.cpi, b0 * ms.cpi / cpb, cpb);
+    if (g.C % 128 == 0)
+      hipLaunchKernelGGL(offset_wgrad_mfma_m2, dim3(nb * ms.cpi / cpb, g.C / 128), dim3(256),
+                         ms.lds_w, s, g, static_cast<const float*>(xT), goff, goffT, ms.rowsB,
+                         ms.cpi, b0 * ms.cpi / cpb, cpb);
+    else
+      hipLaunchKernelGGL(offset_wgrad_mfma_m1, dim3(nb * ms.cpi / cpb, g.C / 64), dim3(256),
+                         ms.lds_w, s, g, static_cast<const float*>(xT), goff, goffT, ms.rowsB,
+                         ms.cpi, b0 * ms.cpi / cpb, cpb);
   } else {
     const float* xf = static_cast<const float*>(xT);
     if (NT <= 4) w4 ? wg(offset_wgrad_mfma<1, true>, xf) : wg(offset_wgrad_mfma<1, false>, xf);

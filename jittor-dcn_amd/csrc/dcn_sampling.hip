@@ -747,8 +747,8 @@ __global__ __launch_bounds__(256) void bins_emit(Geo g, int nch, int NB,
 // ∂offset of a sample is computed once, by the block that reads its bin (bin row R0 is
 // read by two tiles: the lower one, w >= 1, owns it), from the tile's (kTR+1) x (kTQ+1)
 // xT window (rows R0..R0+kTR, columns Q0-1..Q0+kTQ-1) staged in LDS (corners outside the
-// image: zero). ∂offset uses offgrad_cl's op order (per-lane channel sums, fixed xor
-// tree). Used for deform_groups == 1, C % 4 == 0, C <= 256.
+// image: zero). ∂offset uses offgrad_cl's op order (per-lane channel sums, then wave_sum's
+// fixed xor tree, taken for the 2U sums of a batch at once by wave_sum8). Used for deform_groups == 1, C % 4 == 0, C <= 256.
 // ---------------------------------------------------------------------------
 
 // Packed fp32 (v_pk_fma_f32 / v_pk_add_f32 / v_pk_mul_f32: two lanes' elements per
@@ -797,6 +797,7 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
                                                            float* __restrict__ cpart, int b0,
                                                            int tq_n) {
   constexpr int kC2iThreads = (kTR + 1) * 64, WR = kTR + 1, WQ = kTQ + 1;
+  static_assert(U <= 4, "wave_sum8 takes at most 8 ∂offset sums per batch");
   // float4 slots: a zero row (window row -1: wave 0's ∂offset reads it only at image row
   // -1, so no select), the xT window; then the upper rows
   constexpr int ZR = WQ * 64, WIN = WR * WQ * 64, UPR = kTR * kTQ * 64;
@@ -942,6 +943,7 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
             }
           }
           issue(i + U < hi ? i + U : hi);  // next batch of this bin, else the next bin's first
+          float dv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // per-lane ∂offset parts
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             if (i + u >= hi) break;
@@ -967,13 +969,23 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
               const float4 bq = cB ? w4[64] : z4;
               const float4 cq = w4[WQ * 64];
               const float4 d = cB ? w4[(WQ + 1) * 64] : z4;
-              float diy = 0.f, dix = 0.f;
-              acc_dgrad4p(fr, fc, gv[u], a, bq, cq, d, diy, dix);
-              diy = wave_sum(diy);
-              dix = wave_sum(dix);
-              const bool mine = lane == i + u - seg;
-              oy = mine ? diy : oy;
-              ox = mine ? dix : ox;
+              acc_dgrad4p(fr, fc, gv[u], a, bq, cq, d, dv[2 * u], dv[2 * u + 1]);
+              // opaque to hipcc's SLP vectorizer: it would pair the two scalar FMA chains
+              // into packed FMAs behind moves (more VALU, not less)
+              asm("" : "+v"(dv[2 * u]), "+v"(dv[2 * u + 1]));
+            }
+          }
+          if (drow) {  // the batch's 2U wave sums in one tree (wave_sum's order: same bits)
+            const float sd = wave_sum8(dv, lane);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {  // no branch: a sample past hi selects no lane
+              const float sy_u =
+                  __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sd), wave_sum8_lane(2 * u)));
+              const float sx_u = __int_as_float(
+                  __builtin_amdgcn_readlane(__float_as_int(sd), wave_sum8_lane(2 * u + 1)));
+              const bool mine = lane == i + u - seg && i + u < hi;
+              oy = mine ? sy_u : oy;
+              ox = mine ? sx_u : ox;
             }
           }
         }
@@ -1499,7 +1511,9 @@ static void launch_k5_fused(const Geo& g, const XT* xT, const BinsWs& P, const G
   // fold): fp32 U = 2 at 6 waves/SIMD spills 24 B: 0.669-0.673 ms; U = 2 at 5: 0.571;
   // U = 3 at 5 (95 VGPRs): 0.564-0.568; U = 3 at 4: 0.565. bf16 U = 3 at 5: 0.123-0.124,
   // U = 4 at 5: 0.123, U = 3 at 6 (spills): 0.146.
-  launch_c2i<3, 4, 5, 7>(g, xT, P, gcolT, gxT, goff, b0, nb, s);
+  // r04: 4 waves/SIMD (128 VGPRs): two 8-wave workgroups per CU is all that 5 allowed too, and
+  // the batched ∂offset tree (wave_sum8) spills at 5 in the fp32 form
+  launch_c2i<3, 4, 4, 7>(g, xT, P, gcolT, gxT, goff, b0, nb, s);
 }
 
 hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, const float* off,
