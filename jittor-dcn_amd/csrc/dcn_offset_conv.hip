@@ -14,7 +14,6 @@
 #include <algorithm>
 
 #include "dcn_device.h"
-#include <type_traits>
 
 namespace dcn {
 
@@ -1826,13 +1825,11 @@ __global__ __launch_bounds__(256) void offset_bwd_generic(Geo g, const float* __
 // order: deterministic.
 // ---------------------------------------------------------------------------
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-constexpr int kXtCP = 20, kXtRWmax = 64, kXtWts = 9 * 64 * 4 + 3 * 64 * 2;  // floats
+constexpr int kXtCP = 20, kXtRWmax = 64, kXtWts = 9 * 64 * 4 + 9 * 4 * 8;  // floats
 
 // per 16-channel chunk cg, kXtWts floats: B[t][lane][s] = w_off[j = lane&15][c][t] with
-// c = 16cg + 4(lane>>4) + s, then the VALU weights of offset channels 16-17 one per lane:
-// V[ty][lane][r] = w_off[16 + jj][16cg + 4g + s][3ty + tx] for lane = 16g + i, vi = 16r + i =
-// 8tx + 2s + jj (0 for vi >= 24 or j >= J); the kernel broadcasts lane i of its 16-lane group
-// (DPP row_newbcast) instead of reading the same weights from LDS in every lane
+// c = 16cg + 4(lane>>4) + s, then V[t][g][2s + jj] = w_off[16 + jj][16cg + 4g + s][t]
+// (0 for j >= J)
 __global__ __launch_bounds__(256) void woff_to_f32frag(const float* __restrict__ w,
                                                        float* __restrict__ wf, int J, int C) {
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -1845,23 +1842,12 @@ __global__ __launch_bounds__(256) void woff_to_f32frag(const float* __restrict__
     j = lane & 15;
     c = 16 * cg + 4 * (lane >> 4) + s;
   } else {
-    const int v = k - 9 * 256, r = v & 1, lane = (v >> 1) & 63, ty = v >> 7;
-    const int vi = 16 * r + (lane & 15), tx = vi >> 3, s = (vi >> 1) & 3, jj = vi & 1;
-    t = 3 * ty + tx;
-    j = vi < 24 ? 16 + jj : J;
-    c = 16 * cg + 4 * (lane >> 4) + s;
+    const int v = k - 9 * 256, jj = v & 1, s = (v >> 1) & 3, gg = (v >> 3) & 3;
+    t = v >> 5;
+    j = 16 + jj;
+    c = 16 * cg + 4 * gg + s;
   }
   wf[i] = j < J ? w[((size_t)j * C + c) * 9 + t] : 0.f;
-}
-
-// weight VI of the lane's 16-lane group: lane VI % 16 of the group's row of vv (DPP
-// row_newbcast, gfx90a+), component VI / 16
-template <int VI>
-__device__ __forceinline__ float row_bcast_w(float2 vv) {
-  static_assert(VI >= 0 && VI < 32, "two weights per lane");
-  const float v = VI < 16 ? vv.x : vv.y;
-  return __int_as_float(
-      __builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + (VI & 15), 0xf, 0xf, true));
 }
 
 template <int ROWS>  // output rows per workgroup; 4 * ROWS waves
@@ -1982,34 +1968,28 @@ offset_conv_fwd_mfma_xt(Geo g, const float* __restrict__ x, const float* __restr
     }
     const float* LB = L + WIN;
     if (has_tile && live) {
+#pragma unroll 1
+      for (int ty = 0; ty < 3; ++ty)
 #pragma unroll
-      for (int ty = 0; ty < 3; ++ty) {
-        // this row of taps' 24 VALU weights of the lane's group, lane i of the group holding
-        // weights i and 16 + i (one 8-B read per row of taps, not two 16-B reads per tap)
-        const float2 vv = *reinterpret_cast<const float2*>(LB + 9 * 256 + (ty * 64 + lane) * 2);
-        auto tap = [&](auto TX) __attribute__((always_inline)) {
-          constexpr int tx = decltype(TX)::value;
-          const int t = ty * 3 + tx;
-          const float4 bw = *reinterpret_cast<const float4*>(LB + (t * 64 + lane) * 4);
-          const float4 a =
-              *reinterpret_cast<const float4*>(L + ((ra + ty) * RW + ca + tx) * CP + 4 * gq);
-          acc = mfma16(a.x, bw.x, acc);
-          acc = mfma16(a.y, bw.y, acc);
-          acc = mfma16(a.z, bw.z, acc);
-          acc = mfma16(a.w, bw.w, acc);
-          // weight (s, jj) of tap tx: vi = 8tx + 2s + jj
-          e0 = fmaf(a.x, row_bcast_w<8 * tx + 0>(vv), e0);
-          e1 = fmaf(a.x, row_bcast_w<8 * tx + 1>(vv), e1);
-          e0 = fmaf(a.y, row_bcast_w<8 * tx + 2>(vv), e0);
-          e1 = fmaf(a.y, row_bcast_w<8 * tx + 3>(vv), e1);
-          e0 = fmaf(a.z, row_bcast_w<8 * tx + 4>(vv), e0);
-          e1 = fmaf(a.z, row_bcast_w<8 * tx + 5>(vv), e1);
-          e0 = fmaf(a.w, row_bcast_w<8 * tx + 6>(vv), e0);
-          e1 = fmaf(a.w, row_bcast_w<8 * tx + 7>(vv), e1);
-        };
-        tap(std::integral_constant<int, 0>());
-        tap(std::integral_constant<int, 1>());
-        tap(std::integral_constant<int, 2>());
+      for (int tx = 0; tx < 3; ++tx) {
+        const int t = ty * 3 + tx;
+        const float4 bw = *reinterpret_cast<const float4*>(LB + (t * 64 + lane) * 4);
+        const float4 v0 = *reinterpret_cast<const float4*>(LB + 9 * 256 + (t * 4 + gq) * 8);
+        const float4 v1 = *reinterpret_cast<const float4*>(LB + 9 * 256 + (t * 4 + gq) * 8 + 4);
+        const float4 a =
+            *reinterpret_cast<const float4*>(L + ((ra + ty) * RW + ca + tx) * CP + 4 * gq);
+        acc = mfma16(a.x, bw.x, acc);
+        acc = mfma16(a.y, bw.y, acc);
+        acc = mfma16(a.z, bw.z, acc);
+        acc = mfma16(a.w, bw.w, acc);
+        e0 = fmaf(a.x, v0.x, e0);
+        e1 = fmaf(a.x, v0.y, e1);
+        e0 = fmaf(a.y, v0.z, e0);
+        e1 = fmaf(a.y, v0.w, e1);
+        e0 = fmaf(a.z, v1.x, e0);
+        e1 = fmaf(a.z, v1.y, e1);
+        e0 = fmaf(a.w, v1.z, e0);
+        e1 = fmaf(a.w, v1.w, e1);
       }
     }
     // unconditional: past the last chunk it stages a re-loaded chunk nobody reads

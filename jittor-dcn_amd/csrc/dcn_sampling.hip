@@ -883,26 +883,31 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
                                                       (int)((size_t)g.HW * g.K * sizeof(GT)),
                                                       0x00020000);
   const unsigned coff = cok ? (unsigned)(c * sizeof(GT)) : 0x80000000u;
-  auto issue = [&](int ni) {
+  // two register sets for the batch stream, used in turn (a batch reads one while the next
+  // batch's loads land in the other), so no batch copies its rows into place
+  int4 mR[U];
+  RowT mx[U];
+  auto issue_into = [&](int ni, int4(&tR)[U], RowT(&tx)[U]) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int l = min(ni + u, segend - 1) - seg;  // wave-uniform, in [0, 64)
-      nR[u] = make_int4(__builtin_amdgcn_readlane(pg.x, l), __builtin_amdgcn_readlane(pg.y, l),
+      tR[u] = make_int4(__builtin_amdgcn_readlane(pg.x, l), __builtin_amdgcn_readlane(pg.y, l),
                         __builtin_amdgcn_readlane(pg.z, l), __builtin_amdgcn_readlane(pg.w, l));
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const unsigned o = (unsigned)nR[u].x * (unsigned)sizeof(GT) + coff;
+      const unsigned o = (unsigned)tR[u].x * (unsigned)sizeof(GT) + coff;
       if constexpr (sizeof(GT) == 2) {
         const auto q = __builtin_amdgcn_raw_buffer_load_b64(rcol, o, 0, 0);
-        nx[u] = make_uint2(q[0], q[1]);
+        tx[u] = make_uint2(q[0], q[1]);
       } else {
         const auto q = __builtin_amdgcn_raw_buffer_load_b128(rcol, o, 0, 0);
-        nx[u] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]),
+        tx[u] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]),
                             __uint_as_float(q[3]));
       }
     }
   };
+  auto issue = [&](int ni) __attribute__((always_inline)) { issue_into(ni, nR, nx); };
   // two phases: bin column 0 (its left-boundary partials die with it), then columns 1..
   const int mid = bst[1];
   const bool any0 = act && mid > rowlo, any1 = act && rowhi > mid;
@@ -928,21 +933,24 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
       for (int bj = kB0; bj < kB1; ++bj) {
         if (bj >= nbin) break;
         const int lo = max(bst[bj], seg), hi = min(bst[bj + 1], segend);
-        for (int i = lo; i < hi; i += U) {
+        // batch i from (cR, cx); the next batch of this bin, else the next bin's first, into
+        // (tR, tx)
+        auto batch = [&](int i, int4(&cR)[U], RowT(&cx)[U], int4(&tR)[U], RowT(&tx)[U])
+                         __attribute__((always_inline)) {
           int4 R[U];
           float4 gv[U];
 #pragma unroll
           for (int u = 0; u < U; ++u) {
-            R[u] = nR[u];
+            R[u] = cR[u];
             if constexpr (sizeof(GT) == 2) {
-              const uint2 q = nx[u];
+              const uint2 q = cx[u];
               gv[u] = make_float4(__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
                                   __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u));
             } else {
-              gv[u] = nx[u];
+              gv[u] = cx[u];
             }
           }
-          issue(i + U < hi ? i + U : hi);  // next batch of this bin, else the next bin's first
+          issue_into(i + U < hi ? i + U : hi, tR, tx);
           float dv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // per-lane ∂offset parts
 #pragma unroll
           for (int u = 0; u < U; ++u) {
@@ -988,6 +996,20 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
               ox = mine ? sx_u : ox;
             }
           }
+        };
+        // the bin's batches alternate between the sets (nR, nx) and (mR, mx); every bin
+        // starts from (nR, nx), so a bin with an odd batch count moves the next bin's first
+        // batch there once
+        for (int i = lo; i < hi;) {
+          batch(i, nR, nx, mR, mx);
+          i += U;
+          if (i >= hi) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) nR[u] = mR[u], nx[u] = mx[u];
+            break;
+          }
+          batch(i, mR, mx, nR, nx);
+          i += U;
         }
       }
       if (drow && seg + lane < segend) {

@@ -2,7 +2,7 @@
 # r04: K5 batched ∂offset tree (4 waves/SIMD), fp32 offset conv (row-broadcast VALU weights in the
 # forward, 32x32x2 ∂W_off kernel), warp-specialised bf16 kernels reverted. Parity first, then
 # A/B against tools/alt/alt0 (the r03 K5 and offset conv; its fused bf16 kernels pinned to the
-# r03 ones), a bitwise dump comparison, and the whole GPU suite. Stops at the first failure.
+# r03 ones) and tools/alt/nopp (this build without the K5 register-set alternation), a bitwise dump comparison, and the whole GPU suite. Stops at the first failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
@@ -21,6 +21,7 @@ for rep in 1 2; do
   for c in 3 4; do
     CFG=$c run r03_c${c}_$rep $ALT0
     CFG=$c run new_c${c}_$rep DCN_DUMMY=0
+    CFG=$c run nopp_c${c}_$rep DCN_LIB=tools/alt/nopp/libdcn.so
   done
 done
 echo "== bitwise dumps (alt0 vs this build)" && \
