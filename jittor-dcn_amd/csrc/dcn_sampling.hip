@@ -933,6 +933,18 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
       for (int bj = kB0; bj < kB1; ++bj) {
         if (bj >= nbin) break;
         const int lo = max(bst[bj], seg), hi = min(bst[bj + 1], segend);
+        // the bin's four corners (r0, c0) .. (r0+1, c0+1), the same for all its samples, at
+        // window (w-1, bj) .. (w, bj+1); column bj+1 = kTQ+1 is W (the last tile column's bin
+        // W): outside the image. Read once per bin and segment, not per sample.
+        float4 ka = z4, kb = z4, kc = z4, kd = z4;
+        if (drow && lo < hi) {
+          const float4* w4 = lds + ((w - 1) * WQ + bj) * 64 + lane;
+          const bool cB = bj + 1 <= kTQ;  // (bj is unrolled: a constant)
+          ka = w4[0];
+          kb = cB ? w4[64] : z4;
+          kc = w4[WQ * 64];
+          kd = cB ? w4[(WQ + 1) * 64] : z4;
+        }
         // batch i from (cR, cx); the next batch of this bin, else the next bin's first, into
         // (tR, tx)
         auto batch = [&](int i, int4(&cR)[U], RowT(&cx)[U], int4(&tR)[U], RowT(&tx)[U])
@@ -969,15 +981,7 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
               ldn = fma4(fr * gc, gv[u], ldn);
             }
             if (drow) {
-              // corners (r0, c0) .. (r0+1, c0+1) at window (w-1, bj) .. (w, bj+1); column
-              // bj+1 = kTQ+1 is W (the last tile column's bin W): outside the image
-              const float4* w4 = lds + ((w - 1) * WQ + bj) * 64 + lane;
-              const bool cB = bj + 1 <= kTQ;  // (bj is unrolled: a constant)
-              const float4 a = w4[0];
-              const float4 bq = cB ? w4[64] : z4;
-              const float4 cq = w4[WQ * 64];
-              const float4 d = cB ? w4[(WQ + 1) * 64] : z4;
-              acc_dgrad4p(fr, fc, gv[u], a, bq, cq, d, dv[2 * u], dv[2 * u + 1]);
+              acc_dgrad4p(fr, fc, gv[u], ka, kb, kc, kd, dv[2 * u], dv[2 * u + 1]);
               // opaque to hipcc's SLP vectorizer: it would pair the two scalar FMA chains
               // into packed FMAs behind moves (more VALU, not less)
               asm("" : "+v"(dv[2 * u]), "+v"(dv[2 * u + 1]));
