@@ -1,0 +1,26 @@
+#!/bin/bash
+# r04: K5 launch shapes (rows per batch U, waves per SIMD, tile rows) A/B at configs 3 and 4:
+# this build (U 3, 4 waves/SIMD, 7 tile rows) against tools/alt/k5a (bf16: 3, 5, 4), k5b (both:
+# 2, 5, 4), k5c (both: 4, 4, 7); each alt first passes the K5 parity tests. Stops at the first
+# failure.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+T=${1:-k5}
+for a in k5a k5b k5c; do
+  DCN_LIB=tools/alt/$a/libdcn.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_bf16.py -x -q --timeout 120 --timeout-method thread > gpurun_out/${T}_pytest_$a.log 2>&1 || { tail -20 gpurun_out/${T}_pytest_$a.log; exit 1; }
+  echo "$a parity: $(tail -1 gpurun_out/${T}_pytest_$a.log)"
+done
+run() {  # name env...
+  local name=$1; shift
+  env "$@" timeout -k 10 120 python bench.py --config ${CFG:-3} --steps 20 --warmup 5 --no-cpu-baseline --no-strong --no-host-path --no-config4 --alt-math 0 > gpurun_out/${T}_$name.json 2> gpurun_out/${T}_$name.err || { tail -5 gpurun_out/${T}_$name.err; exit 1; }
+  python -c "import json,sys; d=json.loads(open('gpurun_out/${T}_$name.json').read().splitlines()[-1]); print('$name', d['ms_per_step'], {k: d['kernel_ms'].get(k) for k in ('col2im','offset_bwd','offset_fwd')})"
+}
+for rep in 1 2; do
+  for c in 3 4; do
+    CFG=$c run cur_c${c}_$rep DCN_DUMMY=0
+    for a in k5a k5b k5c; do CFG=$c run ${a}_c${c}_$rep DCN_LIB=tools/alt/$a/libdcn.so; done
+  done
+done
+echo k5 done
