@@ -1538,8 +1538,11 @@ static void launch_k5_fused(const Geo& g, const XT* xT, const BinsWs& P, const G
   // U = 3 at 5 (95 VGPRs): 0.564-0.568; U = 3 at 4: 0.565. bf16 U = 3 at 5: 0.123-0.124,
   // U = 4 at 5: 0.123, U = 3 at 6 (spills): 0.146.
   // r04: 4 waves/SIMD (128 VGPRs): two 8-wave workgroups per CU is all that 5 allowed too, and
-  // the batched ∂offset tree (wave_sum8) spills at 5 in the fp32 form
-  launch_c2i<3, 4, 4, 7>(g, xT, P, gcolT, gxT, goff, b0, nb, s);
+  // the batched ∂offset tree (wave_sum8) spills at 5 in the fp32 form. A/B at configs 3 / 4
+  // (profiles/r04_k5_shapes.txt, one box): U = 3 0.514-0.520 / 0.116 ms; U = 4 0.515 / 0.111-0.113;
+  // 5-wave workgroups at 5 waves/SIMD (20 waves per CU), bf16 U = 3: 0.134-0.136; both at U = 2:
+  // 0.538-0.542 / 0.144-0.147. More rows per wave pays, more (smaller) workgroups do not.
+  launch_c2i<4, 4, 4, 7>(g, xT, P, gcolT, gxT, goff, b0, nb, s);
 }
 
 hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, const float* off,

@@ -1,14 +1,15 @@
 #!/bin/bash
 # r04: K5 launch shapes (rows per batch U, waves per SIMD, tile rows) A/B at configs 3 and 4:
-# this build (U 3, 4 waves/SIMD, 7 tile rows) against tools/alt/k5a (bf16: 3, 5, 4), k5b (both:
-# 2, 5, 4), k5c (both: 4, 4, 7); each alt first passes the K5 parity tests. Stops at the first
+# this build (U 3, 4 waves/SIMD, 7 tile rows) and r03's K5 (tools/alt/alt0) against tools/alt/k5a (bf16: 3, 5, 4), k5b (both:
+# 2, 5, 4), k5c (both: 4, 4, 7), and ocf2 (the fp32 offset-conv forward with two MFMA
+# accumulator chains); each alt first passes the parity tests. Stops at the first
 # failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 T=${1:-k5}
-for a in k5a k5b k5c; do
+for a in k5a k5b k5c ocf2; do
   DCN_LIB=tools/alt/$a/libdcn.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_bf16.py -x -q --timeout 120 --timeout-method thread > gpurun_out/${T}_pytest_$a.log 2>&1 || { tail -20 gpurun_out/${T}_pytest_$a.log; exit 1; }
   echo "$a parity: $(tail -1 gpurun_out/${T}_pytest_$a.log)"
 done
@@ -20,7 +21,8 @@ run() {  # name env...
 for rep in 1 2; do
   for c in 3 4; do
     CFG=$c run cur_c${c}_$rep DCN_DUMMY=0
-    for a in k5a k5b k5c; do CFG=$c run ${a}_c${c}_$rep DCN_LIB=tools/alt/$a/libdcn.so; done
+    CFG=$c run r03_c${c}_$rep DCN_LIB=tools/alt/alt0/libdcn.so DCN_FWD_WS=0 DCN_DW_WS=0
+    for a in k5a k5b k5c ocf2; do CFG=$c run ${a}_c${c}_$rep DCN_LIB=tools/alt/$a/libdcn.so; done
   done
 done
 echo k5 done
