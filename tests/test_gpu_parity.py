@@ -242,6 +242,8 @@ def test_channels_last_kernels_match_generic_kernels(gpu_handle, C, H, W, s, off
     (2, 12, 7, 5, (3, 2), (1, 1), (1, 0), (1, 1)),     # rect kernel, Wo < W
     (1, 16, 6, 200, (3, 3), (1, 1), (1, 1), (1, 1)),   # wide rows: 2-row ∂W chunks
     (2, 68, 23, 25, (3, 3), (2, 2), (1, 1), (1, 1)),   # stride 2: VALU kernels only
+    (2, 128, 12, 16, (3, 3), (1, 1), (1, 1), (1, 1)),  # ∂W_off on 32x32x2 (C % 128 == 0)
+    (3, 256, 9, 12, (3, 3), (1, 1), (1, 1), (1, 1)),   # the same, ragged row chunks
 ])
 def test_offset_conv_bwd_mfma_and_valu_vs_oracle(gpu_handle, B, C, H, W, k, s, p, dil):
     """Offset-conv backward (∂W_off, ∂b_off, ∂x accumulated) on the MFMA kernels (stride 1)
