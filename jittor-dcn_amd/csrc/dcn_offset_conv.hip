@@ -1404,8 +1404,10 @@ __device__ __forceinline__ void split8(const float (&v)[8], bf16x8_t& hi, bf16x8
 
 // ∂x: block = 64 input pixels of one image (2 N-tiles) x all channels; wave w = channels
 // 64w..64w+63 (2 M-tiles); D[c][q] + the sampling route's channels-last ∂x, written as
-// bf16 NCHW (the API's grad_x).
-__global__ __launch_bounds__(256) void offset_dgrad_bf16(Geo g, const bf16_t* __restrict__ wc,
+// bf16 NCHW (the API's grad_x). r04: the epilogue reads and writes through buffer resources
+// (32-bit offsets), which cut 160 VGPRs + 64 AGPRs to 121 registers: 4 workgroups per CU
+// instead of 2, so config 4's 832 workgroups run in one round.
+__global__ __launch_bounds__(256, 3) void offset_dgrad_bf16(Geo g, const bf16_t* __restrict__ wc,
                                                         int KT16, const float* __restrict__ goff,
                                                         const float* __restrict__ gxT_in,
                                                         bf16_t* __restrict__ gx, int spi) {
@@ -1491,27 +1493,43 @@ __global__ __launch_bounds__(256) void offset_dgrad_bf16(Geo g, const bf16_t* __
   __syncthreads();  // every wave is done with S: its space holds the transposes
   if (!live) return;
   float* T = S + w * 32 * kDgTP;
+  const auto rgx = __builtin_amdgcn_make_buffer_rsrc(gx + (size_t)b * g.C * g.HWi, 0,
+                                                     (int)((size_t)g.C * g.HWi * 2), 0x00020000);
+  const auto rgt = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(gxT_in + (size_t)b * g.HWi * g.C), 0, (int)((size_t)g.HWi * g.C * 4),
+      0x00020000);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    float4 tv[8];
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
-      const int pl = min(32 * u + 4 * it + (lane >> 4), np - 1);
-      tv[it] = *reinterpret_cast<const float4*>(gxT_in + ((size_t)b * g.HWi + p0 + pl) * g.C + cw +
-                                                 4 * (lane & 15));
+    for (int h2 = 0; h2 < 2; ++h2) {
+      float4 tv[4];
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int pl = min(32 * u + 4 * (4 * h2 + it) + (lane >> 4), np - 1);
+        const auto q = __builtin_amdgcn_raw_buffer_load_b128(
+            rgt, (unsigned)(((p0 + pl) * g.C + cw + 4 * (lane & 15)) * 4), 0, 0);
+        tv[it] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]),
+                             __uint_as_float(q[3]));
+      }
+#pragma unroll
+      for (int it = 0; it < 4; ++it)
+        *reinterpret_cast<float4*>(T + (4 * (4 * h2 + it) + (lane >> 4)) * kDgTP + 4 * (lane & 15)) = tv[it];
     }
-#pragma unroll
-    for (int it = 0; it < 8; ++it)
-      *reinterpret_cast<float4*>(T + (4 * it + (lane >> 4)) * kDgTP + 4 * (lane & 15)) = tv[it];
     __builtin_amdgcn_wave_barrier();
-    if (32 * u + r < np) {
-      const size_t p = (size_t)p0 + 32 * u + r;
+    {
+      // 32-bit offsets into this image's planes through a buffer resource (64-bit addresses per
+      // store held 2 VGPRs each and capped the kernel at 2 waves per SIMD); a pixel past np
+      // stores out of range (dropped)
+      const int pl = 32 * u + r;
+      const unsigned pb = pl < np ? (unsigned)(p0 + pl) * 2u : 0x80000000u;
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int cl = 32 * m + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          gx[((size_t)b * g.C + cw + cl) * g.HWi + p] = f2bf(T[r * kDgTP + cl] + acc[m][u][i]);
+          const unsigned o = pl < np ? (unsigned)(cw + cl) * (unsigned)g.HWi * 2u + pb : pb;
+          __builtin_amdgcn_raw_buffer_store_b16(
+              (unsigned short)f2bf(T[r * kDgTP + cl] + acc[m][u][i]), rgx, o, 0, 0);
         }
     }
     __builtin_amdgcn_wave_barrier();  // the next half overwrites T
