@@ -192,6 +192,8 @@ struct dcn_handle {
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   dcn::GemmEngine* gemm = nullptr;
   int fwd_path = DCN_FWD_AUTO;  // dcn_set_fwd_path
+  // bf16 ∂columns on the vendor GEMM instead of dcol_bf16 (DCN_DCOL_GEMM=1: the A/B switch)
+  bool dcol_gemm = false;
   // workspaces whose last DCN_BF16 forward left no columns in them (DCN_FWD_FUSED_NOCOL or
   // DCN_FWD_NO_COLUMNS): a DCN_BWD_COL_IN_WS backward on one of them recomputes the columns
   // instead of reading whatever its col region holds. One entry per workspace (any number of
@@ -678,13 +680,20 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
   DCN_TRY(dw_final(h, F32(L.gw32), has_bias ? F32(L.gb32) : nullptr, g, exch ? gw : nullptr,
                    exch && has_bias ? gb : nullptr));
   {
-    ProfScope ps(h, DCN_K_GEMM_DCOL);  // ∂colT = ∂outT · Wf, one flat GEMM, bf16 out
+    ProfScope ps(h, DCN_K_GEMM_DCOL);  // ∂colT = ∂outT · Wf over the whole batch, bf16 out
     if (dwg <= 0) HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(gout, goutT, g.B, g.O, g.HW, st));
-    dcn::GemmSpec sp;
-    sp.m = g.K; sp.n = g.B * g.HW; sp.k = g.O;
-    sp.lda = g.K; sp.ldb = g.O; sp.ldc = g.K;
-    sp.bf16_ab = sp.bf16_c = true;
-    GEMM_TRY(h, sp, w, goutT, col);
+    const long npix = (long)g.B * g.HW;
+    if (!h->dcol_gemm && dcn::dcol_bf16_ok(g.K, g.O, npix) && !dcn::get_force_generic()) {
+      // short-K streaming kernel (csrc/dcn_dcol_bf16.hip); its swizzled weight copy (K·O
+      // bf16) in the ∂W partials, which sum_partials has consumed earlier on this stream
+      HIP_TRY(dcn::launch_dcol_bf16(w, goutT, col, BF(L.parts), g.K, g.O, npix, st));
+    } else {
+      dcn::GemmSpec sp;
+      sp.m = g.K; sp.n = g.B * g.HW; sp.k = g.O;
+      sp.lda = g.K; sp.ldb = g.O; sp.ldc = g.K;
+      sp.bf16_ab = sp.bf16_c = true;
+      GEMM_TRY(h, sp, w, goutT, col);
+    }
   }
   DCN_TRY(join_aux(h));
   {
@@ -788,6 +797,7 @@ int dcn_create(int device, dcn_handle** out) {
     dcn_destroy(h);
     return fail(DCN_ERR_HIP, std::string("dcn_create: ") + hipGetErrorString(e));
   }
+  if (const char* f = std::getenv("DCN_DCOL_GEMM")) h->dcol_gemm = std::atoi(f) != 0;
   std::string gerr;
   if (dcn::gemm_engine_create(&h->gemm, &gerr) != 0) {
     (void)hipStreamDestroy(h->own);

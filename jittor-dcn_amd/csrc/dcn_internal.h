@@ -206,7 +206,13 @@ hipError_t launch_roi_pool_bwd(const RoiGeo& q, const float* f, const float* roi
                                const float* offsets, const float* gout, float* gf, float* goffs,
                                hipStream_t s);
 
-// dcn_gemm.cpp: C = op(A)·op(B)// dcn_gemm.cpp: C = op(A)·op(B) (column-major, alpha 1, beta 0), strided batched.
+// dcn_dcol_bf16.hip: the bf16 ∂columns ∂colT[p][k] = Σ_o ∂outT[p][o] · Wf[o][k] (O = 256,
+// K % 256 == 0) as a short-K streaming kernel; wz = K·O bf16 scratch for the swizzled weight
+bool dcol_bf16_ok(int K, int O, long npix);
+hipError_t launch_dcol_bf16(const bf16_t* w, const bf16_t* goutT, bf16_t* col, bf16_t* wz,
+                            int K, int O, long npix, hipStream_t s);
+
+// dcn_gemm.cpp: C = op(A)·op(B) (column-major, alpha 1, beta 0), strided batched.
 struct GemmSpec {
   bool ta = false, tb = false;
   int m = 0, n = 0, k = 0, lda = 0, ldb = 0, ldc = 0;

@@ -163,6 +163,10 @@ def _bf16_sweep(i):
     dict(seed=5, B=3, C=64, O_=32, H=10, W=12, off_scale=2.0),
     dict(seed=6, B=2, C=128, O_=64, H=8, W=4),
     dict(seed=7, B=1, C=192, O_=16, H=13, W=16, off_scale=2.5),
+    # C = O = 256: the ∂columns on dcol_bf16 (K % 256 == 0, O == 256): 507 pixels (a
+    # 59-pixel last chunk), and stride 2 with 144 pixels (a 16-pixel last chunk)
+    dict(seed=8, B=3, C=256, O_=256, H=13, W=13),
+    dict(seed=9, B=2, C=256, O_=256, H=17, W=15, s=(2, 2), off_scale=2.0),
 ] + [_bf16_sweep(i) for i in range(6)])
 def test_bf16_forward_backward_vs_oracle(gpu_handle, case):
     bits, v, s = _case(**case)
@@ -217,6 +221,29 @@ def test_bf16_config4_full_size_bitwise_reproducible(gpu_handle):
     np.testing.assert_array_equal(r1[1].view(np.uint32), r2[1].view(np.uint32), err_msg="off")
     for k in r1[2]:
         np.testing.assert_array_equal(r1[2][k].view(np.uint32), r2[2][k].view(np.uint32),
+                                      err_msg=k)
+
+
+def test_bf16_dcol_kernel_vs_vendor_gemm(gpu_handle, monkeypatch):
+    """The ∂columns of dcol_bf16 (short-K streaming kernel) against the vendor GEMM's on the
+    same inputs (a handle created with DCN_DCOL_GEMM=1): every downstream tensor within the
+    bf16 bound of the other, and the forward tensors bit for bit (the kernel is backward
+    only). Both sum the same 256 exact bf16 products in fp32, in different orders, then
+    round to bf16 once, so ∂col elements may differ by an ulp; ∂x / ∂offset sum them."""
+    bits, _, s = _case(13, B=4, C=256, O_=256, H=20, W=19, off_scale=1.5)
+    a = _device(gpu_handle, bits, s)
+    monkeypatch.setenv("DCN_DCOL_GEMM", "1")
+    h2 = rt.Handle(0)
+    try:
+        b = _device(h2, bits, s)
+    finally:
+        h2.close()
+    np.testing.assert_array_equal(a[0].view(np.uint32), b[0].view(np.uint32), err_msg="out")
+    np.testing.assert_array_equal(a[1].view(np.uint32), b[1].view(np.uint32), err_msg="off")
+    for k in ("x", "offset", "offset_conv.weight", "offset_conv.bias"):
+        assert_bf16_close(a[2][k], b[2][k], k)
+    for k in ("weight", "bias"):  # before the ∂columns: untouched
+        np.testing.assert_array_equal(a[2][k].view(np.uint32), b[2][k].view(np.uint32),
                                       err_msg=k)
 
 
