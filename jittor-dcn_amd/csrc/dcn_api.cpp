@@ -118,6 +118,7 @@ struct WsLayout {
   size_t x32 = 0, xT32 = 0, wb16 = 0, woff32 = 0, boff32 = 0, b32 = 0, off32 = 0, out32 = 0;
   size_t wfr = 0;  // fused bf16 forward: Wf in MFMA lane order
   size_t gx32 = 0, gw32 = 0, gb32 = 0, gwo32 = 0, gbo32 = 0, goff32 = 0;
+  size_t wz = 0;  // dcol_bf16: Wf in MFMA A-fragment order
   size_t total = 0;
 };
 
@@ -175,6 +176,8 @@ WsLayout ws_layout(const Geo& g, bool bwd, bool cols = true) {
     L.gwo32 = take((size_t)g.J * g.C * g.N * f);
     L.gbo32 = take((size_t)g.J * f);
     L.goff32 = take((size_t)g.B * g.J * g.HW * f);
+    L.wz = take(dcn::dcol_bf16_ok(g.K, g.O, (long)g.B * g.HW) ? (size_t)g.K * g.O * sizeof(dcn::bf16_t)
+                                                              : 0);
   }
   L.total = off;
   return L;
@@ -684,9 +687,10 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
     if (dwg <= 0) HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(gout, goutT, g.B, g.O, g.HW, st));
     const long npix = (long)g.B * g.HW;
     if (!h->dcol_gemm && dcn::dcol_bf16_ok(g.K, g.O, npix) && !dcn::get_force_generic()) {
-      // short-K streaming kernel (csrc/dcn_dcol_bf16.hip); its swizzled weight copy (K·O
-      // bf16) in the ∂W partials, which sum_partials has consumed earlier on this stream
-      HIP_TRY(dcn::launch_dcol_bf16(w, goutT, col, BF(L.parts), g.K, g.O, npix, st));
+      // short-K streaming kernel (csrc/dcn_dcol_bf16.hip) after its Wf swizzle (in line:
+      // on the side stream it ran beside the ∂W GEMM and cost that 10 µs, r04 dcol5)
+      HIP_TRY(dcn::launch_dcol_bf16_swizzle(w, g.K, g.O, BF(L.wz), st));
+      HIP_TRY(dcn::launch_dcol_bf16(BF(L.wz), goutT, col, g.K, g.O, npix, st));
     } else {
       dcn::GemmSpec sp;
       sp.m = g.K; sp.n = g.B * g.HW; sp.k = g.O;

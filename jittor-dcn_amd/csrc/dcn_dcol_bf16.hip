@@ -14,8 +14,9 @@
 //     rows (32 × 512 B) go straight into registers as the B fragments, and the next tile's
 //     are loaded while this one computes (two register sets); no barrier after the A copy;
 //   * the A rows of each 32-row tile are permuted (dc_perm) so that the accumulator rows a
-//     lane holds are 16 consecutive k: every lane stores 2 × 16 B per row tile, and a pair of
-//     row tiles writes whole 128-B lines per pixel;
+//     lane holds are 16 consecutive k; a pair of row tiles (64 columns × 32 pixels) passes
+//     through a per-wave 4-KiB LDS stage, so each store instruction writes 8 whole 128-B
+//     lines (the MFMA layout alone gives 32 lines × 2 pieces of 16 B per instruction);
 //   * the row groups of one pixel range run on one XCD (bijective remap), so the L2 serves
 //     a tile's ∂outT rows to all of them after the first read.
 // Rounding: fp32 accumulation over o inside the MFMA, one round-to-nearest-even to bf16 per
@@ -40,6 +41,8 @@ constexpr int kDcRows = 256;                     // ∂col columns per workgroup
 constexpr int kDcMT = kDcRows / 32;              // their 32-row MFMA tiles
 constexpr int kDcWaves = 8;                      // two waves per SIMD, one workgroup per CU
 constexpr int kDcLds = kDcMT * kDcKS * 64 * 16;  // the A image: 128 KiB
+constexpr int kDcLdsAll = kDcLds + kDcWaves * 4096;  // + a 4-KiB output stage per wave
+static_assert(kDcLdsAll <= 160 * 1024, "one workgroup per CU");
 
 // accumulator row r = 8q + 4h + i of a 32x32 tile (lane half h, register 4q + i) takes the
 // A row of ∂col column 16h + 4q + i, so register j of a lane in half h is column 16h + j
@@ -116,13 +119,12 @@ __global__ __launch_bounds__(kDcWaves * 64, 2) void dcol_bf16(const bf16_t* __re
   // stores through a buffer resource: a pixel past the end gets an offset past the range
   const auto rcol = __builtin_amdgcn_make_buffer_rsrc(col, 0, (int)((size_t)npix * K * 2),
                                                       0x00020000);
-  const int kw = rg * kDcRows + 16 * (lane >> 5);  // + 32 per row tile: this lane's columns
+  const int kr = rg * kDcRows;  // the workgroup's first ∂col column
+  char* stage = dl + kDcLds + w * 4096;
   // tile tc from bc while tile tc + 8 loads into bn; row tiles in pairs (two 32x32
   // accumulators), each pair stored as soon as it is done
   auto tile = [&](int tc, const bf16x8(&bc)[kDcKS], bf16x8(&bn)[kDcKS]) {
     if (tc + kDcWaves < t1) load_b(tc + kDcWaves, bn);
-    const int p = tc * 32 + (lane & 31);
-    const unsigned o = p < npix ? (unsigned)(p * K + kw) * 2u : 0x80000000u;
 #pragma unroll
     for (int pr = 0; pr < kDcMT / 2; ++pr) {
       f32x16 acc0, acc1;
@@ -144,11 +146,30 @@ __global__ __launch_bounds__(kDcWaves * 64, 2) void dcol_bf16(const bf16_t* __re
         acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[ks % 3][1], bc[ks], acc1, 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
       }
-      const unsigned oo = o + 128 * pr;  // row tiles 2pr, 2pr + 1: columns 64pr .. 64pr + 63
-      __builtin_amdgcn_raw_buffer_store_b128(pack4(acc0, 0), rcol, oo, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(pack4(acc0, 8), rcol, oo + 16, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(pack4(acc1, 0), rcol, oo + 64, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(pack4(acc1, 8), rcol, oo + 80, 0, 0);
+      // row tiles 2pr, 2pr + 1 = columns 64pr .. 64pr + 63 of the tile's 32 pixels, through
+      // the wave's 4-KiB LDS stage ([pixel][64 columns], 16-B chunk c of row r at c ^ (r & 7))
+      // so that each store writes 8 pixels × one whole 128-B line
+      {
+        const int n = lane & 31, hh = lane >> 5;
+        char* srow = stage + n * 128;
+        auto put = [&](int c, const u32x4& v) {
+          *reinterpret_cast<u32x4*>(srow + ((c ^ (n & 7)) << 4)) = v;
+        };
+        put(2 * hh, pack4(acc0, 0));
+        put(2 * hh + 1, pack4(acc0, 8));
+        put(4 + 2 * hh, pack4(acc1, 0));
+        put(5 + 2 * hh, pack4(acc1, 8));
+      }
+      asm volatile("" ::: "memory");  // the stage's writes before its reads (one wave, in order)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 8 * i + (lane >> 3), c = lane & 7;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(stage + r * 128 + ((c ^ (r & 7)) << 4));
+        const int p = tc * 32 + r;
+        const unsigned o = p < npix ? (unsigned)(p * K + kr + 64 * pr + 8 * c) * 2u : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(v, rcol, o, 0, 0);
+      }
+      asm volatile("" ::: "memory");  // the reads before the next pair's writes
     }
   };
   for (; t < t1; t += 2 * kDcWaves) {
@@ -164,8 +185,15 @@ bool dcol_bf16_ok(int K, int O, long npix) {
   return O == kDcO && K > 0 && K % kDcRows == 0 && npix > 0 && (long)npix * K * 2 < (1l << 31);
 }
 
-hipError_t launch_dcol_bf16(const bf16_t* w, const bf16_t* goutT, bf16_t* col, bf16_t* wz,
-                            int K, int O, long npix, hipStream_t s) {
+hipError_t launch_dcol_bf16_swizzle(const bf16_t* w, int K, int O, bf16_t* wz, hipStream_t s) {
+  if (O != kDcO || K <= 0 || K % kDcRows != 0) return hipErrorInvalidValue;
+  const int nsw = (K / 32) * kDcKS * 64;
+  hipLaunchKernelGGL(dcol_swizzle_w, dim3((nsw + 255) / 256), dim3(256), 0, s, w, K, wz);
+  return hipGetLastError();
+}
+
+hipError_t launch_dcol_bf16(const bf16_t* wz, const bf16_t* goutT, bf16_t* col, int K, int O,
+                            long npix, hipStream_t s) {
   if (!dcol_bf16_ok(K, O, npix)) return hipErrorInvalidValue;
   static std::mutex mu;
   static std::vector<char> attr_set;
@@ -179,20 +207,18 @@ hipError_t launch_dcol_bf16(const bf16_t* w, const bf16_t* goutT, bf16_t* col, b
     if ((int)attr_set.size() <= dev) attr_set.resize(dev + 1, 0);
     if (!attr_set[dev]) {
       const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dcol_bf16),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, kDcLds);
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, kDcLdsAll);
       if (e != hipSuccess) return e;
       attr_set[dev] = 1;
     }
   }
-  const int nsw = (K / 32) * kDcKS * 64;
-  hipLaunchKernelGGL(dcol_swizzle_w, dim3((nsw + 255) / 256), dim3(256), 0, s, w, K, wz);
   // one workgroup per CU: ranges × row groups ≈ 256
   const int nrg = K / kDcRows, ntile = (int)((npix + 31) / 32);
   int ranges = std::max(1, std::min(ntile, 256 / std::max(1, nrg)));
   const int tpr = (ntile + ranges - 1) / ranges;
   ranges = (ntile + tpr - 1) / tpr;
   const int nwg = ranges * nrg;
-  hipLaunchKernelGGL(dcol_bf16, dim3(nwg), dim3(kDcWaves * 64), kDcLds, s, wz, goutT, col, K,
+  hipLaunchKernelGGL(dcol_bf16, dim3(nwg), dim3(kDcWaves * 64), kDcLdsAll, s, wz, goutT, col, K,
                      (int)npix, nrg, tpr, nwg);
   return hipGetLastError();
 }

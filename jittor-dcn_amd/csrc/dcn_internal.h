@@ -207,10 +207,11 @@ hipError_t launch_roi_pool_bwd(const RoiGeo& q, const float* f, const float* roi
                                hipStream_t s);
 
 // dcn_dcol_bf16.hip: the bf16 ∂columns ∂colT[p][k] = Σ_o ∂outT[p][o] · Wf[o][k] (O = 256,
-// K % 256 == 0) as a short-K streaming kernel; wz = K·O bf16 scratch for the swizzled weight
+// K % 256 == 0) as a short-K streaming kernel; wz = K·O bf16, Wf in its A-fragment order
 bool dcol_bf16_ok(int K, int O, long npix);
-hipError_t launch_dcol_bf16(const bf16_t* w, const bf16_t* goutT, bf16_t* col, bf16_t* wz,
-                            int K, int O, long npix, hipStream_t s);
+hipError_t launch_dcol_bf16_swizzle(const bf16_t* w, int K, int O, bf16_t* wz, hipStream_t s);
+hipError_t launch_dcol_bf16(const bf16_t* wz, const bf16_t* goutT, bf16_t* col, int K, int O,
+                            long npix, hipStream_t s);
 
 // dcn_gemm.cpp: C = op(A)·op(B) (column-major, alpha 1, beta 0), strided batched.
 struct GemmSpec {

@@ -1,6 +1,7 @@
 #!/bin/bash
 # r04: the bf16 ∂columns on dcol_bf16 (short-K streaming kernel) against the vendor GEMM
-# (DCN_DCOL_GEMM=1, same build): bf16 parity, then config-4 A/B (bench.py, HIP events) and a
+# (DCN_DCOL_GEMM=1, same build; ALT=path/libdcn.so adds an older build): bf16 parity, then
+# config-4 A/B (bench.py, HIP events) and a
 # rocprofv3 kernel-stats pass. Stops at the first failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -16,6 +17,7 @@ run() {  # name env...
 }
 for rep in 1 2 3; do
   run new_$rep DCN_DUMMY=0 || exit 1
+  [ -n "$ALT" ] && { run alt_$rep DCN_LIB=$ALT || exit 1; }
   run gemm_$rep DCN_DCOL_GEMM=1 || exit 1
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof4 -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-strong --no-host-path --no-config4 --config 4 > gpurun_out/${T}_prof4.log 2>&1 || { tail -5 gpurun_out/${T}_prof4.log; exit 1; }
