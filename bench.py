@@ -894,6 +894,16 @@ def other_rooflines(kernel_ms, B, C, O_, H, W, N, Ho, Wo, J, bf16, fwd_only):
             out.append({"kernel": name, "bound": "mfma", "achieved": round(tf, 1),
                         "peak": peak_tf, "unit": "TFLOP/s", "frac": round(tf / peak_tf, 4),
                         "algorithmic_flop": gemm_flop, "avg_launch_ms": ms})
+    ms = kernel_ms.get("gemm_dcol")
+    if ms and bf16 and not fwd_only:
+        # bf16 ∂columns (dcol_bf16 at config 4): a 256-deep reduction whose 231 MB of bf16
+        # output outweighs its MFMA work (HBM floor 32 µs against 24 µs of MFMA at peak)
+        dc_b = 2 * (M * K + M * O_ + K * O_)
+        gbs = dc_b / (ms * 1e-3) / 1e9
+        out.append({"kernel": "gemm_dcol (bf16 ∂columns: bytes moved)", "bound": "hbm",
+                    "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes": dc_b,
+                    "avg_launch_ms": ms})
     ms = kernel_ms.get("col2im")
     if ms and not bf16 and not fwd_only:
         k5_b = 4 * (M * K + 2 * B * C * H * W + 2 * B * J * Ho * Wo)
