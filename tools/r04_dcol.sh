@@ -1,6 +1,6 @@
 #!/bin/bash
 # r04: the bf16 ∂columns on dcol_bf16 (short-K streaming kernel) against the vendor GEMM
-# (DCN_DCOL_GEMM=1, same build; ALT=path/libdcn.so adds an older build): bf16 parity, then
+# (DCN_DCOL_GEMM=1, same build; ALT='path/libdcn.so ...' adds other builds): bf16 parity, then
 # config-4 A/B (bench.py, HIP events) and a
 # rocprofv3 kernel-stats pass. Stops at the first failure.
 set -o pipefail
@@ -17,7 +17,7 @@ run() {  # name env...
 }
 for rep in 1 2 3; do
   run new_$rep DCN_DUMMY=0 || exit 1
-  [ -n "$ALT" ] && { run alt_$rep DCN_LIB=$ALT || exit 1; }
+  for a in $ALT; do run $(basename $(dirname $a))_$rep DCN_LIB=$a || exit 1; done
   run gemm_$rep DCN_DCOL_GEMM=1 || exit 1
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof4 -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-strong --no-host-path --no-config4 --config 4 > gpurun_out/${T}_prof4.log 2>&1 || { tail -5 gpurun_out/${T}_prof4.log; exit 1; }

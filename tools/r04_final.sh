@@ -25,7 +25,7 @@ echo "== PMC config 3" && bash tools/pmc_pass.sh ${T}c3 && \
 echo "== PMC config 4" && BENCH_ARGS="--config 4" bash tools/pmc_pass.sh ${T}c4 && \
 echo "== bitwise dumps against r03's K5 / offset conv (tools/alt/alt0), GEMM choice pinned, bf16 ∂columns on hipBLASLt in both" && \
 PIN="DCN_GEMM_BACKEND=hipblaslt DCN_GEMM_CANDIDATES=1" && \
-env $PIN DCN_LIB=tools/alt/alt0/libdcn.so DCN_FWD_WS=0 DCN_DW_WS=0 timeout -k 10 300 python tools/ab_bitwise.py dump /tmp/ab_a.npz > gpurun_out/${T}_ab.log 2>&1 && \
+env $PIN DCN_LIB=tools/alt/alt0/libdcn.so timeout -k 10 300 python tools/ab_bitwise.py dump /tmp/ab_a.npz > gpurun_out/${T}_ab.log 2>&1 && \
 env $PIN DCN_DCOL_GEMM=1 timeout -k 10 300 python tools/ab_bitwise.py dump /tmp/ab_b.npz >> gpurun_out/${T}_ab.log 2>&1 && \
 { timeout -k 10 120 python tools/ab_bitwise.py cmp /tmp/ab_a.npz /tmp/ab_b.npz >> gpurun_out/${T}_ab.log 2>&1; grep -v "bitwise equal" gpurun_out/${T}_ab.log | tail -6; } && \
 echo "final evidence done"
