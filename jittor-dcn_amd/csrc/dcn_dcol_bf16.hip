@@ -41,6 +41,9 @@ constexpr int kDcRows = 256;                     // ∂col columns per workgroup
 constexpr int kDcMT = kDcRows / 32;              // their 32-row MFMA tiles
 constexpr int kDcWaves = 8;                      // two waves per SIMD, one workgroup per CU
 constexpr int kDcLds = kDcMT * kDcKS * 64 * 16;  // the A image: 128 KiB
+// A-fragment reads this many k-steps ahead of their MFMAs (r04 dcol6: 1 is 5 % slower; 3,
+// and s_setprio 1 around the MFMAs, no change)
+constexpr int kDcLA = 2;
 constexpr int kDcLdsAll = kDcLds + kDcWaves * 4096;  // + a 4-KiB output stage per wave
 static_assert(kDcLdsAll <= 160 * 1024, "one workgroup per CU");
 
@@ -135,15 +138,17 @@ __global__ __launch_bounds__(kDcWaves * 64, 2) void dcol_bf16(const bf16_t* __re
       auto lda = [&](int m, int ks) {
         return *reinterpret_cast<const bf16x8*>(As + ((m * kDcKS + ks) * 64 + lane) * 8);
       };
-      bf16x8 ra[3][2];
-      ra[0][0] = lda(2 * pr, 0), ra[0][1] = lda(2 * pr + 1, 0);
-      ra[1][0] = lda(2 * pr, 1), ra[1][1] = lda(2 * pr + 1, 1);
+      constexpr int LA = kDcLA;
+      bf16x8 ra[LA + 1][2];
+#pragma unroll
+      for (int d = 0; d < LA; ++d) ra[d][0] = lda(2 * pr, d), ra[d][1] = lda(2 * pr + 1, d);
 #pragma unroll
       for (int ks = 0; ks < kDcKS; ++ks) {
-        if (ks + 2 < kDcKS)
-          ra[(ks + 2) % 3][0] = lda(2 * pr, ks + 2), ra[(ks + 2) % 3][1] = lda(2 * pr + 1, ks + 2);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[ks % 3][0], bc[ks], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[ks % 3][1], bc[ks], acc1, 0, 0, 0);
+        if (ks + LA < kDcKS)
+          ra[(ks + LA) % (LA + 1)][0] = lda(2 * pr, ks + LA),
+          ra[(ks + LA) % (LA + 1)][1] = lda(2 * pr + 1, ks + LA);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[ks % (LA + 1)][0], bc[ks], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra[ks % (LA + 1)][1], bc[ks], acc1, 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
       }
       // row tiles 2pr, 2pr + 1 = columns 64pr .. 64pr + 63 of the tile's 32 pixels, through
