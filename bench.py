@@ -348,6 +348,97 @@ def config4_leg(args, world, rank, wl, rt, make_step, timed, kernel_times, fwd_p
     return res
 
 
+def scope_rooflines(kernel_ms, cfg, B, Ho, Wo):
+    """Every timed libdcn scope (DCN_K_* class, HIP-event average per call) against the
+    roofline of its bound, from SURVEY §8(d)'s algorithmic work for the workload `cfg`:
+    HBM bytes for the byte-moving kernels (K1, K5, transposes, bias), MFMA FLOPs for the
+    contractions (the three GEMMs, the offset conv and its backward). Scope times include
+    small companion launches (partial sums, swizzles), so the fractions are lower bounds.
+    Returns the list, longest scope first: element 0 is the dominant kernel."""
+    bf16 = cfg["dtype"] == "bf16"
+    e = 2 if bf16 else 4
+    C, O_, H, W, k = cfg["C"], cfg["O"], cfg["H"], cfg["W"], cfg["k"]
+    N, J = k * k, 2 * k * k * cfg.get("G", 1)
+    M, K = B * Ho * Wo, N * C
+    peak_tf = 2500.0 if bf16 else 157.3  # dense bf16 / f32 MFMA (MI355X_MICROARCH.md)
+    gemm = 2.0 * M * K * O_
+    oc = 2.0 * M * K * J  # the offset conv is a k×k conv to J channels: same M, K
+    work = {
+        "offset_fwd": ("mfma", oc, "offset conv (K3)"),
+        "im2col": ("hbm", k1_bytes(B, C, H, W, N, Ho, Wo, elem=e, J=J), "K1 deformable im2col"),
+        "gemm_fwd": ("mfma", gemm, "forward GEMM (K2)"),
+        "bias_fwd": ("hbm", 2 * e * B * O_ * Ho * Wo, "bias"),
+        "xpose": ("hbm", 2 * e * B * C * H * W, "x -> channels-last"),
+        "bwd_bias": ("hbm", 2 * e * B * O_ * Ho * Wo, "∂outT + ∂b"),
+        "gemm_dw": ("mfma", gemm, "∂W GEMM (K6)"),
+        "gemm_dcol": ("mfma", gemm, "∂col GEMM (K4)"),
+        "col2im": ("hbm", e * (M * K + 2 * B * C * H * W + 2 * B * J * Ho * Wo),
+                   "K5 col2im: ∂x and ∂offset"),
+        "offset_bwd": ("mfma", 2 * oc, "offset-conv backward (K7)"),
+    }
+    out = []
+    for name, ms in sorted(kernel_ms.items(), key=lambda kv: -kv[1]):
+        if name not in work or not ms:
+            continue
+        bound, amount, what = work[name]
+        rate = amount / (ms * 1e-3)
+        if bound == "hbm":
+            ach, peak, unit = rate / 1e9, HBM_PEAK_GBS, "GB/s"
+        else:
+            ach, peak, unit = rate / 1e12, peak_tf, "TFLOP/s"
+        out.append({"kernel": name, "what": what, "bound": bound, "achieved": round(ach, 1),
+                    "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
+                    ("algorithmic_bytes" if bound == "hbm" else "algorithmic_flop"): amount,
+                    "avg_launch_ms": ms})
+    return out
+
+
+def extra_config_leg(num, args, wl, rt, make_step, timed, kernel_times, sync, cpu=None):
+    """BASELINE config 2 (fp32 forward only, B=8, 64->128, 56x56: "1xMI355X fwd only vs
+    CPU") or config 5 (the DCNv1 option set, B=64, 512->512, 14x14, s2 dil2 G4, fwd+bwd) on
+    one GPU, timed like `value` (warmup, barrier-free synchronize brackets: N = 1); returns
+    the `config2` / `config5` object of the line: ms_per_step, value, kernel_ms, the
+    dominant scope's roofline and the others, and for config 2 its own CPU baseline
+    (`cpu`: the forward-only torch restatement of the reference's op sequence)."""
+    cfg = wl.cfg
+    B = cfg["B"]
+    step, bufs = make_step(wl, B, 5000 + num)
+    for _ in range(args.warmup):
+        step()
+    sync()
+    el = timed(step, args.steps)
+    km = kernel_times(step, args.steps)
+    Ho, Wo = rt.out_shape(wl.desc(B))
+    N = wl.N
+    roofs = scope_rooflines(km, cfg, B, Ho, Wo)
+    fwd_only = cfg.get("fwd_only", False)
+    value = B * Ho * Wo * N * args.steps / el / 1e9
+    res = {
+        "workload": f"config{num}: B={B}/GPU C={cfg['C']}->O={cfg['O']} {cfg['H']}x{cfg['W']} "
+                    f"k{cfg['k']} s{cfg['s']} p{cfg['p']} dil{cfg.get('dil', 1)} "
+                    f"G{cfg.get('G', 1)} {cfg['dtype']} DeformConv2d "
+                    + ("fwd only" if fwd_only else "fwd+bwd"),
+        "dtype": cfg["dtype"],
+        "value": round(value, 5),
+        "unit": "Gsamples/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 4),
+        "samples_per_step": B * Ho * Wo * N,
+        "kernel_ms": km,
+        "roofline": roofs[0] if roofs else None,
+        "rooflines_other": roofs[1:],
+        "cpu_baseline": None,
+    }
+    if cpu is not None:
+        res["cpu_baseline"] = cpu
+        if cpu.get("value"):
+            res["gpu_over_cpu"] = round(value / cpu["value"], 1)
+    del step, bufs
+    return res
+
+
 MATH_NAMES = {0: "f32 MFMA (rocBLAS/hipBLASLt)", 3: "f32 via split-bf16 X3 (2 planes, opt-in)",
               6: "f32 via exact-split bf16 X6", 9: "f32 via exact-split bf16 X9"}
 
@@ -391,6 +482,9 @@ def main():
     ap.add_argument("--no-config4", action="store_true",
                     help="skip the BASELINE config-4 leg (bf16, 64 images per GPU, 28x28) that "
                          "the default config-3 run times beside the headline under `config4`")
+    ap.add_argument("--no-extra-configs", action="store_true",
+                    help="skip the BASELINE config-2 and config-5 legs (one GPU) that the "
+                         "default config-3 run at N=1 times under `config2` / `config5`")
     ap.add_argument("--exchange", action="store_true",
                     help="run the gradient exchange even at N=1 (a 1-rank RCCL group), to "
                          "exercise the overlapped all-reduce path on one GPU")
@@ -669,6 +763,25 @@ def main():
                                fwd_path_split, lambda: torch.cuda.synchronize(dev))
         del wl4
         torch.cuda.empty_cache()
+    # BASELINE configs 2 and 5 (one-GPU configurations: fp32 forward only vs the CPU path, and
+    # the DCNv1 option set) in the default run at N = 1, reported under `config2` /
+    # `config5`, never as `value`
+    extra = {}
+    if (args.config == 3 and world == 1 and not strong and not args.no_extra_configs
+            and not args.graph):
+        for num in (2, 5):
+            h.prof_enable(0)
+            torch.cuda.synchronize(dev)
+            torch.cuda.empty_cache()
+            wlx = Workload(CONFIGS[num], rt, torch, dev, dcn_dp, seed=6000 + num)
+            cpu = None
+            if num == 2 and not args.no_cpu_baseline:
+                cpu = cpu_baseline_framework(CONFIGS[2], min(args.cpu_budget, 8.0),
+                                             name="config2")
+            extra[num] = extra_config_leg(num, args, wlx, rt, make_step, timed, kernel_times,
+                                          lambda: torch.cuda.synchronize(dev), cpu)
+            del wlx
+            torch.cuda.empty_cache()
     if rank == 0:
         achieved = k1_b / (k1_ms * 1e-3) / 1e9 if k1_ms else None
         # the committed PMC summary covers the config-3 (fp32) and config-4 (bf16) K1 only
@@ -721,6 +834,8 @@ def main():
             "fwd_paths_ms_per_step": fwd_paths,
             "strong_scaling": strong_res,
             "config4": cfg4_res,
+            "config2": extra.get(2),
+            "config5": extra.get(5),
             "cpu_baseline": None,
             "cpu_baseline_other": None,
         }

@@ -149,7 +149,7 @@ int dcn_forward(dcn_handle* h, const dcn_desc* d, const float* x,
 /* dcn_forward with per-call flags (ABI 5). DCN_FWD_NO_COLUMNS: no backward will read this
  * forward's columns (inference, jt.no_grad: deform_conv.py:56 under train.py:430), so a
  * DCN_BF16 fused geometry writes none, whatever path the handle is set to; the handle's
- * state is not touched (thread-safe with respect to other callers' paths). ws may then be
+ * forward path is not changed, only its per-workspace column record (below). ws may then be
  * sized by dcn_workspace_bytes(d, DCN_WS_FORWARD_NO_COLUMNS). fp32, and bf16 geometries
  * outside the fused forward, write their columns as usual. flags = 0 is dcn_forward. */
 #define DCN_FWD_NO_COLUMNS 1
@@ -158,9 +158,11 @@ int dcn_forward_ex(dcn_handle* h, const dcn_desc* d, const float* x,
                    const float* b, float* out, float* off, void* ws,
                    size_t ws_bytes, int flags);
 
-#define DCN_BWD_COL_IN_WS 1 /* ws still holds forward's columns. The library remembers,
-                              per workspace, a DCN_BF16 forward that wrote none (NO_COLUMNS /
-                              FUSED_NOCOL): a backward on that workspace recomputes them. */
+#define DCN_BWD_COL_IN_WS 1 /* ws still holds forward's columns. For DCN_BF16 the handle
+                              records the workspaces its forwards wrote columns into (at most
+                              256, the oldest dropped first); a backward on any other
+                              workspace (a NO_COLUMNS / FUSED_NOCOL forward, a dropped record,
+                              another handle's forward) recomputes them. */
 
 /* Autodiff of DeformConv2d.execute as triggered by optimizer.backward
  * (train.py:414). Overwrites grad_x, grad_w, grad_b (if has_bias),
@@ -383,6 +385,15 @@ int dcn_debug_force_generic(int on);
 /* Workgroup count of the fused forward's persistent grid (DCN_FWD_FUSED); 0 = one per CU.
  * Lets the parity tests walk many tiles (straddling images) through one workgroup. */
 int dcn_debug_fused_workgroups(int n);
+/* The ∂W partial planes ([O][K] fp32 each) that each backward path of this geometry writes
+ * into the workspace before its fixed-order sum — planes[0] one per image, planes[1] the
+ * grouped bf16 GEMM, planes[2] the recomputed-column bf16 kernel (0 where a path does not
+ * apply; n >= 3) — and in *capacity the planes the dcn_forward + dcn_backward workspace
+ * layout holds. Host only (no device call): the CPU tests check every count fits. */
+int dcn_debug_dw_parts(const dcn_desc* d, int* planes, int n, int* capacity);
+/* Number of workspaces the handle currently records as holding a DCN_BF16 forward's
+ * columns (DCN_BWD_COL_IN_WS); bounded, see DESIGN.md §1. */
+int dcn_debug_col_ws_records(dcn_handle* h, int* n);
 
 #ifdef __cplusplus
 }

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -100,12 +101,39 @@ int make_geo_f32(const dcn_desc* d, Geo* g) {
   return DCN_OK;
 }
 
+// ∂W as dwg grouped NT GEMMs over B/dwg images each, or one NN GEMM per image (0). r01
+// (tools/dw_ab.sh): bf16 config 4 ∂W 0.178 ms per image -> 0.130 ms in 16 groups (step 1.10 ->
+// 1.02 ms); fp32 config 3 unchanged at 1.65 ms, so fp32 stays per image.
+int dw_groups(const Geo& g) {
+  return (g.dt == DCN_BF16 && g.B > 16 && g.B % 16 == 0) ? 16 : 0;
+}
+
+// The ∂W partial planes ([O][K] fp32 each) that each backward path of this geometry writes
+// into the workspace's `parts` region before its fixed-order sum: one per image (the fp32
+// and the ungrouped bf16 GEMMs), dw_groups(g) (the grouped bf16 GEMM), and
+// fused_dw_bf16_groups(g) (the recomputed-column kernel of DCN_FWD_FUSED_NOCOL). ws_layout
+// sizes `parts` from the largest, and every backward checks its own count against what the
+// layout holds (the region once held fewer planes than a kernel
+// wrote).
+enum { DW_PER_IMAGE, DW_GROUPED, DW_FUSED, DW_PATHS };
+void dw_parts(const Geo& g, int n[DW_PATHS]) {
+  n[DW_PER_IMAGE] = g.B;
+  n[DW_GROUPED] = dw_groups(g);
+  n[DW_FUSED] = g.dt == DCN_BF16 && dcn::fused_dw_bf16_ok(g) ? dcn::fused_dw_bf16_groups(g) : 0;
+}
+int dw_parts_max(const Geo& g) {
+  int n[DW_PATHS];
+  dw_parts(g, n);
+  return *std::max_element(n, n + DW_PATHS);
+}
+
 struct WsLayout {
   size_t xT = 0;     // [B][H*W][C] channels-last copy of x (forward, kept for backward)
   size_t wt = 0;     // transposed w_off copy for the offset-conv kernels
   size_t part = 0;   // offset-conv channel-slice partials (forward)
   size_t col = 0;    // [B][HW][K] channels-last columns / ∂columns
-  size_t parts = 0;  // [B][O*K] ∂W partials
+  size_t parts = 0;  // [dw_parts_max][O*K] ∂W partials
+  int parts_planes = 0;  // the [O][K] planes `parts` holds (0: forward-only layout)
   size_t goff = 0;   // [B][J][HW] ∂offset (when the caller passes none)
   size_t goffT = 0;  // [B][HW][J] channels-last ∂offset (offset-conv ∂W)
   size_t gxT = 0;    // [B][H*W][C] channels-last ∂x (sampling route)
@@ -160,8 +188,9 @@ WsLayout ws_layout(const Geo& g, bool bwd, bool cols = true) {
   }
   if (bwd) {
     // ∂W partials; first also the ∂b tile sums of the fused ∂out transpose
-    L.parts = take(std::max((size_t)g.B * g.O * g.K, dcn::xpose_chsum_floats(g.B, g.O, g.HW)) *
-                   sizeof(float));
+    L.parts_planes = dw_parts_max(g);
+    L.parts = take(std::max((size_t)L.parts_planes * g.O * g.K,
+                            dcn::xpose_chsum_floats(g.B, g.O, g.HW)) * sizeof(float));
     L.goff = take((size_t)g.B * g.J * g.HW * sizeof(float));
     L.goffT = take(dcn::offset_conv_goffT_floats(g) * sizeof(float));
     L.gxT = take((size_t)g.B * g.HWi * g.C * sizeof(float));
@@ -197,11 +226,16 @@ struct dcn_handle {
   int fwd_path = DCN_FWD_AUTO;  // dcn_set_fwd_path
   // bf16 ∂columns on the vendor GEMM instead of dcol_bf16 (DCN_DCOL_GEMM=1: the A/B switch)
   bool dcol_gemm = false;
-  // workspaces whose last DCN_BF16 forward left no columns in them (DCN_FWD_FUSED_NOCOL or
-  // DCN_FWD_NO_COLUMNS): a DCN_BWD_COL_IN_WS backward on one of them recomputes the columns
-  // instead of reading whatever its col region holds. One entry per workspace (any number of
-  // modules may share the handle); a forward that writes columns into a workspace drops it.
-  std::vector<const void*> nocol_ws;
+  // workspaces whose last DCN_BF16 forward on this handle wrote its columns into them, most
+  // recent last. A DCN_BWD_COL_IN_WS backward reads the columns only from a workspace listed
+  // here and recomputes them otherwise (a forward under DCN_FWD_FUSED_NOCOL or
+  // DCN_FWD_NO_COLUMNS drops its workspace). At most kColWsCap entries: the oldest drops
+  // first, and a backward on a dropped workspace just recomputes, so the record never grows
+  // with the number of distinct workspaces (it used to) and is never wrong.
+  // Guarded by col_ws_mu: concurrent forwards / backwards on one handle may touch it.
+  static constexpr size_t kColWsCap = 256;
+  std::vector<const void*> col_ws;
+  std::mutex col_ws_mu;
   // data-parallel gradient exchange (dcn_set_comm / dcn_set_grad_stream): the ∂W/∂b
   // all-reduce runs on comm_stream as soon as they are final (dw_main / dw_aux), beside the
   // rest of the backward; the stream waits for comm_done before anything later
@@ -278,18 +312,30 @@ int set_device(dcn_handle* h) {
   return DCN_OK;
 }
 
-bool ws_is_nocol(const dcn_handle* h, const void* ws) {
-  return std::find(h->nocol_ws.begin(), h->nocol_ws.end(), ws) != h->nocol_ws.end();
+// Does this workspace hold the columns of the last DCN_BF16 forward that used it?
+bool ws_has_columns(dcn_handle* h, const void* ws) {
+  std::lock_guard<std::mutex> lk(h->col_ws_mu);
+  return std::find(h->col_ws.begin(), h->col_ws.end(), ws) != h->col_ws.end();
 }
-void ws_mark_nocol(dcn_handle* h, const void* ws, bool nocol) {
-  auto it = std::find(h->nocol_ws.begin(), h->nocol_ws.end(), ws);
-  if (nocol && it == h->nocol_ws.end()) h->nocol_ws.push_back(ws);
-  if (!nocol && it != h->nocol_ws.end()) h->nocol_ws.erase(it);
+void ws_mark_columns(dcn_handle* h, const void* ws, bool has) {
+  std::lock_guard<std::mutex> lk(h->col_ws_mu);
+  auto it = std::find(h->col_ws.begin(), h->col_ws.end(), ws);
+  if (it != h->col_ws.end()) h->col_ws.erase(it);
+  if (!has) return;
+  if (h->col_ws.size() >= dcn_handle::kColWsCap) h->col_ws.erase(h->col_ws.begin());
+  h->col_ws.push_back(ws);
+}
+
+// Can the DCN_BF16 forward of this geometry skip the column matrix (the fused forward
+// applies)? One predicate for dcn_workspace_bytes(DCN_WS_FORWARD_NO_COLUMNS) and the forward
+// itself (the two disagreed under dcn_debug_force_generic).
+bool fwd_can_skip_columns(const Geo& g) {
+  return g.dt == DCN_BF16 && dcn::fused_fwd_bf16_ok(g) && !dcn::get_force_generic();
 }
 
 // Does a DCN_BF16 forward under this path / these flags skip the columns?
 bool fwd_skips_columns(const dcn_handle* h, const Geo& g, int flags) {
-  return g.dt == DCN_BF16 && dcn::fused_fwd_bf16_ok(g) && !dcn::get_force_generic() &&
+  return fwd_can_skip_columns(g) &&
          (h->fwd_path == DCN_FWD_FUSED_NOCOL || (flags & DCN_FWD_NO_COLUMNS) != 0);
 }
 
@@ -408,13 +454,6 @@ int core_forward(dcn_handle* h, const Geo& g, const float* x, const float* off, 
   return DCN_OK;
 }
 
-// The offset-conv backward, when core_backward runs it interleaved with col2im.
-// ∂W as dwg grouped NT GEMMs over B/dwg images each, or one NN GEMM per image (0). r01
-// (tools/dw_ab.sh): bf16 config 4 ∂W 0.178 ms per image -> 0.130 ms in 16 groups (step 1.10 ->
-// 1.02 ms); fp32 config 3 unchanged at 1.65 ms, so fp32 stays per image.
-int dw_groups(const Geo& g) {
-  return (g.dt == DCN_BF16 && g.B > 16 && g.B % 16 == 0) ? 16 : 0;
-}
 
 int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off, const float* w,
                   const float* gout, float* gx, float* gw, float* gb, bool has_bias, float* goff,
@@ -575,7 +614,7 @@ int forward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x,
   }
   const bool fused_ok = dcn::fused_fwd_bf16_ok(g) && !dcn::get_force_generic();
   // this workspace holds this forward's columns unless it runs without them
-  ws_mark_nocol(h, base, nocol);
+  ws_mark_columns(h, base, !nocol);
   if (fused_ok && (h->fwd_path == DCN_FWD_FUSED || nocol ||
                    (h->fwd_path == DCN_FWD_AUTO && dcn::fused_fwd_bf16_pays(g)))) {
     // f2: the bilinear gather feeds the bf16 MFMAs straight from an LDS window of xT; bias
@@ -653,10 +692,13 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
     ProfScope ps(h, DCN_K_GEMM_DW);
     dcn::GemmSpec sp;
     sp.bf16_ab = true;
-    int nparts = g.B;
+    const int nparts = dw_fused ? dcn::fused_dw_bf16_groups(g) : dwg > 0 ? dwg : g.B;
+    if (nparts > L.parts_planes)  // the ∂W kernels below write nparts planes into `parts`
+      return fail(DCN_ERR_WORKSPACE, "∂W partials: " + std::to_string(nparts) +
+                                         " planes, the workspace layout holds " +
+                                         std::to_string(L.parts_planes));
     if (dw_fused) {
       HIP_TRY(dcn::launch_fused_dw_bf16(g, xT, off32, gout, F32(L.parts), st));
-      nparts = dcn::fused_dw_bf16_groups(g);
     } else if (dwg > 0) {
       // grouped NT over the pixels of B/dwg images (∂outT first, shared with ∂col)
       HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(gout, goutT, g.B, g.O, g.HW, st));
@@ -668,7 +710,6 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
       sp.ldc = g.K; sp.sc = (long)g.K * g.O;
       sp.batch = dwg;
       GEMM_TRY(h, sp, col, goutT, F32(L.parts));
-      nparts = dwg;
     } else {  // P_b(K×O) = colT_b · ∂out_b (NN), bf16 in, fp32 out
       sp.m = g.K; sp.n = g.O; sp.k = g.HW;
       sp.lda = g.K; sp.sa = (long)g.K * g.HW;
@@ -937,8 +978,7 @@ int dcn_workspace_bytes(const dcn_desc* d, int with_backward, size_t* bytes) {
     return fail(DCN_ERR_INVALID, "dcn_workspace_bytes: with_backward must be 0, 1 or 2");
   // DCN_WS_FORWARD_NO_COLUMNS: no col region where the forward skips the columns (DCN_BF16
   // fused geometries); elsewhere the forward writes them and needs the forward layout
-  const bool cols = !(with_backward == DCN_WS_FORWARD_NO_COLUMNS && g.dt == DCN_BF16 &&
-                      dcn::fused_fwd_bf16_ok(g));
+  const bool cols = !(with_backward == DCN_WS_FORWARD_NO_COLUMNS && fwd_can_skip_columns(g));
   *bytes = ws_layout(g, with_backward == 1, cols).total;
   return DCN_OK;
 }
@@ -1081,8 +1121,9 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
     using dcn::bf16_t;
     auto C = [](const float* p) { return reinterpret_cast<const bf16_t*>(p); };
     auto M = [](float* p) { return reinterpret_cast<bf16_t*>(p); };
-    // a DCN_FWD_FUSED_NOCOL forward left no columns in this workspace: recompute them
-    const bool col_valid = (flags & DCN_BWD_COL_IN_WS) != 0 && !ws_is_nocol(h, ws);
+    // the columns are read only where this handle's last forward on this workspace wrote
+    // them (not a DCN_FWD_FUSED_NOCOL / NO_COLUMNS forward); otherwise they are recomputed
+    const bool col_valid = (flags & DCN_BWD_COL_IN_WS) != 0 && ws_has_columns(h, ws);
     return backward_bf16(h, g, d->has_bias != 0, C(x), C(off), C(w_off), C(w), C(grad_out),
                          M(grad_x), M(grad_w), M(grad_b), M(grad_w_off), M(grad_b_off),
                          M(grad_off_out), base, L, col_valid);
@@ -1728,6 +1769,23 @@ int dcn_debug_force_generic(int on) {
 int dcn_debug_fused_workgroups(int n) {
   if (n < 0) return fail(DCN_ERR_INVALID, "dcn_debug_fused_workgroups: negative count");
   dcn::set_fused_workgroups(n);
+  return DCN_OK;
+}
+
+int dcn_debug_dw_parts(const dcn_desc* d, int* planes, int n, int* capacity) {
+  if (!planes || !capacity || n < DW_PATHS)
+    return fail(DCN_ERR_INVALID, "dcn_debug_dw_parts: bad argument");
+  Geo g;
+  DCN_TRY(make_geo(d, &g));
+  dw_parts(g, planes);
+  *capacity = ws_layout(g, true).parts_planes;
+  return DCN_OK;
+}
+
+int dcn_debug_col_ws_records(dcn_handle* h, int* n) {
+  if (!h || !n) return fail(DCN_ERR_INVALID, "dcn_debug_col_ws_records: bad argument");
+  std::lock_guard<std::mutex> lk(h->col_ws_mu);
+  *n = (int)h->col_ws.size();
   return DCN_OK;
 }
 

@@ -1713,8 +1713,11 @@ static void bwd_bf16_lds(const Geo& g, const MfmaStage& ms, size_t* lds_w, size_
 bool offset_bwd_bf16_ok(const Geo& g) {
   MfmaStage ms;
   // (H·W % 8 and W % 4: a chunk's pixel runs start 8-byte aligned in every channel plane)
+  // offset_dgrad_bf16 addresses one image's x (bf16) and channels-last ∂x (fp32) planes
+  // through buffer resources with 32-bit byte offsets (a tall plane wrapped them)
   if (!(g.dt == DCN_BF16 && mfma_stage(g, &ms) && g.C % 64 == 0 && g.HWi % 8 == 0 &&
-        g.W % 4 == 0 && g.kh * g.kw * j8(g.J) <= 256 && !get_force_generic()))
+        g.W % 4 == 0 && g.kh * g.kw * j8(g.J) <= 256 && !get_force_generic() &&
+        (size_t)g.HWi * g.C * 4 < ((size_t)1 << 31)))
     return false;
   size_t lw, lx;
   bwd_bf16_lds(g, ms, &lw, &lx);

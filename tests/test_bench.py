@@ -164,3 +164,71 @@ def test_config4_leg_is_wired(bench):
                             lambda s, w, n: {"x": 1}, lambda: None)
     assert res["n_gpus"] == 8 and res["global_batch"] == 512 and res["fwd_paths_ms_per_step"] is None
     assert "all-reduce" in res["workload"]
+
+
+def test_scope_rooflines_use_survey_work(bench):
+    """Every timed scope against its bound, the longest first (the dominant kernel)."""
+    c3 = bench.CONFIGS[3]
+    km = {"gemm_fwd": 1.6, "im2col": 0.4, "col2im": 0.52, "offset_fwd": 0.2, "offset_bwd": 0.4,
+          "bias_fwd": 0.06, "unknown_scope": 9.0}
+    r = bench.scope_rooflines(km, c3, 64, 56, 56)
+    assert [e["kernel"] for e in r] == ["gemm_fwd", "col2im", "im2col", "offset_bwd",
+                                        "offset_fwd", "bias_fwd"]
+    by = {e["kernel"]: e for e in r}
+    assert by["im2col"]["algorithmic_bytes"] == 2_069_659_648  # SURVEY §8(d) K1
+    assert by["col2im"]["algorithmic_bytes"] == 2_289_631_232  # SURVEY §8(d) K5
+    assert by["gemm_fwd"]["algorithmic_flop"] == 236_760_072_192
+    # offset conv: 2·M·K·2N = 16.65 GFLOP at config 3, its backward twice that
+    assert abs(by["offset_fwd"]["algorithmic_flop"] - 16.65e9) < 0.01e9
+    assert by["offset_bwd"]["algorithmic_flop"] == 2 * by["offset_fwd"]["algorithmic_flop"]
+    assert by["gemm_fwd"]["peak"] == 157.3 and by["im2col"]["peak"] == bench.HBM_PEAK_GBS
+    c5 = bench.CONFIGS[5]  # 4 deform groups: J = 72 offset channels
+    r5 = {e["kernel"]: e for e in bench.scope_rooflines({"im2col": 0.1}, c5, 64, 6, 6)}
+    assert r5["im2col"]["algorithmic_bytes"] == 4 * (64 * 512 * 14 * 14 + 64 * 72 * 36
+                                                      + 64 * 36 * 9 * 512)
+
+
+@pytest.mark.parametrize("num", [2, 5])
+def test_extra_config_legs_are_wired(bench, num):
+    """BASELINE configs 2 (fp32 forward only, vs CPU) and 5 (the
+    DCNv1 option set) are timed in the default N=1 run through the same timed() / warmup /
+    steps and reported under `config2` / `config5` with kernel times, the dominant scope's
+    roofline and, for config 2, its own CPU baseline. Stubbed device: only the wiring runs."""
+    import argparse
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "jittor-dcn_amd"))
+    torch = pytest.importorskip("torch")
+    import dcn_dp
+    import dcn_runtime as rt
+    cfg = bench.CONFIGS[num]
+    wl = bench.Workload(cfg, rt, torch, torch.device("cpu"), dcn_dp, seed=6000 + num)
+    assert wl.desc(cfg["B"]).dtype == rt.DCN_F32
+    calls = {}
+
+    def make_step(w, nb, seed):
+        calls["make_step"] = (w.cfg is cfg, nb)
+        return (lambda: None), ()
+
+    def timed(step, steps):
+        calls["timed"] = steps
+        return 0.1e-3 * steps
+
+    km = ({"offset_fwd": 0.01, "im2col": 0.02, "gemm_fwd": 0.04, "bias_fwd": 0.01} if num == 2
+          else {"gemm_fwd": 0.08, "gemm_dw": 0.09, "gemm_dcol": 0.08, "col2im": 0.05})
+    cpu = {"value": 0.005, "unit": "Gsamples/s"} if num == 2 else None
+    args = argparse.Namespace(warmup=2, steps=5)
+    res = bench.extra_config_leg(num, args, wl, rt, make_step, timed, lambda s, n: km,
+                                 lambda: None, cpu)
+    assert calls["make_step"] == (True, cfg["B"]) and calls["timed"] == 5
+    Ho, Wo = rt.out_shape(wl.desc(cfg["B"]))
+    assert (Ho, Wo) == ((56, 56) if num == 2 else (6, 6))
+    assert res["samples_per_step"] == cfg["B"] * Ho * Wo * 9
+    assert abs(res["value"] - res["samples_per_step"] / 0.1e-3 / 1e9) < 1e-4
+    assert res["workload"].startswith(f"config{num}: B={cfg['B']}/GPU")
+    assert ("fwd only" in res["workload"]) == (num == 2)
+    assert res["roofline"]["kernel"] == max(km, key=km.get)
+    assert len(res["rooflines_other"]) == len(km) - 1
+    if num == 2:
+        assert res["cpu_baseline"] is cpu and res["gpu_over_cpu"] > 1
+    else:
+        assert res["cpu_baseline"] is None

@@ -90,3 +90,27 @@ def test_no_device_fails_loudly():
     with pytest.raises(RuntimeError, match="dcn_create"):
         rt.Handle(0)
     assert rt.last_error() != ""
+
+
+@pytest.mark.parametrize("shape", [dict(C=256, O=256, H=28, W=28), dict(C=64, O=128, H=13, W=17),
+                                   dict(C=32, O=32, H=9, W=11, stride=(2, 2))])
+def test_dw_partials_fit_the_workspace_layout(shape):
+    """every ∂W path writes its partial planes into the workspace's
+    `parts` region before the fixed-order sum. For every batch size 1..64, fp32 and bf16, each
+    path's plane count (from the functions the backward itself uses) must fit what the
+    dcn_forward + dcn_backward layout holds. Host only: no device call."""
+    import ctypes
+    L = rt.load()
+    planes, cap = (ctypes.c_int * 3)(), ctypes.c_int()
+    for dt in (rt.DCN_F32, rt.DCN_BF16):
+        seen = set()
+        for B in range(1, 65):
+            d = desc(B=B, dtype=dt, **shape)
+            rt.check(L.dcn_debug_dw_parts(ctypes.byref(d), planes, 3, ctypes.byref(cap)))
+            n = list(planes)
+            assert n[0] == B  # one plane per image
+            assert max(n) <= cap.value, (dt, B, n, cap.value)
+            seen.add(tuple(v > 0 for v in n))
+        if dt == rt.DCN_BF16 and shape["C"] == 256:
+            # the grouped GEMM (B % 16 == 0, B > 16) and the recomputed-column kernel apply
+            assert (True, True, True) in seen

@@ -224,13 +224,18 @@ def test_bf16_config4_full_size_bitwise_reproducible(gpu_handle):
                                       err_msg=k)
 
 
-def test_bf16_dcol_kernel_vs_vendor_gemm(gpu_handle, monkeypatch):
+@pytest.mark.parametrize("B,H,W", [(4, 20, 19), (24, 28, 28), (64, 28, 28)])
+def test_bf16_dcol_kernel_vs_vendor_gemm(gpu_handle, monkeypatch, B, H, W):
     """The ∂columns of dcol_bf16 (short-K streaming kernel) against the vendor GEMM's on the
     same inputs (a handle created with DCN_DCOL_GEMM=1): every downstream tensor within the
     bf16 bound of the other, and the forward tensors bit for bit (the kernel is backward
     only). Both sum the same 256 exact bf16 products in fp32, in different orders, then
-    round to bf16 once, so ∂col elements may differ by an ulp; ∂x / ∂offset sum them."""
-    bits, _, s = _case(13, B=4, C=256, O_=256, H=20, W=19, off_scale=1.5)
+    round to bf16 once, so ∂col elements may differ by an ulp; ∂x / ∂offset sum them.
+    Geometries (ADVICE r04): 1,520 pixels = 48 tiles of 32 in 24 ranges (one tile per wave);
+    B = 24 at 28x28, 21 tiles per range (3 or 2 per wave: the second register set and the odd
+    tail); config 4 itself (56 per range, 7 per wave). C = 512 (18 row groups) is outside
+    DCN_BF16 (C <= 256), so no op reaches it."""
+    bits, _, s = _case(13, B=B, C=256, O_=256, H=H, W=W, off_scale=1.5)
     a = _device(gpu_handle, bits, s)
     monkeypatch.setenv("DCN_DCOL_GEMM", "1")
     h2 = rt.Handle(0)

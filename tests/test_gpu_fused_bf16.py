@@ -240,3 +240,45 @@ def test_forward_no_columns_flag_small_workspace(gpu_handle):
     finally:
         h.set_fwd_path(rt.DCN_FWD_AUTO)
         D.free()
+
+
+def test_column_record_stays_bounded(gpu_handle):
+    """the handle's per-workspace column record must not grow with the number of
+    distinct workspaces. 100 no-grad forwards (DCN_FWD_NO_COLUMNS) on fresh workspaces add
+    nothing; 300 column-storing forwards on fresh workspaces keep at most 256 records (the
+    oldest dropped). A backward with DCN_BWD_COL_IN_WS on a dropped workspace — whose column
+    region later forwards have overwritten — recomputes the columns: every gradient bit for
+    bit the unfused schedule's (deform_conv.py:41-80 and its autodiff)."""
+    h = gpu_handle
+    c = _case(950, B=1, C=64, O_=256, H=28, W=28, off_scale=1.5)
+    ref = _run(h, c, rt.DCN_FWD_UNFUSED)[2]
+    D = Buf(h)
+    n = ctypes.c_int()
+
+    def records():
+        rt.check(h.lib.dcn_debug_col_ws_records(h.h, ctypes.byref(n)))
+        return n.value
+
+    try:
+        desc, _, p = _upload_case(D, c)
+        wsb = rt.workspace_bytes(desc, True)
+        big = D.zeros(wsb + 400 * 256)  # workspace i at big + 256·i: all distinct addresses
+        ws = lambda i: big + 256 * i
+        r0 = records()
+        for i in range(100):
+            _fwd(h, desc, p, ws(i), wsb, rt.DCN_FWD_NO_COLUMNS)
+        assert records() == r0
+        for i in range(300):
+            _fwd(h, desc, p, ws(100 + i), wsb, 0)
+        assert records() <= 256
+        _bwd(h, desc, p, ws(100), wsb)  # dropped long ago, its columns overwritten
+        got = _grads(D, c, p)
+        for k in got:
+            np.testing.assert_array_equal(got[k], ref[k], err_msg=f"∂{k} on a dropped workspace")
+        _fwd(h, desc, p, ws(399), wsb, 0)  # the newest record: its columns are read
+        _bwd(h, desc, p, ws(399), wsb)
+        got = _grads(D, c, p)
+        for k in got:
+            np.testing.assert_array_equal(got[k], ref[k], err_msg=f"∂{k} on a recorded workspace")
+    finally:
+        D.free()
