@@ -387,8 +387,9 @@ int dcn_debug_force_generic(int on);
 int dcn_debug_fused_workgroups(int n);
 /* The ∂W partial planes ([O][K] fp32 each) that each backward path of this geometry writes
  * into the workspace before its fixed-order sum — planes[0] one per image, planes[1] the
- * grouped bf16 GEMM, planes[2] the recomputed-column bf16 kernel (0 where a path does not
- * apply; n >= 3) — and in *capacity the planes the dcn_forward + dcn_backward workspace
+ * grouped bf16 GEMM, planes[2] the recomputed-column bf16 kernel, planes[3] the bf16
+ * streaming kernel's pixel ranges (0 where a path does not apply; n >= 4) — and in
+ * *capacity the planes the dcn_forward + dcn_backward workspace
  * layout holds. Host only (no device call): the CPU tests check every count fits. */
 int dcn_debug_dw_parts(const dcn_desc* d, int* planes, int n, int* capacity);
 /* Number of workspaces the handle currently records as holding a DCN_BF16 forward's

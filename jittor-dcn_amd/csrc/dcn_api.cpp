@@ -115,11 +115,17 @@ int dw_groups(const Geo& g) {
 // sizes `parts` from the largest, and every backward checks its own count against what the
 // layout holds (the region once held fewer planes than a kernel
 // wrote).
-enum { DW_PER_IMAGE, DW_GROUPED, DW_FUSED, DW_PATHS };
+// dw_stream_bf16 (the stored-column bf16 ∂W kernel, csrc/dcn_dw_bf16.hip) writes one plane
+// per pixel range.
+enum { DW_PER_IMAGE, DW_GROUPED, DW_FUSED, DW_STREAM, DW_PATHS };
+bool dw_stream_applies(const Geo& g) {
+  return g.dt == DCN_BF16 && dcn::dw_stream_bf16_ok(g.K, g.O, (long)g.B * g.HW);
+}
 void dw_parts(const Geo& g, int n[DW_PATHS]) {
   n[DW_PER_IMAGE] = g.B;
   n[DW_GROUPED] = dw_groups(g);
   n[DW_FUSED] = g.dt == DCN_BF16 && dcn::fused_dw_bf16_ok(g) ? dcn::fused_dw_bf16_groups(g) : 0;
+  n[DW_STREAM] = dw_stream_applies(g) ? dcn::dw_stream_bf16_ranges(g.K, (long)g.B * g.HW) : 0;
 }
 int dw_parts_max(const Geo& g) {
   int n[DW_PATHS];
@@ -226,6 +232,8 @@ struct dcn_handle {
   int fwd_path = DCN_FWD_AUTO;  // dcn_set_fwd_path
   // bf16 ∂columns on the vendor GEMM instead of dcol_bf16 (DCN_DCOL_GEMM=1: the A/B switch)
   bool dcol_gemm = false;
+  // bf16 ∂W on the vendor GEMM instead of dw_stream_bf16 (DCN_DW_GEMM=1: the A/B switch)
+  bool dw_gemm = false;
   // workspaces whose last DCN_BF16 forward on this handle wrote its columns into them, most
   // recent last. A DCN_BWD_COL_IN_WS backward reads the columns only from a workspace listed
   // here and recomputes them otherwise (a forward under DCN_FWD_FUSED_NOCOL or
@@ -687,21 +695,35 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
     dcn::launch_channel_sum_bf16(gout, g.B, g.O, g.HW, F32(L.gb32), st, exch ? nullptr : gb);
   }
   bf16_t* goutT = BF(L.goutT);
-  const int dwg = dw_fused ? 0 : dw_groups(g);
+  // ∂W over the stored (or just recomputed) columns: the streaming MFMA kernel where it
+  // applies (O = 256, K % 256 == 0: config 4), else the vendor GEMM (grouped where B allows)
+  const long npix = (long)g.B * g.HW;
+  const bool dw_stream = !dw_fused && !h->dw_gemm && dw_stream_applies(g) &&
+                         !dcn::get_force_generic();
+  const int dwg = dw_fused || dw_stream ? 0 : dw_groups(g);
+  bool have_goutT = false;  // ∂outT (shared by the ∂W kernels and the ∂col product)
   {
     ProfScope ps(h, DCN_K_GEMM_DW);
     dcn::GemmSpec sp;
     sp.bf16_ab = true;
-    const int nparts = dw_fused ? dcn::fused_dw_bf16_groups(g) : dwg > 0 ? dwg : g.B;
+    const int nparts = dw_fused    ? dcn::fused_dw_bf16_groups(g)
+                       : dw_stream ? dcn::dw_stream_bf16_ranges(g.K, npix)
+                       : dwg > 0   ? dwg
+                                   : g.B;
     if (nparts > L.parts_planes)  // the ∂W kernels below write nparts planes into `parts`
       return fail(DCN_ERR_WORKSPACE, "∂W partials: " + std::to_string(nparts) +
                                          " planes, the workspace layout holds " +
                                          std::to_string(L.parts_planes));
     if (dw_fused) {
       HIP_TRY(dcn::launch_fused_dw_bf16(g, xT, off32, gout, F32(L.parts), st));
+    } else if (dw_stream) {
+      HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(gout, goutT, g.B, g.O, g.HW, st));
+      have_goutT = true;
+      HIP_TRY(dcn::launch_dw_stream_bf16(goutT, col, F32(L.parts), g.K, g.O, npix, st));
     } else if (dwg > 0) {
       // grouped NT over the pixels of B/dwg images (∂outT first, shared with ∂col)
       HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(gout, goutT, g.B, g.O, g.HW, st));
+      have_goutT = true;
       const int pg = (g.B / dwg) * g.HW;
       sp.tb = true;
       sp.m = g.K; sp.n = g.O; sp.k = pg;
@@ -725,8 +747,7 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
                    exch && has_bias ? gb : nullptr));
   {
     ProfScope ps(h, DCN_K_GEMM_DCOL);  // ∂colT = ∂outT · Wf over the whole batch, bf16 out
-    if (dwg <= 0) HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(gout, goutT, g.B, g.O, g.HW, st));
-    const long npix = (long)g.B * g.HW;
+    if (!have_goutT) HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(gout, goutT, g.B, g.O, g.HW, st));
     if (!h->dcol_gemm && dcn::dcol_bf16_ok(g.K, g.O, npix) && !dcn::get_force_generic()) {
       // short-K streaming kernel (csrc/dcn_dcol_bf16.hip) after its Wf swizzle (in line:
       // on the side stream it ran beside the ∂W GEMM and cost that 10 µs, r04 dcol5)
@@ -843,6 +864,7 @@ int dcn_create(int device, dcn_handle** out) {
     return fail(DCN_ERR_HIP, std::string("dcn_create: ") + hipGetErrorString(e));
   }
   if (const char* f = std::getenv("DCN_DCOL_GEMM")) h->dcol_gemm = std::atoi(f) != 0;
+  if (const char* f = std::getenv("DCN_DW_GEMM")) h->dw_gemm = std::atoi(f) != 0;
   std::string gerr;
   if (dcn::gemm_engine_create(&h->gemm, &gerr) != 0) {
     (void)hipStreamDestroy(h->own);

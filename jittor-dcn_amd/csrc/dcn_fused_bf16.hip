@@ -186,17 +186,21 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
   const int novf = min(cnt[0], kOvf);
 
   // ---- per-thread production units: u = tid, tid + 256 (u < kUnits): slot u>>2, 8-ch group u&3
+  // (wave-uniform count: waves 0-2 hold two unit sets, wave 3 one)
   const int nu = (tid + 256 < kUnits) ? 2 : 1;
   int uslot[2], ucg[2];
-  unsigned ucol[2];  // the slot's column row in image b (elements), or ~0u outside the output
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int u = min(tid + 256 * k, kUnits - 1);
     uslot[k] = u >> 2;
     ucg[k] = u & 3;
-    const int h = h0 + uslot[k] / kTW, w = w0 + uslot[k] % kTW;
-    ucol[k] = (h < g.Ho && w < g.Wo) ? (unsigned)(h * g.Wo + w) * (unsigned)g.K : ~0u;
   }
+  // column stores (STORE): a wave's unit set k covers slots 16·wave + 64k + 0..15, the two
+  // 32-channel halves of one tap in consecutive steps (B buffers 0 and 1). After the second
+  // half, lane L stores 16-B piece L & 7 of slot 16·wave + 64k + 8i + (L >> 3)'s 128-B column
+  // line (i = 0, 1), read back from the two B buffers: every store instruction writes 8 whole
+  // lines (half-line stores one step apart wrote 1.15x the column bytes).
+  // The slots' column rows are recomputed per store (registers are at the kernel's limit).
 
   f32x4 acc[4][kPB];
 #pragma unroll
@@ -244,13 +248,28 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
           }
         }
         *reinterpret_cast<uint4*>(bt + buf * kSlots * kBPitch + slot * kBPitch + cg * 16) = o;
-        if (STORE && ucol[k] != ~0u) {
-          unsigned* dst = reinterpret_cast<unsigned*>(
-              colT + (size_t)b * g.HW * g.K + ucol[k] + (n * g.C + kCS * cs + 32 * hh + 8 * cg));
-          __builtin_nontemporal_store(o.x, dst);
-          __builtin_nontemporal_store(o.y, dst + 1);
-          __builtin_nontemporal_store(o.z, dst + 2);
-          __builtin_nontemporal_store(o.w, dst + 3);
+      }
+    }
+  };
+  // both halves of tap n of slice cs are in the B buffers (0: channels 0-31, 1: 32-63): each
+  // wave stores its own slots' whole column lines (no other wave writes those slots' units,
+  // and this wave's next production comes after this in program order)
+  auto store_cols = [&](int cs, int n) {
+    const int j = lane & 7;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (k < nu) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int sl = 16 * wave + 64 * k + 8 * i + (lane >> 3);
+          const v4u v = *reinterpret_cast<const v4u*>(bt + (j >> 2) * kSlots * kBPitch +
+                                                      sl * kBPitch + (j & 3) * 16);
+          const int h = h0 + sl / kTW, w = w0 + sl % kTW;
+          if (sl < kSlots && h < g.Ho && w < g.Wo)
+            __builtin_nontemporal_store(
+                v, reinterpret_cast<v4u*>(colT + (size_t)b * g.HW * g.K +
+                                          (unsigned)(h * g.Wo + w) * (unsigned)g.K +
+                                          (n * g.C + kCS * cs + 8 * j)));
         }
       }
     }
@@ -315,6 +334,7 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
       produce(cs, s + 1, 1);
       mfma_step(0, aE);
       __syncthreads();
+      if (STORE) store_cols(cs, s >> 1);
       if (s + 2 < spq) {
         load_a(cs, s + 2, aE);
         produce(cs, s + 2, 0);

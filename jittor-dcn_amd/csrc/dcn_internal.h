@@ -208,6 +208,13 @@ hipError_t launch_roi_pool_bwd(const RoiGeo& q, const float* f, const float* roi
 
 // dcn_dcol_bf16.hip: the bf16 ∂columns ∂colT[p][k] = Σ_o ∂outT[p][o] · Wf[o][k] (O = 256,
 // K % 256 == 0) as a short-K streaming kernel; wz = K·O bf16, Wf in its A-fragment order
+// dcn_dw_bf16.hip: ∂Wf partial planes [ranges][O][K] (fp32) = Σ over each pixel range of
+// ∂outT[p][o] · col[p][k] (bf16 operands, O == 256, K % 256 == 0); launch_sum_partials over
+// dw_stream_bf16_ranges planes gives ∂W.
+bool dw_stream_bf16_ok(int K, int O, long npix);
+int dw_stream_bf16_ranges(int K, long npix);
+hipError_t launch_dw_stream_bf16(const bf16_t* goutT, const bf16_t* col, float* parts, int K,
+                                 int O, long npix, hipStream_t s);
 bool dcol_bf16_ok(int K, int O, long npix);
 hipError_t launch_dcol_bf16_swizzle(const bf16_t* w, int K, int O, bf16_t* wz, hipStream_t s);
 hipError_t launch_dcol_bf16(const bf16_t* wz, const bf16_t* goutT, bf16_t* col, int K, int O,

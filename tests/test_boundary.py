@@ -101,16 +101,17 @@ def test_dw_partials_fit_the_workspace_layout(shape):
     dcn_forward + dcn_backward layout holds. Host only: no device call."""
     import ctypes
     L = rt.load()
-    planes, cap = (ctypes.c_int * 3)(), ctypes.c_int()
+    planes, cap = (ctypes.c_int * 4)(), ctypes.c_int()
     for dt in (rt.DCN_F32, rt.DCN_BF16):
         seen = set()
         for B in range(1, 65):
             d = desc(B=B, dtype=dt, **shape)
-            rt.check(L.dcn_debug_dw_parts(ctypes.byref(d), planes, 3, ctypes.byref(cap)))
+            rt.check(L.dcn_debug_dw_parts(ctypes.byref(d), planes, 4, ctypes.byref(cap)))
             n = list(planes)
             assert n[0] == B  # one plane per image
             assert max(n) <= cap.value, (dt, B, n, cap.value)
             seen.add(tuple(v > 0 for v in n))
         if dt == rt.DCN_BF16 and shape["C"] == 256:
-            # the grouped GEMM (B % 16 == 0, B > 16) and the recomputed-column kernel apply
-            assert (True, True, True) in seen
+            # the grouped GEMM (B % 16 == 0, B > 16), the recomputed-column kernel and the
+            # streaming kernel (O == 256) apply
+            assert (True, True, True, True) in seen

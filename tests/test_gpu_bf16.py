@@ -252,6 +252,44 @@ def test_bf16_dcol_kernel_vs_vendor_gemm(gpu_handle, monkeypatch, B, H, W):
                                       err_msg=k)
 
 
+@pytest.mark.parametrize("B,H,W,k", [(3, 13, 13, (3, 3)), (5, 23, 23, (3, 3)),
+                                     (24, 28, 28, (3, 3)), (64, 28, 28, (3, 3)),
+                                     (2, 20, 20, (1, 1))])
+def test_bf16_dw_stream_vs_vendor_gemm(gpu_handle, monkeypatch, B, H, W, k):
+    """∂W of dw_stream_bf16 (split-K streaming MFMA kernel over the stored columns,
+    csrc/dcn_dw_bf16.hip) against the vendor GEMM's (a handle created with DCN_DW_GEMM=1) on
+    the same inputs, and against the oracle: both sum exact bf16 products in fp32 (different
+    orders), so ∂W may differ by one bf16 rounding; every other tensor is untouched by the
+    choice (bit for bit). Geometries: 507 pixels = 16 stages of 32 in 16 one-stage ranges (a
+    27-pixel last stage: the masked tail); 2,645 pixels (a 21-pixel last stage); B = 24 at
+    28x28 (28 ranges of 21 stages: the unrolled ring plus a one-stage tail); config 4 (56
+    stages per range); a 1x1 kernel (K = 256: one column tile, 25 one-stage ranges)."""
+    pad = (1, 1) if k == (3, 3) else (0, 0)
+    bits, v, s = _case(17 + B, B=B, C=256, O_=256, H=H, W=W, off_scale=1.5, k=k, p=pad)
+    a = _device(gpu_handle, bits, s, pad=pad)
+    monkeypatch.setenv("DCN_DW_GEMM", "1")
+    h2 = rt.Handle(0)
+    try:
+        b = _device(h2, bits, s, pad=pad)
+    finally:
+        h2.close()
+    np.testing.assert_array_equal(a[0].view(np.uint32), b[0].view(np.uint32), err_msg="out")
+    np.testing.assert_array_equal(a[1].view(np.uint32), b[1].view(np.uint32), err_msg="off")
+    for name in ("x", "offset", "bias", "offset_conv.weight", "offset_conv.bias"):
+        np.testing.assert_array_equal(a[2][name].view(np.uint32), b[2][name].view(np.uint32),
+                                      err_msg=name)
+    gw, gv = a[2]["weight"].astype(np.float64), b[2]["weight"].astype(np.float64)
+    rms = float(np.sqrt(np.mean(gv * gv)))
+    lim = 2.0 ** -7 * np.abs(gv) + 2.0 ** -14 * rms
+    assert np.all(np.abs(gw - gv) <= lim), \
+        f"∂W: {int((np.abs(gw - gv) > lim).sum())} elements past one bf16 rounding of the GEMM's"
+    if B <= 5:
+        _, _, cache = O.forward(v["x"], v["w_off"], v["b_off"], v["w"], v["b"], s, pad,
+                                offsets=a[1])
+        rg = O.backward(cache, v["grad_out"])
+        assert_bf16_close(a[2]["weight"], rg["weight"], "∂W vs oracle")
+
+
 @pytest.mark.parametrize("k,pad,C,H,W", [((1, 3), (0, 1), 24, 13, 11), ((3, 1), (1, 0), 24, 13, 11),
                                          ((2, 2), (1, 1), 24, 13, 11),
                                          ((1, 3), (0, 1), 64, 9, 8), ((2, 2), (1, 1), 128, 6, 12)])
