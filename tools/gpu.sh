@@ -22,7 +22,7 @@ prof() {  # prof TAG ARGS...
   local tag=$1
   shift
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_$tag -o run --output-format csv -- python3 bench.py "$@" > gpurun_out/${T}_$tag.log 2>&1 || { tail -5 gpurun_out/${T}_$tag.log; return 1; }
-  python3 tools/kstats.py gpurun_out/${T}_$tag | head -30
+  python3 tools/kstats.py gpurun_out/${T}_$tag --top=30
 }
 for S in "$@"; do
   echo "== $S"
