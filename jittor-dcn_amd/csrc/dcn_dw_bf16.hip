@@ -41,18 +41,32 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) void gvoid;
 typedef __attribute__((address_space(3))) void lvoid;
 
+// Pipeline shape (compile-time; the A/B builds of DESIGN.md §4 set them with -D): DW_PX
+// pixels per stage (16 or 32), DW_RING LDS stages, DW_NT = 1 streams the column DMAs with the
+// non-temporal policy (the columns are read once; ∂outT is re-read by every column tile).
+#ifndef DW_PX
+#define DW_PX 32
+#endif
+#ifndef DW_RING
+#define DW_RING 4
+#endif
+#ifndef DW_NT
+#define DW_NT 0
+#endif
 constexpr int kDwO = 256;                          // output channels: the tile's rows
 constexpr int kDwN = 256;                          // ∂W columns per tile
-constexpr int kDwPx = 32;                          // pixels per stage
-constexpr int kDwRing = 4;                         // LDS stages
+constexpr int kDwPx = DW_PX;                       // pixels per stage
+constexpr int kDwRing = DW_RING;                   // LDS stages
 constexpr int kDwAhead = kDwRing - 1;              // stages in flight while one is consumed
 constexpr int kDwRowB = 512;                       // one pixel row of either operand (256 bf16)
-constexpr int kDwOpB = kDwPx * kDwRowB;            // 16 KiB per operand per stage
+constexpr int kDwOpB = kDwPx * kDwRowB;            // 16 KiB per operand per 32-pixel stage
 constexpr int kDwStageB = 2 * kDwOpB;              // A (∂outT) then B (columns)
-constexpr int kDwLds = kDwRing * kDwStageB;        // 128 KiB
+constexpr int kDwLds = kDwRing * kDwStageB;        // 128 KiB (4 × 32 px)
 constexpr int kDwWaves = 8;
 constexpr int kDwGlds = kDwStageB / (kDwWaves * 1024);  // DMA instructions per wave per stage
-static_assert(kDwGlds == 4, "vmcnt counts below assume 4 DMAs per wave per stage");
+constexpr int kDwOpI = kDwPx / 2;                  // DMA instructions per operand (2 rows each)
+static_assert(kDwPx == 16 || kDwPx == 32, "stage = one or two 16-pixel k-steps");
+static_assert(kDwRing >= 3 && kDwRing <= 8, "ring depth");
 static_assert(kDwLds <= 160 * 1024, "one workgroup per CU");
 
 // byte offset of 16-B chunk `ch` of row `r` in an operand image
@@ -78,6 +92,40 @@ __global__ __launch_bounds__(kDwWaves * 64, 1) void dw_stream_bf16(
   // dynamic array: s_waitcnt vmcnt(0) before the first read of every stage)
   __shared__ __attribute__((aligned(1024))) char ring0[kDwStageB], ring1[kDwStageB],
       ring2[kDwStageB], ring3[kDwStageB];
+#if DW_RING > 4
+  __shared__ __attribute__((aligned(1024))) char ring4[kDwStageB];
+#endif
+#if DW_RING > 5
+  __shared__ __attribute__((aligned(1024))) char ring5[kDwStageB];
+#endif
+#if DW_RING > 6
+  __shared__ __attribute__((aligned(1024))) char ring6[kDwStageB];
+#endif
+#if DW_RING > 7
+  __shared__ __attribute__((aligned(1024))) char ring7[kDwStageB];
+#endif
+  char* const slots[8] = {ring0, ring1, ring2, ring3,
+#if DW_RING > 4
+                          ring4,
+#else
+                          nullptr,
+#endif
+#if DW_RING > 5
+                          ring5,
+#else
+                          nullptr,
+#endif
+#if DW_RING > 6
+                          ring6,
+#else
+                          nullptr,
+#endif
+#if DW_RING > 7
+                          ring7
+#else
+                          nullptr
+#endif
+  };
   const int bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int tile = wg % ntile, range = wg / ntile;
@@ -99,13 +147,17 @@ __global__ __launch_bounds__(kDwWaves * 64, 1) void dw_stream_bf16(
     j = min(j, nst - 1);  // past the range: re-read its last stage (L2), never read back
 #pragma unroll
     for (int u = 0; u < kDwGlds; ++u) {
-      const int ii = u * kDwWaves + w, op = ii >> 4, i = ii & 15;
+      const int ii = u * kDwWaves + w, op = ii / kDwOpI, i = ii % kDwOpI;
       const int row = 2 * i + lrow;
       const unsigned ch = (unsigned)(lpc ^ (4 * (row & 3)));
       const int p = min(px0 + j * kDwPx + row, npix - 1);  // past the end: re-read the last row
       const char* src = opbase[op] + ((unsigned)p * opstride[op] + ch * 16u);
-      __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(slot + op * kDwOpB + i * 1024), 16,
-                                       0, 0);
+      if (op == 0 || !DW_NT)
+        __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(slot + op * kDwOpB + i * 1024),
+                                         16, 0, 0);
+      else  // aux 2: the non-temporal policy (MI355X_MICROARCH.md nt-weights)
+        __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(slot + op * kDwOpB + i * 1024),
+                                         16, 0, 2);
     }
   };
 
@@ -145,7 +197,7 @@ __global__ __launch_bounds__(kDwWaves * 64, 1) void dw_stream_bf16(
   // fragments, so their products vanish
   auto compute = [&](const char* slot, int nvalid) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < kDwPx / 16; ++ks) {
       const char* base = slot + ks * 16 * kDwRowB;
       bf16x8 a[4], b[2];
 #pragma unroll
@@ -175,7 +227,8 @@ __global__ __launch_bounds__(kDwWaves * 64, 1) void dw_stream_bf16(
   // every step and on every path: hipcc's own wait before a slot's first read then never
   // drains the queue)
   auto step = [&](int s, char* cur, char* refill) {
-    // this wave's DMAs of stage s have landed once only those of s + 1, s + 2 are pending
+    // this wave's DMAs of stage s have landed once only those of s + 1 .. s + kDwAhead - 1
+    // are pending
     vm_wait<(kDwAhead - 1) * kDwGlds>();
     // every wave's DMAs of stage s landed; every wave finished reading stage s - 1, whose
     // slot (`refill`) the DMA of stage s + kDwAhead now refills
@@ -185,20 +238,18 @@ __global__ __launch_bounds__(kDwWaves * 64, 1) void dw_stream_bf16(
     __builtin_amdgcn_sched_barrier(0);
     compute(cur, min(kDwPx, npix - (px0 + s * kDwPx)));
   };
-  static_assert(kDwRing == 4, "the unrolled ring below");
-  issue(0, ring0);
-  issue(1, ring1);
-  issue(2, ring2);
+  // (slot k + kDwRing - 1 is refilled while slot k is read; the loops are fully unrolled, so
+  // every slot pointer is a compile-time LDS object)
+#pragma unroll
+  for (int k = 0; k < kDwAhead; ++k) issue(k, slots[k]);
   int s = 0;
-  for (; s + 4 <= nst; s += 4) {
-    step(s, ring0, ring3);
-    step(s + 1, ring1, ring0);
-    step(s + 2, ring2, ring1);
-    step(s + 3, ring3, ring2);
+  for (; s + kDwRing <= nst; s += kDwRing) {
+#pragma unroll
+    for (int k = 0; k < kDwRing; ++k) step(s + k, slots[k], slots[(k + kDwRing - 1) % kDwRing]);
   }
-  if (s < nst) step(s, ring0, ring3);
-  if (s + 1 < nst) step(s + 1, ring1, ring0);
-  if (s + 2 < nst) step(s + 2, ring2, ring1);
+#pragma unroll
+  for (int k = 0; k < kDwRing - 1; ++k)
+    if (s + k < nst) step(s + k, slots[k], slots[(k + kDwRing - 1) % kDwRing]);
   vm_wait<0>();  // no DMA may land in LDS after the workgroup has ended
 
   // ---- partial plane `range`: D row i = o, column j = k; lane (n = l & 31, h = l >> 5),
