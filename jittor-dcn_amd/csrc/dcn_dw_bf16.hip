@@ -53,11 +53,22 @@ typedef __attribute__((address_space(3))) void lvoid;
 #ifndef DW_NT
 #define DW_NT 0
 #endif
+// DW_EARLY = 1: each step issues its DMAs BEFORE waiting at the stage barrier, into the slot
+// of stage s - 2 (every wave finished reading it before the previous barrier), so the refill
+// does not wait for the slowest wave; kDwRing - 2 stages ahead instead of kDwRing - 1.
+// DW_PIN = 1: a scheduling barrier after each stage's MFMAs keeps them ahead of the next
+// stage's wait and barrier (hipcc otherwise sinks them past the barrier, delaying the DMAs).
+#ifndef DW_EARLY
+#define DW_EARLY 0
+#endif
+#ifndef DW_PIN
+#define DW_PIN 0
+#endif
 constexpr int kDwO = 256;                          // output channels: the tile's rows
 constexpr int kDwN = 256;                          // ∂W columns per tile
 constexpr int kDwPx = DW_PX;                       // pixels per stage
 constexpr int kDwRing = DW_RING;                   // LDS stages
-constexpr int kDwAhead = kDwRing - 1;              // stages in flight while one is consumed
+constexpr int kDwAhead = kDwRing - 1 - DW_EARLY;   // stages issued ahead of the one consumed
 constexpr int kDwRowB = 512;                       // one pixel row of either operand (256 bf16)
 constexpr int kDwOpB = kDwPx * kDwRowB;            // 16 KiB per operand per 32-pixel stage
 constexpr int kDwStageB = 2 * kDwOpB;              // A (∂outT) then B (columns)
@@ -227,6 +238,16 @@ __global__ __launch_bounds__(kDwWaves * 64, 1) void dw_stream_bf16(
   // every step and on every path: hipcc's own wait before a slot's first read then never
   // drains the queue)
   auto step = [&](int s, char* cur, char* refill) {
+#if DW_EARLY
+    // every wave finished reading stage s - 2 before the previous step's barrier
+    issue(s + kDwAhead, refill);
+    __builtin_amdgcn_sched_barrier(0);
+    // this wave's DMAs of stage s have landed once only those of s + 1 .. s + kDwAhead are
+    // pending
+    vm_wait<kDwAhead * kDwGlds>();
+    __builtin_amdgcn_s_barrier();  // every wave's DMAs of stage s landed
+    __builtin_amdgcn_sched_barrier(0);
+#else
     // this wave's DMAs of stage s have landed once only those of s + 1 .. s + kDwAhead - 1
     // are pending
     vm_wait<(kDwAhead - 1) * kDwGlds>();
@@ -236,20 +257,24 @@ __global__ __launch_bounds__(kDwWaves * 64, 1) void dw_stream_bf16(
     __builtin_amdgcn_sched_barrier(0);
     issue(s + kDwAhead, refill);
     __builtin_amdgcn_sched_barrier(0);
+#endif
     compute(cur, min(kDwPx, npix - (px0 + s * kDwPx)));
+#if DW_PIN
+    __builtin_amdgcn_sched_barrier(0);
+#endif
   };
-  // (slot k + kDwRing - 1 is refilled while slot k is read; the loops are fully unrolled, so
+  // (slot k + kDwAhead is refilled while slot k is read; the loops are fully unrolled, so
   // every slot pointer is a compile-time LDS object)
 #pragma unroll
   for (int k = 0; k < kDwAhead; ++k) issue(k, slots[k]);
   int s = 0;
   for (; s + kDwRing <= nst; s += kDwRing) {
 #pragma unroll
-    for (int k = 0; k < kDwRing; ++k) step(s + k, slots[k], slots[(k + kDwRing - 1) % kDwRing]);
+    for (int k = 0; k < kDwRing; ++k) step(s + k, slots[k], slots[(k + kDwAhead) % kDwRing]);
   }
 #pragma unroll
   for (int k = 0; k < kDwRing - 1; ++k)
-    if (s + k < nst) step(s + k, slots[k], slots[(k + kDwRing - 1) % kDwRing]);
+    if (s + k < nst) step(s + k, slots[k], slots[(k + kDwAhead) % kDwRing]);
   vm_wait<0>();  // no DMA may land in LDS after the workgroup has ended
 
   // ---- partial plane `range`: D row i = o, column j = k; lane (n = l & 31, h = l >> 5),
