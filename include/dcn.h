@@ -385,6 +385,9 @@ int dcn_debug_force_generic(int on);
 /* Workgroup count of the fused forward's persistent grid (DCN_FWD_FUSED); 0 = one per CU.
  * Lets the parity tests walk many tiles (straddling images) through one workgroup. */
 int dcn_debug_fused_workgroups(int n);
+/* 1 = build K5's sample bins with the chunked three-kernel sort even where one block sort
+ * per image applies (H·W·kh·kw <= 8192); the parity tests compare the two bit for bit. */
+int dcn_debug_bins_chunked(int on);
 /* The ∂W partial planes ([O][K] fp32 each) that each backward path of this geometry writes
  * into the workspace before its fixed-order sum — planes[0] one per image, planes[1] the
  * grouped bf16 GEMM, planes[2] the recomputed-column bf16 kernel, planes[3] the bf16

@@ -1797,6 +1797,11 @@ int dcn_debug_force_generic(int on) {
   return DCN_OK;
 }
 
+int dcn_debug_bins_chunked(int on) {
+  dcn::set_bins_chunked(on);
+  return DCN_OK;
+}
+
 int dcn_debug_fused_workgroups(int n) {
   if (n < 0) return fail(DCN_ERR_INVALID, "dcn_debug_fused_workgroups: negative count");
   dcn::set_fused_workgroups(n);

@@ -251,6 +251,7 @@ hipError_t launch_gemm_split(int math, const GemmSpec& s, const float* A, const 
 // Selection of the im2col / col2im implementation (tests force the generic
 // global-memory kernels to cross-check the channels-last ones).
 void set_force_generic(int on);
+void set_bins_chunked(int on);
 int get_force_generic();
 
 }  // namespace dcn

@@ -33,6 +33,13 @@ static int g_force_generic = 0;
 
 
 void set_force_generic(int on) { g_force_generic = on; }
+// 1 = the chunked three-kernel bins even where one block sort per segment applies (the
+// parity tests compare the two bit for bit; dcn_debug_bins_chunked)
+#ifndef BINS_CHUNKED
+#define BINS_CHUNKED 0  // (an A/B build sets 1: tools/ab.sh)
+#endif
+static int g_bins_chunked = BINS_CHUNKED;
+void set_bins_chunked(int on) { g_bins_chunked = on; }
 int get_force_generic() { return g_force_generic; }
 
 // ---------------------------------------------------------------------------
@@ -728,6 +735,59 @@ __global__ __launch_bounds__(256) void bins_emit(Geo g, int nch, int NB,
     if (next > pos) copy_run(c, pos, next - pos, Rs[(size_t)c * NBp]);
     pos = next;
   }
+}
+
+// One workgroup per segment when the segment's samples fit one block sort (NS <= 8192:
+// config 4's 7,056 per image), for the fused K5 only: the same stable radix sort on the bin
+// key (ascending sample index within a bin) over the whole segment at once, then each
+// thread writes the packed records of its sorted positions and the bin starts its key
+// boundaries open. One launch replaces chunk sort + scan table + emit (r04: 127 µs of
+// side-stream kernels per config-4 step, running beside the ∂W / ∂col products and taking
+// their CUs), no H / R / sorted scratch, and the records are the same bits in the same order.
+constexpr int kBsT = 1024, kBsIPT = 8, kBsMax = kBsT * kBsIPT;
+__global__ __launch_bounds__(kBsT) void bins_sort_seg(Geo g, const float* __restrict__ off, int b0,
+                                                      int NB, unsigned kbits,
+                                                      int* __restrict__ start,
+                                                      int4* __restrict__ brec) {
+  using Sort = rocprim::block_radix_sort<unsigned, kBsT, kBsIPT, unsigned short>;
+  __shared__ typename Sort::storage_type sst;
+  __shared__ unsigned lastk[kBsT];
+  const int tid = threadIdx.x, bg = blockIdx.x;
+  const int NS = g.HW * g.N, gi = bg % g.G, b = b0 + bg / g.G;
+  unsigned key[kBsIPT];
+  unsigned short val[kBsIPT];
+#pragma unroll
+  for (int u = 0; u < kBsIPT; ++u) {
+    const int s = tid * kBsIPT + u;  // blocked: input order = sample order
+    val[u] = (unsigned short)s;
+    key[u] = s < NS ? sample_bin(g, off, b, gi, s, NB, nullptr) : (unsigned)NB + 1;
+  }
+  Sort().sort(key, val, sst, 0, kbits);  // stable; thread t now holds ranks t*IPT + u
+  lastk[tid] = key[kBsIPT - 1];
+  __syncthreads();
+  int* st = start + (size_t)bg * (NB + 1);
+  int4* out = brec + (size_t)bg * NS;
+  unsigned prev = tid > 0 ? lastk[tid - 1] : ~0u;  // ~0u: before bin 0
+#pragma unroll
+  for (int u = 0; u < kBsIPT; ++u) {
+    const int pos = tid * kBsIPT + u;
+    const unsigned k = key[u];
+    // bins (prev, k] (clamped to the sentinel NB) start at this position
+    if (k != prev) {
+      const int lo = prev == ~0u ? 0 : (int)prev + 1, hi = min((int)k, NB);
+      for (int bn = lo; bn <= hi; ++bn) st[bn] = pos;
+    }
+    if (k < (unsigned)NB) {
+      const int s = val[u], m = s / g.N, tap = s - m * g.N;
+      const Tap t = sample_tap(g, off, b, gi, tap, m);
+      out[pos] = make_int4(m * g.K + tap * g.C, __float_as_int(t.fr), __float_as_int(t.fc),
+                           tap * g.HW + m);
+    }
+    prev = k;
+  }
+  // every key below the sentinel: the bins after the last one end at the segment's end
+  if (tid == kBsT - 1 && key[kBsIPT - 1] < (unsigned)NB)
+    for (int bn = (int)key[kBsIPT - 1] + 1; bn <= NB; ++bn) st[bn] = kBsMax;
 }
 
 // ---------------------------------------------------------------------------
@@ -1473,6 +1533,15 @@ hipError_t launch_bins(const Geo& g, const float* off, void* bins_ws, float* gof
   const size_t seg = (size_t)nb * g.G;
   const BinsWs P = bins_ptrs(g, bins_ws, nb);
   const bool fused = k5_fused(g);
+  if (fused && g.HW * g.N <= kBsMax && !g_bins_chunked) {
+    hipLaunchKernelGGL(bins_sort_seg, dim3((unsigned)seg), dim3(kBsT), 0, s, g, off, b0, NB, kbits,
+                       P.start, P.brec);
+    // samples in no bin (every corner outside the image) have ∂offset 0
+    hipError_t e = hipMemsetAsync(goff + (size_t)b0 * g.J * g.HW, 0,
+                                  (size_t)nb * g.J * g.HW * sizeof(float), s);
+    if (e != hipSuccess) return e;
+    return hipGetLastError();
+  }
   // H must start at 0 (only the bins present in a chunk are written); R needs no init
   hipError_t e = hipMemsetAsync(P.H, 0, seg * nch * bins_nbp(NB) * sizeof(int), s);
   if (e != hipSuccess) return e;

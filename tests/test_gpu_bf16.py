@@ -290,6 +290,27 @@ def test_bf16_dw_stream_vs_vendor_gemm(gpu_handle, monkeypatch, B, H, W, k):
         assert_bf16_close(a[2]["weight"], rg["weight"], "∂W vs oracle")
 
 
+@pytest.mark.parametrize("B,C,H,W,s", [(8, 256, 28, 28, (1, 1)), (3, 64, 20, 17, (1, 1)),
+                                       (2, 32, 30, 26, (2, 2))])
+def test_bf16_bins_one_block_sort_vs_chunked(gpu_handle, B, C, H, W, s):
+    """K5's sample bins from one block radix sort per image (bins_sort_seg: H·W·9 <= 8192)
+    against the chunked three-kernel sort (dcn_debug_bins_chunked): the same stable order and
+    the same records, so every output tensor is bit for bit the same (deform_conv.py:47-52
+    autodiff). Geometries: config 4's 28x28 (7,056 samples per image), ragged 20x17, and
+    stride 2 (a 15x13 output over a 30x26 input)."""
+    bits, _, st = _case(71, B=B, C=C, O_=64, H=H, W=W, s=s, off_scale=2.0)
+    a = _device(gpu_handle, bits, st)
+    rt.check(gpu_handle.lib.dcn_debug_bins_chunked(1))
+    try:
+        b = _device(gpu_handle, bits, st)
+    finally:
+        rt.check(gpu_handle.lib.dcn_debug_bins_chunked(0))
+    np.testing.assert_array_equal(a[0].view(np.uint32), b[0].view(np.uint32), err_msg="out")
+    for name in a[2]:
+        np.testing.assert_array_equal(a[2][name].view(np.uint32), b[2][name].view(np.uint32),
+                                      err_msg=name)
+
+
 @pytest.mark.parametrize("k,pad,C,H,W", [((1, 3), (0, 1), 24, 13, 11), ((3, 1), (1, 0), 24, 13, 11),
                                          ((2, 2), (1, 1), 24, 13, 11),
                                          ((1, 3), (0, 1), 64, 9, 8), ((2, 2), (1, 1), 128, 6, 12)])
