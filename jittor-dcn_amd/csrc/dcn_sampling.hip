@@ -752,15 +752,41 @@ __global__ __launch_bounds__(kBsT) void bins_sort_seg(Geo g, const float* __rest
   using Sort = rocprim::block_radix_sort<unsigned, kBsT, kBsIPT, unsigned short>;
   __shared__ typename Sort::storage_type sst;
   __shared__ unsigned lastk[kBsT];
+  // the segment's offsets ([2N][HW] fp32 <= 64 KiB, since HW·N <= kBsMax), staged with
+  // coalesced loads: every sample's (Δx, Δy) is then an LDS read (a sample's two planes are
+  // HW apart, so read from global they were 4-B gathers, one line per lane)
+  __shared__ __attribute__((aligned(16))) float offL[2 * kBsMax];
   const int tid = threadIdx.x, bg = blockIdx.x;
   const int NS = g.HW * g.N, gi = bg % g.G, b = b0 + bg / g.G;
+  {
+    const float* ob = off + ((size_t)b * g.J + (size_t)gi * 2 * g.N) * g.HW;
+    const int n = 2 * g.N * g.HW;
+    if ((g.HW & 3) == 0 && ((reinterpret_cast<uintptr_t>(ob) & 15) == 0)) {
+      for (int i = tid; i < n / 4; i += kBsT)
+        reinterpret_cast<float4*>(offL)[i] = reinterpret_cast<const float4*>(ob)[i];
+    } else {
+      for (int i = tid; i < n; i += kBsT) offL[i] = ob[i];
+    }
+  }
+  __syncthreads();
+  // the segment's sample taps from the staged offsets (sample_tap's arithmetic: same bits)
+  auto tap_of = [&](int n, int m) {
+    const int h = m / g.Wo, w = m - h * g.Wo;
+    float iy, ix;
+    ref_coord(h, w, offL[n * g.HW + m], offL[(g.N + n) * g.HW + m], g, iy, ix);
+    return make_tap(iy, ix, g);
+  };
   unsigned key[kBsIPT];
   unsigned short val[kBsIPT];
 #pragma unroll
   for (int u = 0; u < kBsIPT; ++u) {
     const int s = tid * kBsIPT + u;  // blocked: input order = sample order
     val[u] = (unsigned short)s;
-    key[u] = s < NS ? sample_bin(g, off, b, gi, s, NB, nullptr) : (unsigned)NB + 1;
+    key[u] = (unsigned)NB + 1;
+    if (s < NS) {  // sample_bin's key
+      const Tap t = tap_of(s % g.N, s / g.N);
+      key[u] = t.ok ? (unsigned)((t.r0 + 1) * (g.W + 1) + (t.c0 + 1)) : (unsigned)NB;
+    }
   }
   Sort().sort(key, val, sst, 0, kbits);  // stable; thread t now holds ranks t*IPT + u
   lastk[tid] = key[kBsIPT - 1];
@@ -779,7 +805,7 @@ __global__ __launch_bounds__(kBsT) void bins_sort_seg(Geo g, const float* __rest
     }
     if (k < (unsigned)NB) {
       const int s = val[u], m = s / g.N, tap = s - m * g.N;
-      const Tap t = sample_tap(g, off, b, gi, tap, m);
+      const Tap t = tap_of(tap, m);
       out[pos] = make_int4(m * g.K + tap * g.C, __float_as_int(t.fr), __float_as_int(t.fc),
                            tap * g.HW + m);
     }
