@@ -748,7 +748,8 @@ constexpr int kBsT = 1024, kBsIPT = 8, kBsMax = kBsT * kBsIPT;
 __global__ __launch_bounds__(kBsT) void bins_sort_seg(Geo g, const float* __restrict__ off, int b0,
                                                       int NB, unsigned kbits,
                                                       int* __restrict__ start,
-                                                      int4* __restrict__ brec) {
+                                                      int4* __restrict__ brec,
+                                                      float* __restrict__ goff) {
   using Sort = rocprim::block_radix_sort<unsigned, kBsT, kBsIPT, unsigned short>;
   __shared__ typename Sort::storage_type sst;
   __shared__ unsigned lastk[kBsT];
@@ -802,6 +803,12 @@ __global__ __launch_bounds__(kBsT) void bins_sort_seg(Geo g, const float* __rest
     if (k != prev) {
       const int lo = prev == ~0u ? 0 : (int)prev + 1, hi = min((int)k, NB);
       for (int bn = lo; bn <= hi; ++bn) st[bn] = pos;
+    }
+    if (k == (unsigned)NB) {  // in no bin (every corner outside): K5 never sees it, ∂offset 0
+      const int s = val[u], m = s / g.N, tap = s - m * g.N;
+      float* gob = goff + ((size_t)b * g.J + (size_t)gi * 2 * g.N) * g.HW;
+      gob[(size_t)tap * g.HW + m] = 0.f;
+      gob[(size_t)(g.N + tap) * g.HW + m] = 0.f;
     }
     if (k < (unsigned)NB) {
       const int s = val[u], m = s / g.N, tap = s - m * g.N;
@@ -1560,12 +1567,9 @@ hipError_t launch_bins(const Geo& g, const float* off, void* bins_ws, float* gof
   const BinsWs P = bins_ptrs(g, bins_ws, nb);
   const bool fused = k5_fused(g);
   if (fused && g.HW * g.N <= kBsMax && !g_bins_chunked) {
+    // (the samples in no bin get their zero ∂offset from the sort kernel: no memset)
     hipLaunchKernelGGL(bins_sort_seg, dim3((unsigned)seg), dim3(kBsT), 0, s, g, off, b0, NB, kbits,
-                       P.start, P.brec);
-    // samples in no bin (every corner outside the image) have ∂offset 0
-    hipError_t e = hipMemsetAsync(goff + (size_t)b0 * g.J * g.HW, 0,
-                                  (size_t)nb * g.J * g.HW * sizeof(float), s);
-    if (e != hipSuccess) return e;
+                       P.start, P.brec, goff);
     return hipGetLastError();
   }
   // H must start at 0 (only the bins present in a chunk are written); R needs no init
