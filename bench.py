@@ -393,7 +393,8 @@ def scope_rooflines(kernel_ms, cfg, B, Ho, Wo):
     return out
 
 
-def extra_config_leg(num, args, wl, rt, make_step, timed, kernel_times, sync, cpu=None):
+def extra_config_leg(num, args, wl, rt, make_step, timed, kernel_times, sync, cpu=None,
+                     graph_timed=None):
     """BASELINE config 2 (fp32 forward only, B=8, 64->128, 56x56: "1xMI355X fwd only vs
     CPU") or config 5 (the DCNv1 option set, B=64, 512->512, 14x14, s2 dil2 G4, fwd+bwd) on
     one GPU, timed like `value` (warmup, barrier-free synchronize brackets: N = 1); returns
@@ -408,6 +409,10 @@ def extra_config_leg(num, args, wl, rt, make_step, timed, kernel_times, sync, cp
     sync()
     el = timed(step, args.steps)
     km = kernel_times(step, args.steps)
+    # the same step replayed from a HIP graph: these configurations are small enough that the
+    # host's launch rate can set the eager step time (config 2: ≈0.09 ms of kernels), so the
+    # device-side rate is reported beside it (never as this object's `value`)
+    gms = graph_timed(step, args.steps) if graph_timed is not None else None
     Ho, Wo = rt.out_shape(wl.desc(B))
     N = wl.N
     roofs = scope_rooflines(km, cfg, B, Ho, Wo)
@@ -426,6 +431,7 @@ def extra_config_leg(num, args, wl, rt, make_step, timed, kernel_times, sync, cp
         "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 4),
         "samples_per_step": B * Ho * Wo * N,
+        "graph_ms_per_step": round(gms, 4) if gms else None,
         "kernel_ms": km,
         "roofline": roofs[0] if roofs else None,
         "rooflines_other": roofs[1:],
@@ -653,6 +659,32 @@ def main():
             el_ = float(t.item())
         return el_
 
+    def graph_timed(step, steps):
+        """ms per replay of `step` captured into a HIP graph (libdcn bound to the capture
+        stream for the capture), after two untimed replays; None if capture fails."""
+        try:
+            cs = torch.cuda.Stream(dev)
+            cs.wait_stream(stream)
+            gr = torch.cuda.CUDAGraph()
+            h.set_stream(cs.cuda_stream)
+            try:
+                with torch.cuda.graph(gr, stream=cs):
+                    step()
+            finally:
+                h.set_stream(stream.cuda_stream)
+            for _ in range(2):
+                gr.replay()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                gr.replay()
+            torch.cuda.synchronize(dev)
+            return (time.perf_counter() - t0) / steps * 1e3
+        except Exception:  # capture unsupported here: eager only
+            h.set_stream(stream.cuda_stream)
+            torch.cuda.synchronize(dev)
+            return None
+
     step, bufs = make_step(wl_main, B, 1000 + rank)
     for _ in range(args.warmup):
         step()
@@ -779,7 +811,7 @@ def main():
                 cpu = cpu_baseline_framework(CONFIGS[2], min(args.cpu_budget, 8.0),
                                              name="config2")
             extra[num] = extra_config_leg(num, args, wlx, rt, make_step, timed, kernel_times,
-                                          lambda: torch.cuda.synchronize(dev), cpu)
+                                          lambda: torch.cuda.synchronize(dev), cpu, graph_timed)
             del wlx
             torch.cuda.empty_cache()
     if rank == 0:

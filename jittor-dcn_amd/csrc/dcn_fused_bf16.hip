@@ -36,6 +36,11 @@ namespace {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
+// FUSED_LINES = 1: the stored columns leave as whole 128-B lines (store_cols); 0: r04's
+// per-unit half-line stores (A/B builds only)
+#ifndef FUSED_LINES
+#define FUSED_LINES 1
+#endif
 constexpr int kTH = 7, kTW = 16;  // output tile rows (h) × columns (w)
 constexpr int kPB = kTH * kTW / 16;  // 16-slot MFMA column blocks
 constexpr int kSlots = kPB * 16;
@@ -248,6 +253,18 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
           }
         }
         *reinterpret_cast<uint4*>(bt + buf * kSlots * kBPitch + slot * kBPitch + cg * 16) = o;
+#if !FUSED_LINES
+        // (A/B build) r04's column stores: each unit's 16 B as it is produced, so a 128-B line
+        // is written in two halves one step apart
+        if (STORE) {
+          const int h = h0 + slot / kTW, w = w0 + slot % kTW;
+          if (h < g.Ho && w < g.Wo)
+            __builtin_nontemporal_store(
+                as_v(o), reinterpret_cast<v4u*>(colT + (size_t)b * g.HW * g.K +
+                                                (unsigned)(h * g.Wo + w) * (unsigned)g.K +
+                                                (n * g.C + kCS * cs + 32 * hh + 8 * cg)));
+        }
+#endif
       }
     }
   };
@@ -334,7 +351,7 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
       produce(cs, s + 1, 1);
       mfma_step(0, aE);
       __syncthreads();
-      if (STORE) store_cols(cs, s >> 1);
+      if (STORE && FUSED_LINES) store_cols(cs, s >> 1);
       if (s + 2 < spq) {
         load_a(cs, s + 2, aE);
         produce(cs, s + 2, 0);

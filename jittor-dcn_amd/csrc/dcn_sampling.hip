@@ -894,8 +894,23 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
   // float4 slots: a zero row (window row -1: wave 0's ∂offset reads it only at image row
   // -1, so no select), the xT window; then the upper rows
   constexpr int ZR = WQ * 64, WIN = WR * WQ * 64, UPR = kTR * kTQ * 64;
-  __shared__ float4 lds_[ZR + WIN > UPR ? ZR + WIN : UPR];
-  float4* const lds = lds_ + ZR;  // the window; the upper rows use lds_ from slot 0
+  // the window holds xT's own element type (bf16: 8 B per lane and pixel, widened when a
+  // bin's corners are read): r05, half the LDS of the fp32 image, so 4 instead of 3
+  // workgroups of 8 waves fit a CU (the upper-row exchange after the loop, fp32, is the
+  // larger use then)
+  typedef typename std::conditional<sizeof(XT) == 2, uint2, float4>::type WinT;
+  constexpr int kWinB = (ZR + WIN) * (int)sizeof(WinT), kUprB = UPR * 16;
+  __shared__ __attribute__((aligned(16))) char lds_raw[kWinB > kUprB ? kWinB : kUprB];
+  WinT* const lwin = reinterpret_cast<WinT*>(lds_raw);
+  WinT* const lds = lwin + ZR;                                 // the window
+  float4* const lds_ = reinterpret_cast<float4*>(lds_raw);    // the upper rows
+  auto widen = [](const WinT& v) -> float4 {
+    if constexpr (sizeof(XT) == 2)
+      return make_float4(__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u),
+                         __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u));
+    else
+      return v;
+  };
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const Block3 blk = xcd_block();
@@ -910,15 +925,15 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
   // orders LDS only, so the stream's first rows are in flight across it (r01 staged the
   // window first: the stream began a full staging round trip later)
   constexpr int WIT = (WIN + kC2iThreads - 1) / kC2iThreads;
-  float4 wv[WIT];
+  WinT wv[WIT];
 #pragma unroll
   for (int k = 0; k < WIT; ++k) {
     const int idx = tid + k * kC2iThreads;
     const int pix = idx >> 6, l = idx & 63;
     const int r = R0 + pix / WQ, q = Q0 - 1 + pix % WQ, cc = l * 4;
     wv[k] = (idx < WIN && r < g.H && q >= 0 && q < g.W && cc < g.C)
-                ? ld4(xb + ((size_t)r * g.W + q) * g.C + cc)
-                : make_float4(0.f, 0.f, 0.f, 0.f);
+                ? *reinterpret_cast<const WinT*>(xb + ((size_t)r * g.W + q) * g.C + cc)
+                : WinT{};
   }
   const int NB = (g.H + 1) * (g.W + 1);
   const int* st = start + (size_t)bl * (NB + 1);
@@ -1014,7 +1029,7 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
   for (int k = 0; k < WIT; ++k)
     if (tid + k * kC2iThreads < WIN) lds[tid + k * kC2iThreads] = wv[k];
-  for (int k = tid; k < ZR; k += kC2iThreads) lds_[k] = z4;
+  for (int k = tid; k < ZR; k += kC2iThreads) lwin[k] = WinT{};
   lds_barrier();
   // the samples [rlo, rhi) of bin columns BJ0..BJ1-1, segment by segment (the first segment
   // already loaded and issued)
@@ -1031,12 +1046,12 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
         // W): outside the image. Read once per bin and segment, not per sample.
         float4 ka = z4, kb = z4, kc = z4, kd = z4;
         if (drow && lo < hi) {
-          const float4* w4 = lds + ((w - 1) * WQ + bj) * 64 + lane;
+          const WinT* w4 = lds + ((w - 1) * WQ + bj) * 64 + lane;
           const bool cB = bj + 1 <= kTQ;  // (bj is unrolled: a constant)
-          ka = w4[0];
-          kb = cB ? w4[64] : z4;
-          kc = w4[WQ * 64];
-          kd = cB ? w4[(WQ + 1) * 64] : z4;
+          ka = widen(w4[0]);
+          kb = cB ? widen(w4[64]) : z4;
+          kc = widen(w4[WQ * 64]);
+          kd = cB ? widen(w4[(WQ + 1) * 64]) : z4;
         }
         // batch i from (cR, cx); the next batch of this bin, else the next bin's first, into
         // (tR, tx)
@@ -1606,6 +1621,12 @@ static BinsWs bins_view(const Geo& g, void* bins_ws, int b0, int nb, int bins_nb
 // r01 A/B at config 3 (2-deep prefetch pipeline): U=2 0.92 ms col2im, U=4 0.93, U=8 1.50;
 // 4x6 tiles 1.05x slower, 4x8 tiles no longer unroll (2.7 ms). r02: column sweeps and
 // strips without the tile's bin-row re-read measured no faster (DESIGN.md §4 "K5").
+#ifndef K5B_WPE
+#define K5B_WPE 4
+#endif
+#ifndef K5B_U
+#define K5B_U 4
+#endif
 template <int U, int TQ, int WPE, int TR, typename GT, typename XT>
 static void launch_c2i(const Geo& g, const XT* xT, const BinsWs& P, const GT* gcolT, float* gxT,
                        float* goff, int b0, int nb, hipStream_t s) {
@@ -1641,7 +1662,12 @@ static void launch_k5_fused(const Geo& g, const XT* xT, const BinsWs& P, const G
   // (profiles/r04_k5_shapes.txt, one box): U = 3 0.514-0.520 / 0.116 ms; U = 4 0.515 / 0.111-0.113;
   // 5-wave workgroups at 5 waves/SIMD (20 waves per CU), bf16 U = 3: 0.134-0.136; both at U = 2:
   // 0.538-0.542 / 0.144-0.147. More rows per wave pays, more (smaller) workgroups do not.
-  launch_c2i<4, 4, 4, 7>(g, xT, P, gcolT, gxT, goff, b0, nb, s);
+  // r05: the bf16 window in LDS is bf16 (28 KB per workgroup instead of 46): the launch shape
+  // of the bf16 instance is K5B_U rows per batch at K5B_WPE waves per SIMD (A/B builds)
+  if constexpr (sizeof(XT) == 2)
+    launch_c2i<K5B_U, 4, K5B_WPE, 7>(g, xT, P, gcolT, gxT, goff, b0, nb, s);
+  else
+    launch_c2i<4, 4, 4, 7>(g, xT, P, gcolT, gxT, goff, b0, nb, s);
 }
 
 hipError_t launch_col2im_coord(const Geo& g, const float* x, const float* xT, const float* off,

@@ -218,7 +218,8 @@ def test_extra_config_legs_are_wired(bench, num):
     cpu = {"value": 0.005, "unit": "Gsamples/s"} if num == 2 else None
     args = argparse.Namespace(warmup=2, steps=5)
     res = bench.extra_config_leg(num, args, wl, rt, make_step, timed, lambda s, n: km,
-                                 lambda: None, cpu)
+                                 lambda: None, cpu, lambda s, n: 0.05)
+    assert res["graph_ms_per_step"] == 0.05
     assert calls["make_step"] == (True, cfg["B"]) and calls["timed"] == 5
     Ho, Wo = rt.out_shape(wl.desc(cfg["B"]))
     assert (Ho, Wo) == ((56, 56) if num == 2 else (6, 6))
