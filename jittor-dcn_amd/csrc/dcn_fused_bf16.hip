@@ -41,6 +41,18 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 #ifndef FUSED_LINES
 #define FUSED_LINES 1
 #endif
+// FUSED_NT = 0: the column stores with the default cache policy instead of non-temporal
+// (A/B: whether L2 merges the two half-line writes of FUSED_LINES = 0 before write-back)
+#ifndef FUSED_NT
+#define FUSED_NT 1
+#endif
+template <typename T>
+__device__ __forceinline__ void col_store(T v, T* p) {
+  if (FUSED_NT)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
 constexpr int kTH = 7, kTW = 16;  // output tile rows (h) × columns (w)
 constexpr int kPB = kTH * kTW / 16;  // 16-slot MFMA column blocks
 constexpr int kSlots = kPB * 16;
@@ -259,7 +271,7 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
         if (STORE) {
           const int h = h0 + slot / kTW, w = w0 + slot % kTW;
           if (h < g.Ho && w < g.Wo)
-            __builtin_nontemporal_store(
+            col_store(
                 as_v(o), reinterpret_cast<v4u*>(colT + (size_t)b * g.HW * g.K +
                                                 (unsigned)(h * g.Wo + w) * (unsigned)g.K +
                                                 (n * g.C + kCS * cs + 32 * hh + 8 * cg)));
@@ -283,7 +295,7 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
                                                       sl * kBPitch + (j & 3) * 16);
           const int h = h0 + sl / kTW, w = w0 + sl % kTW;
           if (sl < kSlots && h < g.Ho && w < g.Wo)
-            __builtin_nontemporal_store(
+            col_store(
                 v, reinterpret_cast<v4u*>(colT + (size_t)b * g.HW * g.K +
                                           (unsigned)(h * g.Wo + w) * (unsigned)g.K +
                                           (n * g.C + kCS * cs + 8 * j)));
