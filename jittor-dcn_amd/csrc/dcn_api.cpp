@@ -597,15 +597,22 @@ int forward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x,
   hipStream_t st = h->stream;
   bf16_t* xT = BF(L.xT);  // channels-last bf16 x: K1, K5 and the offset conv read it
   float *off32 = F32(L.off32), *out32 = F32(L.out32);
-  {
-    dcn::ConvBatch cb;  // the fp32 biases, one launch
-    cb.add(b_off, F32(L.boff32), (size_t)g.J, false);
-    if (has_bias) cb.add(b, F32(L.b32), (size_t)g.O, false);
-    HIP_TRY(dcn::launch_convert_multi(cb, st));
-  }
   // f3: the offset conv stages its windows from the NCHW x and writes xT itself (one pass
   // over x, no transpose launch) wherever its row kernel applies with stride 1
   const bool fold = dcn::offset_fwd_bf16_fold_ok(g) && !dcn::get_force_generic();
+  const bool off_mfma = fold || dcn::offset_fwd_mfma_bf16_ok(g);
+  const bool fused_ok = dcn::fused_fwd_bf16_ok(g) && !dcn::get_force_generic();
+  const bool fused = fused_ok && (h->fwd_path == DCN_FWD_FUSED || nocol ||
+                                  (h->fwd_path == DCN_FWD_AUTO && dcn::fused_fwd_bf16_pays(g)));
+  {
+    // one launch for the fp32 biases and the weight re-layouts of the MFMA kernels below
+    dcn::PrepBatch pb;
+    pb.f32(b_off, F32(L.boff32), (size_t)g.J);
+    if (has_bias) pb.f32(b, F32(L.b32), (size_t)g.O);
+    if (off_mfma) pb.add(dcn::prep_tjc(g, w_off, BF(L.wb16)));
+    if (fused) pb.add(dcn::prep_frag16(g, w, BF(L.wfr)));
+    HIP_TRY(dcn::launch_prep_bf16(pb, st));
+  }
   if (!fold) {
     ProfScope ps(h, DCN_K_XPOSE);
     HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(x, xT, g.B, g.C, g.HWi, st));
@@ -614,12 +621,12 @@ int forward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x,
     ProfScope ps(h, DCN_K_OFFSET_FWD);
     if (fold) {
       HIP_TRY(dcn::launch_offset_conv_fwd_bf16(g, xT, w_off, F32(L.boff32), off32, off,
-                                               BF(L.wb16), st, x));
-    } else if (dcn::offset_fwd_mfma_bf16_ok(g)) {
+                                               BF(L.wb16), st, x, true));
+    } else if (off_mfma) {
       // bf16 MFMA straight from the bf16 xT: the offsets, rounded to bf16 (off) and as
       // fp32 values (off32, what the sampling uses)
       HIP_TRY(dcn::launch_offset_conv_fwd_bf16(g, xT, w_off, F32(L.boff32), off32, off,
-                                               BF(L.wb16), st));
+                                               BF(L.wb16), st, nullptr, true));
     } else {  // fp32 VALU kernels on an fp32 copy of x
       float* x32 = F32(L.x32);
       HIP_TRY(dcn::launch_bf16_to_f32(x, x32, (size_t)g.B * g.C * g.HWi, st));
@@ -629,18 +636,16 @@ int forward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x,
       HIP_TRY(dcn::launch_round_to_bf16(off32, off, (size_t)g.B * g.J * g.HW, st));
     }
   }
-  const bool fused_ok = dcn::fused_fwd_bf16_ok(g) && !dcn::get_force_generic();
   // this workspace holds this forward's columns unless it runs without them
   ws_mark_columns(h, base, !nocol);
-  if (fused_ok && (h->fwd_path == DCN_FWD_FUSED || nocol ||
-                   (h->fwd_path == DCN_FWD_AUTO && dcn::fused_fwd_bf16_pays(g)))) {
+  if (fused) {
     // f2: the bilinear gather feeds the bf16 MFMAs straight from an LDS window of xT; bias
     // and the bf16 rounding in the epilogue; the columns are written only for a backward
     // that reuses them (not for DCN_FWD_FUSED_NOCOL)
     ProfScope ps(h, DCN_K_GEMM_FWD);
     HIP_TRY(dcn::launch_fused_fwd_bf16(g, xT, off32, w, BF(L.wfr),
                                        has_bias ? F32(L.b32) : nullptr, out,
-                                       nocol ? nullptr : BF(L.col), st));
+                                       nocol ? nullptr : BF(L.col), st, true));
     return DCN_OK;
   }
   {
@@ -675,11 +680,21 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
   bf16_t* col = BF(L.col);
   const size_t nx = (size_t)g.B * g.C * g.HWi, noff = (size_t)g.B * g.J * g.HW;
   const size_t nwo = (size_t)g.J * g.C * g.N;
+  const long npix = (long)g.B * g.HW;
+  const bool off_mfma = dcn::offset_bwd_bf16_ok(g);
+  const bool dcol_k = !h->dcol_gemm && dcn::dcol_bf16_ok(g.K, g.O, npix) &&
+                      !dcn::get_force_generic();
   {
-    dcn::ConvBatch cb;
-    cb.add(off, off32, noff, false);  // == the forward's rounded offsets
-    cb.add(w_off, F32(L.woff32), nwo, false);
-    HIP_TRY(dcn::launch_convert_multi(cb, st));
+    // one launch: the fp32 offsets (== the forward's rounded ones), and the weights in the
+    // layouts of the kernels below (fp32 w_off only for the non-MFMA offset-conv paths)
+    dcn::PrepBatch pb;
+    pb.f32(off, off32, noff);
+    if (off_mfma)
+      pb.add(dcn::prep_ck(g, w_off, BF(L.wb16)));
+    else
+      pb.f32(w_off, F32(L.woff32), nwo);
+    if (dcol_k) pb.add(dcn::prep_dcol(g.K, w, BF(L.wz)));
+    HIP_TRY(dcn::launch_prep_bf16(pb, st));
   }
   DCN_TRY(fork_aux(h));
   HIP_TRY(dcn::launch_bins(g, off32, base + L.bins, goff32, 0, g.B,
@@ -706,7 +721,6 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
   bf16_t* goutT = BF(L.goutT);
   // ∂W over the stored (or just recomputed) columns: the streaming MFMA kernel where it
   // applies (O = 256, K % 256 == 0: config 4), else the vendor GEMM (grouped where B allows)
-  const long npix = (long)g.B * g.HW;
   const bool dw_stream = !dw_fused && !h->dw_gemm && dw_stream_applies(g) &&
                          !dcn::get_force_generic();
   const int dwg = dw_fused || dw_stream ? 0 : dw_groups(g);
@@ -757,10 +771,9 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
   {
     ProfScope ps(h, DCN_K_GEMM_DCOL);  // ∂colT = ∂outT · Wf over the whole batch, bf16 out
     if (!have_goutT) HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(gout, goutT, g.B, g.O, g.HW, st));
-    if (!h->dcol_gemm && dcn::dcol_bf16_ok(g.K, g.O, npix) && !dcn::get_force_generic()) {
-      // short-K streaming kernel (csrc/dcn_dcol_bf16.hip) after its Wf swizzle (in line:
-      // on the side stream it ran beside the ∂W GEMM and cost that 10 µs, r04 dcol5)
-      HIP_TRY(dcn::launch_dcol_bf16_swizzle(w, g.K, g.O, BF(L.wz), st));
+    if (dcol_k) {
+      // short-K streaming kernel (csrc/dcn_dcol_bf16.hip) on the Wf swizzled by the prep
+      // launch (r04: the swizzle on the side stream beside ∂W cost that 10 µs, dcol5)
       HIP_TRY(dcn::launch_dcol_bf16(BF(L.wz), goutT, col, g.K, g.O, npix, st));
     } else {
       dcn::GemmSpec sp;
@@ -777,11 +790,12 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
                                     g.B, true, st));
   }
   ProfScope ps(h, DCN_K_OFFSET_BWD);
-  if (dcn::offset_bwd_bf16_ok(g)) {
+  if (off_mfma) {
     // bf16 MFMA: bf16 x and w_off, the fp32 ∂offset split into two bf16 planes; writes the
     // bf16 grad_x directly (transpose of the sampling route + the offset-conv route)
     HIP_TRY(dcn::launch_offset_conv_bwd_bf16(g, x, w_off, goff32, F32(L.gxT), BF(L.wb16),
-                                             F32(L.goffT), gx, F32(L.gwo32), F32(L.gbo32), st));
+                                             F32(L.goffT), gx, F32(L.gwo32), F32(L.gbo32), st,
+                                             nullptr, nullptr, nullptr, true));
     // (r02: the Wc swizzle and ∂b_off sums on the side stream beside ∂W_off measured slower,
     // offset bwd 0.115 -> 0.121 ms at config 4: concurrent kernels slow each other)
   } else if (dcn::offset_bwd_chunkable(g)) {
@@ -801,7 +815,7 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
   // the bf16 results, one launch (the offset-conv parameter grads after the exchange when
   // there is one)
   dcn::ConvBatch cb;
-  if (!dcn::offset_bwd_bf16_ok(g)) cb.add(gx32, gx, nx, true);
+  if (!off_mfma) cb.add(gx32, gx, nx, true);
   if (goff_out) cb.add(goff32, goff_out, noff, true);
   if (!exch) {
     cb.add(F32(L.gwo32), gw_off, nwo, true);

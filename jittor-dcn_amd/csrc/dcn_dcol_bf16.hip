@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "dcn_device.h"
+#include "dcn_swizzle.h"
 
 namespace dcn {
 namespace {
@@ -46,28 +47,6 @@ constexpr int kDcLds = kDcMT * kDcKS * 64 * 16;  // the A image: 128 KiB
 constexpr int kDcLA = 2;
 constexpr int kDcLdsAll = kDcLds + kDcWaves * 4096;  // + a 4-KiB output stage per wave
 static_assert(kDcLdsAll <= 160 * 1024, "one workgroup per CU");
-
-// accumulator row r = 8q + 4h + i of a 32x32 tile (lane half h, register 4q + i) takes the
-// A row of ∂col column 16h + 4q + i, so register j of a lane in half h is column 16h + j
-__host__ __device__ constexpr int dc_perm(int r) {
-  return 16 * ((r >> 2) & 1) + 4 * (r >> 3) + (r & 3);
-}
-
-// wz[T][ks][lane][j] = Wf[o = 16ks + 8(lane >> 5) + j][k = 32T + dc_perm(lane & 31)]: the
-// A fragments of 32-column tile T, 16 B per lane; a row group's 8 tiles are one 128 KiB run
-__global__ __launch_bounds__(256) void dcol_swizzle_w(const bf16_t* __restrict__ w, int K,
-                                                       bf16_t* __restrict__ wz) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (K / 32) * kDcKS * 64) return;
-  const int lane = i & 63, ks = (i >> 6) % kDcKS, T = (i >> 6) / kDcKS;
-  const int k = 32 * T + dc_perm(lane & 31), o0 = 16 * ks + 8 * (lane >> 5);
-  unsigned u[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    u[j] = (unsigned)w[(size_t)(o0 + 2 * j) * K + k] |
-           ((unsigned)w[(size_t)(o0 + 2 * j + 1) * K + k] << 16);
-  reinterpret_cast<uint4*>(wz)[i] = make_uint4(u[0], u[1], u[2], u[3]);
-}
 
 __device__ __forceinline__ unsigned pack_bf16(float a, float b) {
   return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
@@ -190,11 +169,10 @@ bool dcol_bf16_ok(int K, int O, long npix) {
   return O == kDcO && K > 0 && K % kDcRows == 0 && npix > 0 && (long)npix * K * 2 < (1l << 31);
 }
 
-hipError_t launch_dcol_bf16_swizzle(const bf16_t* w, int K, int O, bf16_t* wz, hipStream_t s) {
-  if (O != kDcO || K <= 0 || K % kDcRows != 0) return hipErrorInvalidValue;
-  const int nsw = (K / 32) * kDcKS * 64;
-  hipLaunchKernelGGL(dcol_swizzle_w, dim3((nsw + 255) / 256), dim3(256), 0, s, w, K, wz);
-  return hipGetLastError();
+// the A fragments of 32-column tile T (dc_perm, swz_dcol: dcn_swizzle.h), 16 B per lane, written
+// by the backward's prep launch; a row group's 8 tiles are one 128 KiB run
+PrepJob prep_dcol(int K, const bf16_t* w, bf16_t* wz) {
+  return PrepJob{PREP_DCOL, (long)(K / 32) * kDcKS * 64, w, wz, 0, K, 0, 0, 0, 0};
 }
 
 hipError_t launch_dcol_bf16(const bf16_t* wz, const bf16_t* goutT, bf16_t* col, int K, int O,

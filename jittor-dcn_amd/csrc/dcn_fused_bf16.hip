@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "dcn_device.h"
+#include "dcn_swizzle.h"
 
 namespace dcn {
 namespace {
@@ -138,12 +139,7 @@ __device__ __forceinline__ v4u blend8(float4 wv, v4u ua, v4u ub, v4u uc, v4u ud)
 __global__ __launch_bounds__(256) void wf_to_frag16(const bf16_t* __restrict__ w,
                                                     bf16_t* __restrict__ wfr, int O, int K) {
   const long f = (long)blockIdx.x * 256 + threadIdx.x;  // fragment = (ob, ks, lane)
-  if (f >= (long)O * K / 8) return;
-  const int l = (int)(f & 63);
-  const long rest = f >> 6;
-  const int NKS = K / 32, ob = (int)(rest / NKS), ks = (int)(rest - (long)ob * NKS);
-  *reinterpret_cast<uint4*>(wfr + f * 8) = *reinterpret_cast<const uint4*>(
-      w + (size_t)(16 * ob + (l & 15)) * K + 32 * ks + 8 * (l >> 4));
+  if (f < (long)O * K / 8) swz_frag16(w, wfr, K, f);
 }
 
 template <bool STORE>
@@ -724,13 +720,18 @@ bool fused_fwd_bf16_pays(const Geo& g) { return g.O == kOT && g.HW >= 28 * 28; }
 
 size_t fused_fwd_bf16_wfr_elems(const Geo& g) { return (size_t)g.O * g.K; }
 
+PrepJob prep_frag16(const Geo& g, const bf16_t* w, bf16_t* wfr) {
+  return PrepJob{PREP_FRAG16, (long)g.O * g.K / 8, w, wfr, 0, g.K, 0, 0, 0, 0};
+}
+
 hipError_t launch_fused_fwd_bf16(const Geo& g, const bf16_t* xT, const float* off,
                                  const bf16_t* w, bf16_t* wfr, const float* bias, bf16_t* out,
-                                 bf16_t* colT, hipStream_t s) {
+                                 bf16_t* colT, hipStream_t s, bool wfr_ready) {
   if (!fused_fwd_bf16_ok(g)) return hipErrorInvalidValue;
   const long nw = (long)g.O * g.K;
-  hipLaunchKernelGGL(wf_to_frag16, dim3((unsigned)((nw / 8 + 255) / 256)), dim3(256), 0, s, w,
-                     wfr, g.O, g.K);
+  if (!wfr_ready)
+    hipLaunchKernelGGL(wf_to_frag16, dim3((unsigned)((nw / 8 + 255) / 256)), dim3(256), 0, s, w,
+                       wfr, g.O, g.K);
   const int th_n = (g.Ho + kTH - 1) / kTH, tw_n = (g.Wo + kTW - 1) / kTW;
   const dim3 grid(th_n * tw_n, g.B, g.O / kOT);
   if (colT)

@@ -76,7 +76,7 @@ bool fused_fwd_bf16_pays(const Geo& g);  // DCN_FWD_AUTO picks it
 size_t fused_fwd_bf16_wfr_elems(const Geo& g);
 hipError_t launch_fused_fwd_bf16(const Geo& g, const bf16_t* xT, const float* off,
                                  const bf16_t* w, bf16_t* wfr, const float* bias, bf16_t* out,
-                                 bf16_t* colT, hipStream_t s);
+                                 bf16_t* colT, hipStream_t s, bool wfr_ready = false);
 // ∂Wf partials with the columns recomputed from xT (no column matrix): parts[grp][O][K] for
 // fused_dw_bf16_groups(g) image groups, summed afterwards in a fixed order.
 bool fused_dw_bf16_ok(const Geo& g);
@@ -105,7 +105,8 @@ size_t offset_fwd_bf16_wb_elems(const Geo& g);
 bool offset_fwd_bf16_fold_ok(const Geo& g);
 hipError_t launch_offset_conv_fwd_bf16(const Geo& g, const bf16_t* xT, const bf16_t* w_off,
                                        const float* b_off, float* off32, bf16_t* off, bf16_t* wb,
-                                       hipStream_t s, const bf16_t* x_nchw = nullptr);
+                                       hipStream_t s, const bf16_t* x_nchw = nullptr,
+                                       bool wb_ready = false);
 // DCN_BF16 offset-conv backward on bf16 MFMA (stride 1, C % 64 == 0, H·W % 8 == 0): gx is
 // the bf16 NCHW grad_x = transpose(gxT_in) + the offset-conv route. part: the goffT scratch;
 // wc: offset_bwd_bf16_wc_elems(g) bf16 values.
@@ -117,7 +118,8 @@ hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16
                                        const float* goff, const float* gxT_in, bf16_t* wc,
                                        float* part, bf16_t* gx, float* gw_off, float* gb_off,
                                        hipStream_t s, hipStream_t aux = nullptr,
-                                       hipEvent_t fork = nullptr, hipEvent_t join = nullptr);
+                                       hipEvent_t fork = nullptr, hipEvent_t join = nullptr,
+                                       bool wc_ready = false);
 // xT: channels-last x; goffT: scratch of offset_conv_goffT_floats(g). gxT_in == NULL:
 // grad_x is accumulated; else grad_x = transpose(gxT_in) + the offset-conv route, written
 // once (gxT_in: the sampling-route ∂x left channels-last by launch_col2im_*).
@@ -163,6 +165,42 @@ struct ConvBatch {
   }
 };
 hipError_t launch_convert_multi(const ConvBatch& cb, hipStream_t s);
+// One launch for a direction's small preparation work (dcn_reduce.hip, dcn_swizzle.h): bf16 ->
+// fp32 copies and the weight re-layouts of the bf16 kernels.
+enum PrepKind { PREP_F32 = 0, PREP_TJC = 1, PREP_CK = 2, PREP_FRAG16 = 3, PREP_DCOL = 4 };
+struct PrepJob {
+  int kind;
+  long units;  // PREP_F32: quads of elements; TJC / CK: elements; FRAG16 / DCOL: 16-B fragments
+  const void* in;
+  void* out;
+  long n;  // PREP_F32: elements
+  int a, b, c, d, e;
+};
+constexpr int kMaxPrep = 6;
+struct PrepBatch {
+  PrepJob job[kMaxPrep];
+  int n = 0;
+  bool overflow = false;
+  void add(const PrepJob& j) {
+    if (j.units <= 0) return;
+    if (n == kMaxPrep) {
+      overflow = true;
+      return;
+    }
+    job[n++] = j;
+  }
+  void f32(const bf16_t* in, float* out, size_t count) {
+    add(PrepJob{PREP_F32, (long)((count + 3) / 4), in, out, (long)count, 0, 0, 0, 0, 0});
+  }
+};
+hipError_t launch_prep_bf16(const PrepBatch& pb, hipStream_t s);
+// the batch jobs of the weight re-layouts: launch_offset_conv_fwd_bf16 (TJC: wb),
+// launch_offset_conv_bwd_bf16 (CK: wc) and launch_fused_fwd_bf16 (FRAG16: wfr) launch their own
+// unless told it is ready; launch_dcol_bf16 (DCOL: wz) always reads the prep's
+PrepJob prep_tjc(const Geo& g, const bf16_t* w_off, bf16_t* wb);
+PrepJob prep_ck(const Geo& g, const bf16_t* w_off, bf16_t* wc);
+PrepJob prep_frag16(const Geo& g, const bf16_t* w, bf16_t* wfr);
+PrepJob prep_dcol(int K, const bf16_t* w, bf16_t* wz);
 hipError_t launch_f32_to_bf16(const float* in, bf16_t* out, size_t n, hipStream_t s);
 hipError_t launch_round_to_bf16(float* v, bf16_t* out, size_t n, hipStream_t s);
 // out_bf[b][o][m] = bf16(out32[b][o][m] + bias[o]) (bias may be null)
@@ -216,7 +254,6 @@ int dw_stream_bf16_ranges(int K, long npix);
 hipError_t launch_dw_stream_bf16(const bf16_t* goutT, const bf16_t* col, float* parts, int K,
                                  int O, long npix, hipStream_t s);
 bool dcol_bf16_ok(int K, int O, long npix);
-hipError_t launch_dcol_bf16_swizzle(const bf16_t* w, int K, int O, bf16_t* wz, hipStream_t s);
 hipError_t launch_dcol_bf16(const bf16_t* wz, const bf16_t* goutT, bf16_t* col, int K, int O,
                             long npix, hipStream_t s);
 

@@ -14,6 +14,7 @@
 #include <algorithm>
 
 #include "dcn_device.h"
+#include "dcn_swizzle.h"
 
 namespace dcn {
 
@@ -1002,11 +1003,7 @@ __global__ __launch_bounds__(256) void woff_to_tjc_bf16(const bf16_t* __restrict
                                                        bf16_t* __restrict__ wb, int J, int C,
                                                        int Cp, int KK) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= KK * 32 * Cp) return;
-  const int e = i & 7, lane = (i >> 3) & 63, tks = i >> 9;
-  const int NKS = Cp / 16, t = tks / NKS, ks = tks - t * NKS;
-  const int j = lane & 31, c = 16 * ks + 8 * (lane >> 5) + e;
-  wb[i] = (j < J && c < C) ? w[((size_t)j * C + c) * KK + t] : (bf16_t)0;
+  if (i < KK * 32 * Cp) swz_tjc(w, wb, J, C, Cp, KK, i);
 }
 
 __device__ __forceinline__ bf16x8_t ld_bf16x8(const bf16_t* p) {
@@ -1276,15 +1273,21 @@ bool offset_fwd_bf16_fold_ok(const Geo& g) {
          g.ph >= 0 && g.ph < g.kh && g.pw >= 0 && g.pw < g.kw && g.C % 8 == 0;
 }
 
+PrepJob prep_tjc(const Geo& g, const bf16_t* w_off, bf16_t* wb) {
+  const int KK = g.kh * g.kw, Cp = (g.C + 63) / 64 * 64;
+  return PrepJob{PREP_TJC, (long)KK * 32 * Cp, w_off, wb, 0, g.J, g.C, Cp, KK, 0};
+}
+
 hipError_t launch_offset_conv_fwd_bf16(const Geo& g, const bf16_t* xT, const bf16_t* w_off,
                                        const float* b_off, float* off32, bf16_t* off, bf16_t* wb,
-                                       hipStream_t s, const bf16_t* x_nchw) {
+                                       hipStream_t s, const bf16_t* x_nchw, bool wb_ready) {
   if (!offset_fwd_mfma_bf16_ok(g)) return hipErrorInvalidValue;
   if (x_nchw && !offset_fwd_bf16_fold_ok(g)) return hipErrorInvalidValue;
   const int KK = g.kh * g.kw, Cp = (g.C + 63) / 64 * 64;
   const int n = KK * 32 * Cp;
-  hipLaunchKernelGGL(woff_to_tjc_bf16, dim3((n + 255) / 256), dim3(256), 0, s, w_off, wb, g.J,
-                     g.C, Cp, KK);
+  if (!wb_ready)
+    hipLaunchKernelGGL(woff_to_tjc_bf16, dim3((n + 255) / 256), dim3(256), 0, s, w_off, wb, g.J,
+                       g.C, Cp, KK);
   const int tiles = (g.HW + 31) / 32, spt = Cp / 64;  // 16-channel steps per tap and wave
   int SWc = 0;
   const size_t lds = fwd_bf16_row_lds(g, &SWc);
@@ -1349,12 +1352,7 @@ __global__ __launch_bounds__(256) void woff_to_ck_bf16(const bf16_t* __restrict_
                                                       bf16_t* __restrict__ wc, int J, int J8,
                                                       int C, int KK, int KT16) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= C * KT16) return;
-  const int e = i & 7, l = (i >> 3) & 63, mks = i >> 9;
-  const int NKS = KT16 / 16, mt = mks / NKS, ks = mks - mt * NKS;
-  const int c = 32 * mt + (l & 31), k = 16 * ks + 8 * (l >> 5) + e;
-  const int t = k / J8, j = k - t * J8;
-  wc[i] = (t < KK && j < J) ? w[((size_t)j * C + c) * KK + t] : (bf16_t)0;
+  if (i < C * KT16) swz_ck(w, wc, J, J8, C, KK, KT16, i);
 }
 
 __device__ __forceinline__ void stage_goff8(const Geo& g, const float* __restrict__ goff, int b,
@@ -1728,11 +1726,16 @@ size_t offset_bwd_bf16_wc_elems(const Geo& g) { return (size_t)g.C * kt16(g); }
 // DCN_BF16 offset-conv backward: x bf16 NCHW, w_off bf16, goff fp32; writes gw_off /
 // gb_off (fp32) and gx (bf16 NCHW) = transpose(gxT_in) + the offset-conv route.
 // part: the goffT scratch (offset_conv_goffT_floats); wc: offset_bwd_bf16_wc_elems.
+PrepJob prep_ck(const Geo& g, const bf16_t* w_off, bf16_t* wc) {
+  return PrepJob{PREP_CK, (long)g.C * kt16(g), w_off, wc, 0, g.J, j8(g.J), g.C, g.kh * g.kw,
+                 kt16(g)};
+}
+
 hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16_t* w_off,
                                        const float* goff, const float* gxT_in, bf16_t* wc,
                                        float* part, bf16_t* gx, float* gw_off, float* gb_off,
                                        hipStream_t s, hipStream_t aux, hipEvent_t fork,
-                                       hipEvent_t join) {
+                                       hipEvent_t join, bool wc_ready) {
   MfmaStage ms;
   if (!offset_bwd_bf16_ok(g) || !mfma_stage(g, &ms)) return hipErrorInvalidValue;
   const int KK = g.kh * g.kw, J8 = j8(g.J), KT16 = kt16(g);
@@ -1745,8 +1748,9 @@ hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16
     if (e != hipSuccess) return e;
   }
   const int n = g.C * KT16;
-  hipLaunchKernelGGL(woff_to_ck_bf16, dim3((n + 255) / 256), dim3(256), 0, s2, w_off, wc, g.J, J8,
-                     g.C, KK, KT16);
+  if (!wc_ready)
+    hipLaunchKernelGGL(woff_to_ck_bf16, dim3((n + 255) / 256), dim3(256), 0, s2, w_off, wc, g.J,
+                       J8, g.C, KK, KT16);
   // ∂b_off: one block per channel (r02, config 4: the two-level (channel, image) sum that the
   // fp32 path runs on its side stream measured 0.122 against 0.112 ms for this scope here)
   if (gb_off) launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s2);

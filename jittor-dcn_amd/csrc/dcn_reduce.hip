@@ -1,6 +1,7 @@
 // dcn_reduce.hip — bias add (deform_conv.py:79-80) and the deterministic channel
 // / partial reductions of the backward (∂b, ∂b_off, Σ_b ∂W partials).
 #include "dcn_device.h"
+#include "dcn_swizzle.h"
 
 namespace dcn {
 
@@ -297,6 +298,55 @@ hipError_t launch_convert_multi(const ConvBatch& cb, hipStream_t s) {
   for (int k = 0; k < cb.n; ++k) quads += (cb.seg[k].n + 3) / 4;
   if (quads == 0) return hipGetLastError();
   hipLaunchKernelGGL(convert_multi_kernel, dim3(grid_for(quads * 4, 4)), dim3(256), 0, s, cb);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void prep_bf16_kernel(PrepBatch pb) {
+  long q0[kMaxPrep + 1];
+  q0[0] = 0;
+#pragma unroll
+  for (int k = 0; k < kMaxPrep; ++k) q0[k + 1] = q0[k] + (k < pb.n ? pb.job[k].units : 0);
+  for (long q = (long)blockIdx.x * 256 + threadIdx.x; q < q0[kMaxPrep];
+       q += (long)gridDim.x * 256) {
+    int k = 0;
+#pragma unroll
+    for (int t = 1; t < kMaxPrep; ++t) k += q >= q0[t] ? 1 : 0;
+    const PrepJob& jb = pb.job[k];
+    const long u = q - q0[k];
+    const bf16_t* in = static_cast<const bf16_t*>(jb.in);
+    switch (jb.kind) {
+      case PREP_F32: {
+        float* out = static_cast<float*>(jb.out);
+        const long i = u * 4;
+        if (i + 4 <= jb.n && (((uintptr_t)(in + i) & 7) | ((uintptr_t)(out + i) & 15)) == 0)
+          *reinterpret_cast<float4*>(out + i) = ld4(in + i);
+        else
+          for (long e = i; e < jb.n && e < i + 4; ++e) out[e] = bf2f(in[e]);
+        break;
+      }
+      case PREP_TJC:
+        swz_tjc(in, static_cast<bf16_t*>(jb.out), jb.a, jb.b, jb.c, jb.d, (int)u);
+        break;
+      case PREP_CK:
+        swz_ck(in, static_cast<bf16_t*>(jb.out), jb.a, jb.b, jb.c, jb.d, jb.e, (int)u);
+        break;
+      case PREP_FRAG16:
+        swz_frag16(in, static_cast<bf16_t*>(jb.out), jb.a, u);
+        break;
+      default:  // PREP_DCOL
+        swz_dcol(in, jb.a, static_cast<bf16_t*>(jb.out), (int)u);
+        break;
+    }
+  }
+}
+
+hipError_t launch_prep_bf16(const PrepBatch& pb, hipStream_t s) {
+  if (pb.overflow) return hipErrorInvalidValue;
+  long units = 0;
+  for (int k = 0; k < pb.n; ++k) units += pb.job[k].units;
+  if (!units) return hipSuccess;
+  hipLaunchKernelGGL(prep_bf16_kernel, dim3((unsigned)std::min((units + 255) / 256, 4096l)),
+                     dim3(256), 0, s, pb);
   return hipGetLastError();
 }
 
