@@ -714,17 +714,26 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
     }
   }
   const bool exch = h->comm != nullptr;  // sum the fp32 copies over ranks, then round
+  bf16_t* goutT = BF(L.goutT);
+  bool have_goutT = false;  // ∂outT (shared by the ∂W kernels and the ∂col product)
   if (has_bias) {
     ProfScope ps(h, DCN_K_BWD_BIAS);  // Σ over images and pixels of the bf16 ∂out, in fp32
-    dcn::launch_channel_sum_bf16(gout, g.B, g.O, g.HW, F32(L.gb32), st, exch ? nullptr : gb);
+    // with ∂outT from the same pass where the 16-byte transpose applies (tile partials in
+    // gxT, which only K5 writes, after this)
+    if (dcn::xpose_chsum_bf16_floats(g.B, g.O, g.HW) <= (size_t)g.B * g.HWi * g.C &&
+        dcn::launch_xpose_chsum_bf16(gout, goutT, F32(L.gxT), F32(L.gb32), exch ? nullptr : gb,
+                                     g.B, g.O, g.HW, st)) {
+      HIP_TRY(hipGetLastError());
+      have_goutT = true;
+    } else {
+      dcn::launch_channel_sum_bf16(gout, g.B, g.O, g.HW, F32(L.gb32), st, exch ? nullptr : gb);
+    }
   }
-  bf16_t* goutT = BF(L.goutT);
   // ∂W over the stored (or just recomputed) columns: the streaming MFMA kernel where it
   // applies (O = 256, K % 256 == 0: config 4), else the vendor GEMM (grouped where B allows)
   const bool dw_stream = !dw_fused && !h->dw_gemm && dw_stream_applies(g) &&
                          !dcn::get_force_generic();
   const int dwg = dw_fused || dw_stream ? 0 : dw_groups(g);
-  bool have_goutT = false;  // ∂outT (shared by the ∂W kernels and the ∂col product)
   {
     ProfScope ps(h, DCN_K_GEMM_DW);
     dcn::GemmSpec sp;
@@ -740,12 +749,12 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
     if (dw_fused) {
       HIP_TRY(dcn::launch_fused_dw_bf16(g, xT, off32, gout, F32(L.parts), st));
     } else if (dw_stream) {
-      HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(gout, goutT, g.B, g.O, g.HW, st));
+      if (!have_goutT) HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(gout, goutT, g.B, g.O, g.HW, st));
       have_goutT = true;
       HIP_TRY(dcn::launch_dw_stream_bf16(goutT, col, F32(L.parts), g.K, g.O, npix, st));
     } else if (dwg > 0) {
       // grouped NT over the pixels of B/dwg images (∂outT first, shared with ∂col)
-      HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(gout, goutT, g.B, g.O, g.HW, st));
+      if (!have_goutT) HIP_TRY(dcn::launch_nchw_to_nhwc_bf16(gout, goutT, g.B, g.O, g.HW, st));
       have_goutT = true;
       const int pg = (g.B / dwg) * g.HW;
       sp.tb = true;

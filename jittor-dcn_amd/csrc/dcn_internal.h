@@ -215,6 +215,13 @@ void launch_channel_sum_bf16(const bf16_t* in, int B, int Cn, int HW, float* out
 // scratch of xpose_chsum_floats(B, C, P) floats.
 size_t xpose_chsum_floats(int B, int C, int P);
 bool launch_xpose_f4(const float* in, float* out, int B, int C, int P, hipStream_t s);
+// bf16 NCHW -> NHWC in 16-byte accesses (false when it does not apply: P % 8, C % 64, 16-B
+// alignment), and the same pass with the channel sums (fp32 chsum, bf16 chsum_bf if not
+// null; tile partials in tsum, xpose_chsum_bf16_floats(B, C, P) floats)
+bool launch_xpose_b8(const bf16_t* in, bf16_t* out, int B, int C, int P, hipStream_t s);
+size_t xpose_chsum_bf16_floats(int B, int C, int P);
+bool launch_xpose_chsum_bf16(const bf16_t* in, bf16_t* out, float* tsum, float* chsum,
+                             bf16_t* chsum_bf, int B, int C, int P, hipStream_t s);
 // ∂out -> ∂outT with ∂b; the per-channel fold of the tile sums runs on s_sum (after event ev)
 // when given, so tsum must then stay untouched until s_sum is joined.
 hipError_t launch_xpose_chsum(const float* in, float* out, float* tsum, float* chsum, int B,

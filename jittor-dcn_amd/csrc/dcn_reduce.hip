@@ -491,17 +491,123 @@ static bool xpose_f4_ok(const float* in, const float* out, int C, int P) {
   return P % 4 == 0 && C % 64 == 0 && ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0;
 }
 
+// bf16 form (DCN_BF16's ∂out -> ∂outT, x -> xT): 16-byte accesses both ways (P % 8 == 0,
+// C % 64 == 0, 16-B aligned). A block walks kXbSub 64-pixel tiles of one (image, 64-channel)
+// slab, the next tile's loads in flight while the current one is written. Thread (lr, lq)
+// loads 8 pixels of channel rows lr and lr + 32 and, from the LDS tile (rows padded to 66
+// elements: the column reads hit 32 distinct banks), stores 8 channels of pixel rows lr and
+// lr + 32. With SUMS the channel sums ride along: a thread's 8-pixel sums in a fixed tree,
+// folded over the 8 lanes of its channel row by a fixed xor tree, one partial per (block,
+// channel) in tsum[c][image·gridDim.x + blockIdx.x] (r05: ∂b and the transpose were two passes
+// over ∂out, 9.2 + 13.7 us at config 4).
+constexpr int kXbSub = 4;
+static int xpose_b8_blocks_x(int P) { return (P + 64 * kXbSub - 1) / (64 * kXbSub); }
+
+__device__ __forceinline__ float sum2_bf16(unsigned u) {
+  return __uint_as_float(u << 16) + __uint_as_float(u & 0xffff0000u);
+}
+__device__ __forceinline__ float sum8_bf16(uint4 v) {
+  return (sum2_bf16(v.x) + sum2_bf16(v.y)) + (sum2_bf16(v.z) + sum2_bf16(v.w));
+}
+
+template <bool SUMS>
+__global__ __launch_bounds__(256) void xpose_b8(const bf16_t* __restrict__ in,
+                                                bf16_t* __restrict__ out,
+                                                float* __restrict__ tsum, int C, int P) {
+  __shared__ unsigned short t[64][66];  // [c][p]
+  const int c0 = blockIdx.y * 64, b = blockIdx.z;
+  const bf16_t* ib = in + (size_t)b * C * P;
+  bf16_t* ob = out + (size_t)b * C * P;
+  const int tid = threadIdx.x, lr = tid >> 3, lq = tid & 7;
+  const int pb = blockIdx.x * 64 * kXbSub;
+  const int nsub = min(kXbSub, (P - pb + 63) / 64);
+  uint4 r[2];
+  auto load = [&](int p0) {
+    const int p = p0 + 8 * lq;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      r[k] = p < P ? *reinterpret_cast<const uint4*>(ib + (size_t)(c0 + lr + 32 * k) * P + p)
+                   : make_uint4(0u, 0u, 0u, 0u);
+  };
+  float cs[2] = {0.f, 0.f};
+  load(pb);
+  for (int sub = 0; sub < nsub; ++sub) {
+    const int p0 = pb + 64 * sub;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      unsigned* row = reinterpret_cast<unsigned*>(&t[lr + 32 * k][8 * lq]);
+      row[0] = r[k].x, row[1] = r[k].y, row[2] = r[k].z, row[3] = r[k].w;
+      if (SUMS) cs[k] += sum8_bf16(r[k]);  // zeros past P
+    }
+    __syncthreads();
+    if (sub + 1 < nsub) load(p0 + 64);  // in flight while this tile is written
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int pr = lr + 32 * k, p = p0 + pr;
+      unsigned u[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        u[i] = (unsigned)t[8 * lq + 2 * i][pr] | ((unsigned)t[8 * lq + 2 * i + 1][pr] << 16);
+      if (p < P)
+        *reinterpret_cast<uint4*>(ob + (size_t)p * C + c0 + 8 * lq) =
+            make_uint4(u[0], u[1], u[2], u[3]);
+    }
+    __syncthreads();
+  }
+  if (SUMS) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      float v = cs[k];  // the 8 lanes of channel row lr + 32k are consecutive
+      v += __shfl_xor(v, 1);
+      v += __shfl_xor(v, 2);
+      v += __shfl_xor(v, 4);
+      if (lq == 0)
+        tsum[(size_t)(c0 + lr + 32 * k) * gridDim.x * gridDim.z + (size_t)b * gridDim.x +
+             blockIdx.x] = v;
+    }
+  }
+}
+
+static bool xpose_b8_ok(const bf16_t* in, const bf16_t* out, int C, int P) {
+  return P % 8 == 0 && C % 64 == 0 && ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0;
+}
+
 // One wave per channel: lane l sums partials i ≡ l (mod 64) (all loads in flight
 // together), then a fixed DPP tree (wave_sum) folds the 64 lane sums: deterministic.
 __global__ __launch_bounds__(64) void tile_sum_to_channels(const float* __restrict__ tsum,
                                                            int ntiles, int C,
-                                                           float* __restrict__ out) {
+                                                           float* __restrict__ out,
+                                                           bf16_t* __restrict__ out_bf = nullptr) {
   const int c = blockIdx.x, lane = threadIdx.x;
   float s = 0.f;
 #pragma unroll 8
   for (int i = lane; i < ntiles; i += 64) s += tsum[(size_t)c * ntiles + i];  // coalesced
   s = wave_sum(s);
-  if (lane == 0) out[c] = s;
+  if (lane == 0) {
+    out[c] = s;
+    if (out_bf) out_bf[c] = f2bf(s);
+  }
+}
+
+bool launch_xpose_b8(const bf16_t* in, bf16_t* out, int B, int C, int P, hipStream_t s) {
+  if (!xpose_b8_ok(in, out, C, P)) return false;
+  dim3 grid(xpose_b8_blocks_x(P), C / 64, B);
+  hipLaunchKernelGGL(xpose_b8<false>, grid, dim3(256), 0, s, in, out, nullptr, C, P);
+  return true;
+}
+
+size_t xpose_chsum_bf16_floats(int B, int C, int P) {
+  return (size_t)B * xpose_b8_blocks_x(P) * C;
+}
+
+bool launch_xpose_chsum_bf16(const bf16_t* in, bf16_t* out, float* tsum, float* chsum,
+                             bf16_t* chsum_bf, int B, int C, int P, hipStream_t s) {
+  if (!xpose_b8_ok(in, out, C, P)) return false;
+  dim3 grid(xpose_b8_blocks_x(P), C / 64, B);
+  hipLaunchKernelGGL(xpose_b8<true>, grid, dim3(256), 0, s, in, out, tsum, C, P);
+  hipLaunchKernelGGL(tile_sum_to_channels, dim3(C), dim3(64), 0, s, tsum, B * (int)grid.x, C,
+                     chsum, chsum_bf);
+  return true;
 }
 
 // the plain fp32 NCHW -> NHWC transpose in the 16-byte form; false when it does not apply
@@ -529,7 +635,7 @@ hipError_t launch_xpose_chsum(const float* in, float* out, float* tsum, float* c
     s = s_sum;
   }
   hipLaunchKernelGGL(tile_sum_to_channels, dim3(C), dim3(64), 0, s, tsum, B * xpose_blocks_x(P), C,
-                     chsum);
+                     chsum, nullptr);
   return hipGetLastError();
 }
 

@@ -1379,6 +1379,7 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc_bf16x4(const bf16_t* __restr
 
 hipError_t launch_nchw_to_nhwc_bf16(const bf16_t* in, bf16_t* out, int B, int C, int P,
                                     hipStream_t s) {
+  if (launch_xpose_b8(in, out, B, C, P, s)) return hipGetLastError();
   dim3 grid((P + 63) / 64, (C + 63) / 64, B);
   // 8-byte global accesses need 4-element alignment of every row start
   if (P % 4 == 0 && C % 4 == 0 && ((uintptr_t)in & 7) == 0 && ((uintptr_t)out & 7) == 0)
