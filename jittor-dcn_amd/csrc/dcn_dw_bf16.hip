@@ -64,6 +64,11 @@ typedef __attribute__((address_space(3))) void lvoid;
 #ifndef DW_PIN
 #define DW_PIN 0
 #endif
+// DW_ABL (diagnostic A/B builds only, wrong results): 1 LDS reads without MFMAs, 2 the DMA
+// stream alone, 3 the column tiles read as contiguous [tile][pixel][256] blocks
+#ifndef DW_ABL
+#define DW_ABL 0
+#endif
 constexpr int kDwO = 256;                          // output channels: the tile's rows
 constexpr int kDwN = 256;                          // ∂W columns per tile
 constexpr int kDwPx = DW_PX;                       // pixels per stage
@@ -74,7 +79,13 @@ constexpr int kDwOpB = kDwPx * kDwRowB;            // 16 KiB per operand per 32-
 constexpr int kDwStageB = 2 * kDwOpB;              // A (∂outT) then B (columns)
 constexpr int kDwLds = kDwRing * kDwStageB;        // 128 KiB (4 × 32 px)
 constexpr int kDwWaves = 8;
-constexpr int kDwGlds = kDwStageB / (kDwWaves * 1024);  // DMA instructions per wave per stage
+// DW_LOADERS: the waves that issue the stage DMAs (waves 0 .. DW_LOADERS - 1; all 8 by default)
+#ifndef DW_LOADERS
+#define DW_LOADERS 8
+#endif
+constexpr int kDwLoaders = DW_LOADERS;
+static_assert(kDwLoaders == 2 || kDwLoaders == 4 || kDwLoaders == 8, "loader waves");
+constexpr int kDwGlds = kDwStageB / (kDwLoaders * 1024);  // DMA instructions per loader per stage
 constexpr int kDwOpI = kDwPx / 2;                  // DMA instructions per operand (2 rows each)
 static_assert(kDwPx == 16 || kDwPx == 32, "stage = one or two 16-pixel k-steps");
 static_assert(kDwRing >= 3 && kDwRing <= 8, "ring depth");
@@ -151,14 +162,21 @@ __global__ __launch_bounds__(kDwWaves * 64, 1) void dw_stream_bf16(
   // uniform); lane L writes physical chunk L & 31 of row 2i + (L >> 5), i.e. fetches logical
   // chunk (L & 31) ^ 4·(row & 3). Byte offsets are 32-bit (dw_stream_bf16_ok).
   const int lrow = lane >> 5, lpc = lane & 31;
+#if DW_ABL == 3  // (diagnostic build: each column tile read as if stored [tile][pixel][256])
+  const char* opbase[2] = {reinterpret_cast<const char*>(goutT),
+                           reinterpret_cast<const char*>(col) + (size_t)tile * npix * kDwRowB};
+  const unsigned opstride[2] = {(unsigned)kDwRowB, (unsigned)kDwRowB};
+#else
   const char* opbase[2] = {reinterpret_cast<const char*>(goutT),
                            reinterpret_cast<const char*>(col) + (size_t)tile * kDwN * 2};
   const unsigned opstride[2] = {(unsigned)kDwRowB, (unsigned)K * 2u};
+#endif
   auto issue = [&](int j, char* slot) {
+    if (w >= kDwLoaders) return;  // wave-uniform
     j = min(j, nst - 1);  // past the range: re-read its last stage (L2), never read back
 #pragma unroll
     for (int u = 0; u < kDwGlds; ++u) {
-      const int ii = u * kDwWaves + w, op = ii / kDwOpI, i = ii % kDwOpI;
+      const int ii = u * kDwLoaders + w, op = ii / kDwOpI, i = ii % kDwOpI;
       const int row = 2 * i + lrow;
       const unsigned ch = (unsigned)(lpc ^ (4 * (row & 3)));
       const int p = min(px0 + j * kDwPx + row, npix - 1);  // past the end: re-read the last row
@@ -207,6 +225,9 @@ __global__ __launch_bounds__(kDwWaves * 64, 1) void dw_stream_bf16(
   // launch: the ∂outT rows past the end (DMA'd from the last row) are zeroed in the A
   // fragments, so their products vanish
   auto compute = [&](const char* slot, int nvalid) {
+#if DW_ABL == 2
+    return;  // (diagnostic build: the DMA stream alone)
+#endif
 #pragma unroll
     for (int ks = 0; ks < kDwPx / 16; ++ks) {
       const char* base = slot + ks * 16 * kDwRowB;
@@ -224,11 +245,15 @@ __global__ __launch_bounds__(kDwWaves * 64, 1) void dw_stream_bf16(
           for (int e = 0; e < 8; ++e)
             if (r0 + (e & 3) + 4 * (e >> 2) >= nvalid) a[mi][e] = (__bf16)0.f;
       }
+#if DW_ABL == 1  // (diagnostic build: LDS reads, no MFMAs)
+      asm volatile("" ::"v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(b[0]), "v"(b[1]));
+#else
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni)
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+#endif
     }
   };
 
