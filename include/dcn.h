@@ -388,6 +388,10 @@ int dcn_debug_fused_workgroups(int n);
 /* 1 = build K5's sample bins with the chunked three-kernel sort even where one block sort
  * per image applies (H·W·kh·kw <= 8192); the parity tests compare the two bit for bit. */
 int dcn_debug_bins_chunked(int on);
+/* 0 = run the fp32 offset conv (forward and backward) on its VALU kernels where it would run
+ * as GEMMs over its own im2col (geometries without an MFMA offset-conv kernel, e.g. BASELINE
+ * config 5); the parity tests compare the two. Default 1. */
+int dcn_debug_offset_gemm(int on);
 /* The ∂W partial planes ([O][K] fp32 each) that each backward path of this geometry writes
  * into the workspace before its fixed-order sum — planes[0] one per image, planes[1] the
  * grouped bf16 GEMM, planes[2] the recomputed-column bf16 kernel, planes[3] the bf16

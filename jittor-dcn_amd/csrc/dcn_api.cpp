@@ -1106,6 +1106,59 @@ int dcn_col2im_coord_bwd(dcn_handle* h, const dcn_desc* d, const float* x, const
   return DCN_OK;
 }
 
+namespace {
+// r05: the fp32 offset conv as GEMMs (dcn::offset_conv_gemm_ok geometries that have no MFMA
+// offset-conv kernel; dcn_debug_offset_gemm(0) keeps the VALU kernels, for the parity tests)
+int g_ocg = 1;
+bool ocg_on(const Geo& g) {
+  return g_ocg && !dcn::offset_fwd_mfma_xt_ok(g) && !dcn::offset_bwd_chunkable(g) &&
+         dcn::offset_conv_gemm_ok(g) && !dcn::get_force_generic();
+}
+// off[B][J][HW] from xT; wp: J·K floats, ocol: B·HW·K floats, offT: B·HW·J floats
+int offset_conv_fwd_gemm(dcn_handle* h, const Geo& g, const float* xT, const float* w_off,
+                         const float* b_off, float* off, float* wp, float* ocol, float* offT) {
+  const int K = g.C * g.kh * g.kw, P = g.B * g.HW;
+  HIP_TRY(dcn::launch_ocg_wprime(g, w_off, wp, h->stream));
+  HIP_TRY(dcn::launch_ocg_im2col(g, xT, ocol, h->stream));
+  // column-major offT(J × P) = W'ᵀ(J × K) · ocol(K × P)   (W' = [J][K], ocol = [P][K])
+  dcn::GemmSpec sp;
+  sp.ta = true;
+  sp.m = g.J; sp.n = P; sp.k = K;
+  sp.lda = K; sp.ldb = K; sp.ldc = g.J;
+  GEMM_TRY(h, sp, wp, ocol, offT);
+  HIP_TRY(dcn::launch_ocg_offt_to_off(g, offT, b_off, off, h->stream));
+  return DCN_OK;
+}
+// ∂w_off and ∂x (= transpose(gxT_in) + the offset route) from ∂off; wp: J·K floats,
+// ocol: B·HW·K floats (ocol, then ∂ocol), goffT: B·HW·J floats, gwp: J·K floats
+int offset_conv_bwd_gemm(dcn_handle* h, const Geo& g, const float* xT, const float* w_off,
+                         const float* goff, float* wp, float* ocol, float* goffT, float* gwp,
+                         const float* gxT_in, float* gx, float* gw_off) {
+  const int K = g.C * g.kh * g.kw, P = g.B * g.HW;
+  HIP_TRY(dcn::launch_ocg_wprime(g, w_off, wp, h->stream));
+  HIP_TRY(dcn::launch_ocg_im2col(g, xT, ocol, h->stream));
+  HIP_TRY(dcn::launch_ocg_goff_to_pj(g, goff, goffT, h->stream));
+  {
+    // column-major ∂W'(K × J) = ocol(K × P) · ∂offT(P × J)   (∂offT = [P][J])
+    dcn::GemmSpec sp;
+    sp.tb = true;
+    sp.m = K; sp.n = g.J; sp.k = P;
+    sp.lda = K; sp.ldb = g.J; sp.ldc = K;
+    GEMM_TRY(h, sp, ocol, goffT, gwp);
+  }
+  HIP_TRY(dcn::launch_ocg_wgrad_out(g, gwp, gw_off, h->stream));
+  {
+    // column-major ∂ocol(K × P) = W'(K × J) · ∂offTᵀ(J × P), over the columns just read
+    dcn::GemmSpec sp;
+    sp.m = K; sp.n = P; sp.k = g.J;
+    sp.lda = K; sp.ldb = g.J; sp.ldc = K;
+    GEMM_TRY(h, sp, wp, goffT, ocol);
+  }
+  HIP_TRY(dcn::launch_ocg_col2im(g, ocol, gxT_in, gx, h->stream));
+  return DCN_OK;
+}
+}  // namespace
+
 int dcn_forward(dcn_handle* h, const dcn_desc* d, const float* x, const float* w_off,
                 const float* b_off, const float* w, const float* b, float* out, float* off,
                 void* ws, size_t ws_bytes) {
@@ -1139,6 +1192,23 @@ int dcn_forward_ex(dcn_handle* h, const dcn_desc* d, const float* x, const float
       ProfScope ps(h, DCN_K_OFFSET_FWD);
       HIP_TRY(dcn::launch_offset_conv_fwd_xt(g, x, w_off, b_off, off, xT,
                                              reinterpret_cast<float*>(base + L.wt), h->stream));
+    }
+    return core_forward(h, g, x, off, w, b, d->has_bias != 0, out, xT,
+                        reinterpret_cast<float*>(base + L.col), true);
+  }
+  if (ocg_on(g)) {
+    // r05: the offset conv as one GEMM over its own im2col (config 5: C = 512, J = 72,
+    // stride 2, dilation 2, where the VALU kernel ran at 0.06 of the f32 MFMA peak)
+    {
+      ProfScope ps(h, DCN_K_XPOSE);
+      HIP_TRY(dcn::launch_nchw_to_nhwc(x, xT, g.B, g.C, g.HWi, h->stream));
+    }
+    {
+      ProfScope ps(h, DCN_K_OFFSET_FWD);
+      DCN_TRY(offset_conv_fwd_gemm(h, g, xT, w_off, b_off, off,
+                                   reinterpret_cast<float*>(base + L.wt),
+                                   reinterpret_cast<float*>(base + L.col),
+                                   reinterpret_cast<float*>(base + L.part)));
     }
     return core_forward(h, g, x, off, w, b, d->has_bias != 0, out, xT,
                         reinterpret_cast<float*>(base + L.col), true);
@@ -1194,9 +1264,17 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
     DCN_TRY(fork_aux(h));
     // two-level over (channel, image) blocks (one block per channel held 18 CUs for 0.11 ms)
     dcn::launch_channel_sum_2l(goff, g.B, g.J, g.HW, F(L.part), grad_b_off, h->aux);
-    HIP_TRY(dcn::launch_offset_conv_bwd(g, x, F(L.xT), w_off, goff, F(L.goffT), F(L.wt), grad_x,
-                                        grad_w_off, nullptr,
-                                        dcn::get_force_generic() ? nullptr : F(L.gxT), h->stream));
+    if (ocg_on(g) && (size_t)g.J * g.K <= (size_t)g.B * g.HW * g.O) {
+      // r05: ∂W_off and the offset route of ∂x as GEMMs over the offset conv's im2col (the
+      // columns region is free after K5; ∂W' [J][K] in the ∂outT region, free after ∂col)
+      DCN_TRY(offset_conv_bwd_gemm(h, g, F(L.xT), w_off, goff, F(L.wt), F(L.col), F(L.goffT),
+                                   F(L.goutT), F(L.gxT), grad_x, grad_w_off));
+    } else {
+      HIP_TRY(dcn::launch_offset_conv_bwd(g, x, F(L.xT), w_off, goff, F(L.goffT), F(L.wt), grad_x,
+                                          grad_w_off, nullptr,
+                                          dcn::get_force_generic() ? nullptr : F(L.gxT),
+                                          h->stream));
+    }
     DCN_TRY(join_aux(h));
   }
   return grads_final(h, grad_w_off, grad_b_off, g);
@@ -1822,6 +1900,11 @@ int dcn_debug_force_generic(int on) {
 
 int dcn_debug_bins_chunked(int on) {
   dcn::set_bins_chunked(on);
+  return DCN_OK;
+}
+
+int dcn_debug_offset_gemm(int on) {
+  g_ocg = on != 0;
   return DCN_OK;
 }
 

@@ -132,6 +132,19 @@ hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
 // can run on a side stream beside chunk k+1's col2im: prep (w_off transpose) once,
 // chunk(b0, nb) per image range (after that range's ∂offset exists), finish once (∂W_off
 // partial fold and ∂b_off). Same results as launch_offset_conv_bwd with gxT_in.
+// r05 (fp32, geometries without an MFMA offset-conv kernel): the offset conv as GEMMs over its
+// own im2col `ocol` [B·HW][KK·C] (the `col` region's shape); the host (dcn_api.cpp) runs the
+// GEMMs. W' = [J][KK·C] (w_off with k = t·C + c), offT / ∂offT = [B·HW][J].
+bool offset_conv_gemm_ok(const Geo& g);
+hipError_t launch_ocg_im2col(const Geo& g, const float* xT, float* ocol, hipStream_t s);
+hipError_t launch_ocg_wprime(const Geo& g, const float* w_off, float* wp, hipStream_t s);
+hipError_t launch_ocg_offt_to_off(const Geo& g, const float* offT, const float* b_off, float* off,
+                                  hipStream_t s);
+hipError_t launch_ocg_goff_to_pj(const Geo& g, const float* goff, float* goffT, hipStream_t s);
+hipError_t launch_ocg_wgrad_out(const Geo& g, const float* gwp, float* gw_off, hipStream_t s);
+// ∂x = (gxT_in ? transpose(gxT_in) : ∂x) + the gather of ∂ocol
+hipError_t launch_ocg_col2im(const Geo& g, const float* docol, const float* gxT_in, float* gx,
+                             hipStream_t s);
 bool offset_bwd_chunkable(const Geo& g);
 hipError_t launch_offset_bwd_prep(const Geo& g, const float* w_off, float* wt2, hipStream_t s);
 // xT: the fp32 channels-last x, or (xT_bf16) the bf16 one of DCN_BF16.

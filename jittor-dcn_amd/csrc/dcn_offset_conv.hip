@@ -20,6 +20,7 @@ namespace dcn {
 
 constexpr int kJB = 18;  // offset channels per pass (one pass for the reference's 3x3)
 constexpr int kCB = 32;  // channels per K7b pass
+constexpr int kOcgMaxW = 128;  // ocg_col2im: input row width held in LDS
 
 // Padded sizes: the uniform operand runs are zero-padded so every scalar load is
 // unconditional (the compiler then merges them into s_load_dwordx8/x16).
@@ -2272,6 +2273,166 @@ hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
                                              wt2, goff, gx, gxT_in));
     }
   }
+  return hipGetLastError();
+}
+
+
+// ---------------------------------------------------------------------------
+// r05: the offset conv as GEMMs for the geometries the K3 / K7 kernels above serve only with
+// their VALU forms (stride or dilation != 1, e.g. BASELINE config 5: C = 512, J = 72, 14x14
+// stride 2 dilation 2, where K3 ran at 0.06 and K7 at 0.09 of the f32 MFMA peak). The conv is
+// an ordinary convolution (deform_conv.py:16-21), so with its own im2col
+//   ocol[p][t·C + c] = x[b][c][ho·sh - ph + i·dh][wo·sw - pw + k·dw]   (p = b·HW + m, t = i·kw + k)
+// in the layout of the deformable columns (k = t·C + c: the `col` workspace region serves),
+//   fwd   offT[p][j] = Σ_k W'[j][k] ocol[p][k]           (W'[j][t·C + c] = w_off[j][c][t])
+//   ∂W    ∂W'[j][k]  = Σ_p ∂offT[p][j] ocol[p][k]
+//   ∂x    ∂ocol[p][k] = Σ_j ∂offT[p][j] W'[j][k], then the fixed-order gather of ∂ocol into ∂x
+// on the vendor f32 MFMA GEMMs (dcn_gemm.cpp); every sum has a fixed order (deterministic).
+// ---------------------------------------------------------------------------
+bool offset_conv_gemm_ok(const Geo& g) {
+  const long P = (long)g.B * g.HW, K = (long)g.C * g.kh * g.kw;
+  return g.dt == DCN_F32 && g.C % 4 == 0 && g.W <= kOcgMaxW && g.kh * g.kw <= 9 &&
+         P * K < (1l << 31) &&
+         (long)g.B * g.HWi * g.C < (1l << 31);
+}
+
+// ocol from channels-last xT, one float4 (4 channels) per thread
+__global__ __launch_bounds__(256) void ocg_im2col(Geo g, const float* __restrict__ xT,
+                                                  float* __restrict__ ocol) {
+  const int C4 = g.C >> 2, KK = g.kh * g.kw;
+  const long n = (long)g.B * g.HW * KK * C4;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int c4 = (int)(i % C4);
+    const long r = i / C4;
+    const int t = (int)(r % KK);
+    const long p = r / KK;
+    const int m = (int)(p % g.HW), b = (int)(p / g.HW);
+    const int ho = m / g.Wo, wo = m - ho * g.Wo, ti = t / g.kw, tk = t - ti * g.kw;
+    const int y = ho * g.sh - g.ph + ti * g.dh, x = wo * g.sw - g.pw + tk * g.dw;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (y >= 0 && y < g.H && x >= 0 && x < g.W)
+      v = *reinterpret_cast<const float4*>(xT + (((size_t)b * g.H + y) * g.W + x) * g.C + 4 * c4);
+    reinterpret_cast<float4*>(ocol)[i] = v;  // i = (p·KK + t)·C4 + c4
+  }
+}
+
+// W'[j][t·C + c] = w_off[j][c][t]
+__global__ __launch_bounds__(256) void ocg_wprime(const float* __restrict__ w, float* __restrict__ wp,
+                                                  int J, int C, int KK) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= J * C * KK) return;
+  const int j = i / (C * KK), r = i - j * C * KK, t = r / C, c = r - t * C;
+  wp[i] = w[((size_t)j * C + c) * KK + t];
+}
+
+// off[b][j][m] = offT[b·HW + m][j] + b_off[j] (the bias last, as offset_conv_combine)
+__global__ __launch_bounds__(256) void ocg_offt_to_off(const float* __restrict__ offT,
+                                                       const float* __restrict__ b_off,
+                                                       float* __restrict__ off, int J, int HW,
+                                                       long total) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;  // over (b, j, m): coalesced stores
+  if (i >= total) return;
+  const int m = (int)(i % HW);
+  const long bj = i / HW;
+  const int j = (int)(bj % J), b = (int)(bj / J);
+  off[i] = offT[((size_t)b * HW + m) * J + j] + b_off[j];
+}
+
+// ∂w_off[j][c][t] = ∂W'[j][t·C + c]
+__global__ __launch_bounds__(256) void ocg_wgrad_out(const float* __restrict__ gwp,
+                                                     float* __restrict__ gw, int J, int C, int KK) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // over (j, c, t)
+  if (i >= J * C * KK) return;
+  const int j = i / (C * KK), r = i - j * C * KK, c = r / KK, t = r - c * KK;
+  gw[i] = gwp[(size_t)j * C * KK + (size_t)t * C + c];
+}
+
+// ∂x[b][c][y][x] = (gxT_in ? gxT_in[b][y][x][c] : ∂x[b][c][y][x]) + Σ over the taps t that
+// reach (y, x) from an output pixel, in tap order, of ∂ocol[b·HW + m][t·C + c]. One workgroup
+// per (image, row y, 64-channel slice): lanes run over channels (coalesced ∂ocol rows), the
+// row's sums go through LDS so the NCHW stores run along x. Which output row each kernel row
+// ti reaches from y, and which output column each (x, kernel column tk) comes from, are
+// tabulated once per workgroup (no integer division in the loop).
+constexpr int kOcgT = 9;  // taps tabulated per input pixel (kh·kw <= 9)
+__global__ __launch_bounds__(256) void ocg_col2im(Geo g, const float* __restrict__ docol,
+                                                  const float* __restrict__ gxT_in,
+                                                  float* __restrict__ gx) {
+  __shared__ float tile[kOcgMaxW][65];
+  __shared__ int src[kOcgMaxW][kOcgT];  // ∂ocol element offset of (x, tap) in the image, or -1
+  const int y = blockIdx.x, c0 = blockIdx.y * 64, b = blockIdx.z;
+  const int cl = threadIdx.x & 63, xs = threadIdx.x >> 6;
+  const int c = c0 + cl, KK = g.kh * g.kw;
+  const int K = KK * g.C;
+  for (int i = threadIdx.x; i < g.W * kOcgT; i += 256) {
+    const int x = i / kOcgT, t = i - x * kOcgT;
+    int o = -1;
+    if (t < KK) {
+      const int ti = t / g.kw, tk = t - ti * g.kw;
+      const int yy = y + g.ph - ti * g.dh, xx = x + g.pw - tk * g.dw;
+      if (yy >= 0 && xx >= 0 && yy % g.sh == 0 && xx % g.sw == 0 && yy / g.sh < g.Ho &&
+          xx / g.sw < g.Wo)
+        o = ((yy / g.sh) * g.Wo + xx / g.sw) * K + t * g.C;
+    }
+    src[x][t] = o;
+  }
+  __syncthreads();
+  const float* db = docol + (size_t)b * g.HW * K + min(c, g.C - 1);
+  for (int x = xs; x < g.W; x += 4) {
+    // every tap's load unconditional (a lane past C or a tap that does not reach (y, x) reads
+    // a valid element and drops it): no branch, so no wait per load
+    float v[kOcgT];
+#pragma unroll
+    for (int t = 0; t < kOcgT; ++t) v[t] = db[max(src[x][t], 0)];
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < kOcgT; ++t) s += src[x][t] >= 0 ? v[t] : 0.f;  // tap order
+    // the sampling route's channels-last ∂x, read along the channels (coalesced)
+    tile[x][cl] = gxT_in && c < g.C ? gxT_in[(((size_t)b * g.H + y) * g.W + x) * g.C + c] + s : s;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * g.W; i += 256) {
+    const int cc = i / g.W, x = i - cc * g.W;
+    if (c0 + cc >= g.C) continue;
+    const size_t o = (((size_t)b * g.C + c0 + cc) * g.H + y) * g.W + x;
+    gx[o] = gxT_in ? tile[x][cc] : gx[o] + tile[x][cc];
+  }
+}
+
+hipError_t launch_ocg_im2col(const Geo& g, const float* xT, float* ocol, hipStream_t s) {
+  const long n = (long)g.B * g.HW * g.kh * g.kw * (g.C / 4);
+  const unsigned nb = (unsigned)std::min<long>((n + 255) / 256, 256l * 64);
+  hipLaunchKernelGGL(ocg_im2col, dim3(nb), dim3(256), 0, s, g, xT, ocol);
+  return hipGetLastError();
+}
+hipError_t launch_ocg_wprime(const Geo& g, const float* w_off, float* wp, hipStream_t s) {
+  const int n = g.J * g.C * g.kh * g.kw;
+  hipLaunchKernelGGL(ocg_wprime, dim3((n + 255) / 256), dim3(256), 0, s, w_off, wp, g.J, g.C,
+                     g.kh * g.kw);
+  return hipGetLastError();
+}
+hipError_t launch_ocg_offt_to_off(const Geo& g, const float* offT, const float* b_off, float* off,
+                                  hipStream_t s) {
+  const long n = (long)g.B * g.J * g.HW;
+  hipLaunchKernelGGL(ocg_offt_to_off, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, offT,
+                     b_off, off, g.J, g.HW, n);
+  return hipGetLastError();
+}
+hipError_t launch_ocg_goff_to_pj(const Geo& g, const float* goff, float* goffT, hipStream_t s) {
+  const long n = (long)g.B * g.J * g.HW;
+  hipLaunchKernelGGL(goff_to_pj, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, goff, goffT,
+                     g.J, g.J, g.HW, n);
+  return hipGetLastError();
+}
+hipError_t launch_ocg_wgrad_out(const Geo& g, const float* gwp, float* gw_off, hipStream_t s) {
+  const int n = g.J * g.C * g.kh * g.kw;
+  hipLaunchKernelGGL(ocg_wgrad_out, dim3((n + 255) / 256), dim3(256), 0, s, gwp, gw_off, g.J, g.C,
+                     g.kh * g.kw);
+  return hipGetLastError();
+}
+hipError_t launch_ocg_col2im(const Geo& g, const float* docol, const float* gxT_in, float* gx,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(ocg_col2im, dim3(g.H, (g.C + 63) / 64, g.B), dim3(256), 0, s, g, docol,
+                     gxT_in, gx);
   return hipGetLastError();
 }
 

@@ -104,6 +104,7 @@ SIGNATURES = {
     "dcn_debug_fused_workgroups": [ctypes.c_int],
     "dcn_debug_dw_parts": [_dp, _ip, ctypes.c_int, _ip],
     "dcn_debug_bins_chunked": [ctypes.c_int],
+    "dcn_debug_offset_gemm": [ctypes.c_int],
     "dcn_debug_col_ws_records": [_vp, _ip],
     "dcn_debug_gemm": [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                        _vp, ctypes.c_int, ctypes.c_long, _vp, ctypes.c_int, ctypes.c_long, _vp,

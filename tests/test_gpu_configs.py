@@ -161,6 +161,30 @@ def test_config5_two_images_vs_float64_oracle(gpu_handle):
     _check_all(out, off, g, ro, roff, O.backward(cache, c["grad_out"]), "config5 f64")
 
 
+@pytest.mark.parametrize("geo", [
+    dict(C=512, O_=64, H=14, W=14, s=(2, 2), p=(1, 1), dil=(2, 2), G=4),  # config 5's offset conv
+    dict(C=64, O_=32, H=13, W=11, s=(2, 1), p=(1, 0), dil=(1, 2), G=1),   # ragged, mixed s / dil
+])
+def test_offset_conv_gemm_vs_valu_kernels(gpu_handle, geo):
+    """r05: the fp32 offset conv of geometries without an MFMA offset-conv kernel runs as GEMMs
+    over its own im2col (dcn_api.cpp offset_conv_fwd_gemm / _bwd_gemm). Same results as the
+    VALU kernels it replaced (dcn_debug_offset_gemm(0)) up to fp32 summation order, and the
+    whole step against the C oracle (conditioned on the device's offsets)."""
+    c = _rand_case(511, B=4, **geo)
+    L = gpu_handle.lib
+    rt.check(L.dcn_debug_offset_gemm(0))
+    try:
+        out0, off0, g0 = _device_fwd_bwd(gpu_handle, c)
+    finally:
+        rt.check(L.dcn_debug_offset_gemm(1))
+    out1, off1, g1 = _device_fwd_bwd(gpu_handle, c)
+    assert_close(off1, off0, what="offsets: GEMM vs VALU")
+    for k in ("offset_conv.weight", "offset_conv.bias"):
+        assert_close_reduction(g1[k], g0[k], what=f"∂{k}: GEMM vs VALU")
+    ro, roff, rg = _c_oracle_all(c, off1)
+    _check_all(out1, off1, g1, ro, roff, rg, "offset-conv GEMM path")
+
+
 # ---- data-parallel exchange hooks on one rank -------------------------------------------
 
 def test_fp32_backward_with_attached_comm_single_rank(gpu_handle):
