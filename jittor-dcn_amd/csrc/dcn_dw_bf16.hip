@@ -65,7 +65,8 @@ typedef __attribute__((address_space(3))) void lvoid;
 #define DW_PIN 0
 #endif
 // DW_ABL (diagnostic A/B builds only, wrong results): 1 LDS reads without MFMAs, 2 the DMA
-// stream alone, 3 the column tiles read as contiguous [tile][pixel][256] blocks
+// stream alone, 3 the column tiles read as contiguous [tile][pixel][256] blocks, 5 the column
+// DMAs only (no ∂outT stream), 6 no partial-plane stores
 #ifndef DW_ABL
 #define DW_ABL 0
 #endif
@@ -86,6 +87,7 @@ constexpr int kDwWaves = 8;
 constexpr int kDwLoaders = DW_LOADERS;
 static_assert(kDwLoaders == 2 || kDwLoaders == 4 || kDwLoaders == 8, "loader waves");
 constexpr int kDwGlds = kDwStageB / (kDwLoaders * 1024);  // DMA instructions per loader per stage
+constexpr int kDwWaitG = DW_ABL == 5 ? kDwGlds / 2 : kDwGlds;  // ... that the waits count
 constexpr int kDwOpI = kDwPx / 2;                  // DMA instructions per operand (2 rows each)
 static_assert(kDwPx == 16 || kDwPx == 32, "stage = one or two 16-pixel k-steps");
 static_assert(kDwRing >= 3 && kDwRing <= 8, "ring depth");
@@ -177,6 +179,9 @@ __global__ __launch_bounds__(kDwWaves * 64, 1) void dw_stream_bf16(
 #pragma unroll
     for (int u = 0; u < kDwGlds; ++u) {
       const int ii = u * kDwLoaders + w, op = ii / kDwOpI, i = ii % kDwOpI;
+#if DW_ABL == 5  // (diagnostic build: the column DMAs only, no ∂outT stream)
+      if (op == 0) continue;
+#endif
       const int row = 2 * i + lrow;
       const unsigned ch = (unsigned)(lpc ^ (4 * (row & 3)));
       const int p = min(px0 + j * kDwPx + row, npix - 1);  // past the end: re-read the last row
@@ -269,13 +274,13 @@ __global__ __launch_bounds__(kDwWaves * 64, 1) void dw_stream_bf16(
     __builtin_amdgcn_sched_barrier(0);
     // this wave's DMAs of stage s have landed once only those of s + 1 .. s + kDwAhead are
     // pending
-    vm_wait<kDwAhead * kDwGlds>();
+    vm_wait<kDwAhead * kDwWaitG>();
     __builtin_amdgcn_s_barrier();  // every wave's DMAs of stage s landed
     __builtin_amdgcn_sched_barrier(0);
 #else
     // this wave's DMAs of stage s have landed once only those of s + 1 .. s + kDwAhead - 1
     // are pending
-    vm_wait<(kDwAhead - 1) * kDwGlds>();
+    vm_wait<(kDwAhead - 1) * kDwWaitG>();
     // every wave's DMAs of stage s landed; every wave finished reading stage s - 1, whose
     // slot (`refill`) the DMA of stage s + kDwAhead now refills
     __builtin_amdgcn_s_barrier();
@@ -313,7 +318,11 @@ __global__ __launch_bounds__(kDwWaves * 64, 1) void dw_stream_bf16(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int o = 128 * wo + 32 * mi + drow(r, hh);
+#if DW_ABL == 6  // (diagnostic build: no partial-plane stores)
+        asm volatile("" ::"v"(acc[mi][ni][r]));
+#else
         dst[(size_t)o * K + 64 * wk + 32 * ni + n] = acc[mi][ni][r];
+#endif
       }
 }
 

@@ -57,6 +57,9 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 #ifndef FUSED_ABL
 #define FUSED_ABL 0
 #endif
+#ifndef FUSED_STAGGER
+#define FUSED_STAGGER 0
+#endif
 // FUSED_PP = 1 (A/B builds): the forwards run as fwd_fused_bf16_pp (two tiles per workgroup
 // in ping-pong); 0: fwd_fused_bf16 (one tile per workgroup, the measured faster: DESIGN.md §4.8)
 #ifndef FUSED_PP
@@ -199,6 +202,13 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
   const int stamp_wg = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
   (void)stamp_wg;
   STAMP(0);
+#if FUSED_STAGGER
+  // (A/B builds) the second half of the grid, dispatched as each CU's second workgroup,
+  // starts FUSED_STAGGER × 64 cycles late, so the two workgroups of a CU run out of phase
+  if (stamp_wg >= (int)(gridDim.x * gridDim.y * gridDim.z) / 2) {
+    for (int i = 0; i < FUSED_STAGGER / 16; ++i) __builtin_amdgcn_s_sleep(16);
+  }
+#endif
   const int h0 = th_i * kTH, w0 = tw_i * kTW;
   const int o0 = blk.z * kOT + 64 * wave;
   const int rlo = (int)floorf((float)w0 * (float)(g.H - 1) / (float)(g.Wo - 1)) - kMar;
