@@ -2353,15 +2353,19 @@ __global__ __launch_bounds__(256) void ocg_wgrad_out(const float* __restrict__ g
 // row's sums go through LDS so the NCHW stores run along x. Which output row each kernel row
 // ti reaches from y, and which output column each (x, kernel column tk) comes from, are
 // tabulated once per workgroup (no integer division in the loop).
-constexpr int kOcgT = 9;  // taps tabulated per input pixel (kh·kw <= 9)
+constexpr int kOcgT = 9;     // taps tabulated per input pixel (kh·kw <= 9)
+constexpr int kOcgXC = 16;   // input pixels of a row per pass (LDS tile rows)
+// workgroup = (image, row y, 256-channel slice); lane = 4 channels (16-B loads of the ∂ocol
+// rows), the 4 waves split the row's pixels; passes of kOcgXC pixels through an LDS tile so
+// the NCHW stores run along x
 __global__ __launch_bounds__(256) void ocg_col2im(Geo g, const float* __restrict__ docol,
                                                   const float* __restrict__ gxT_in,
                                                   float* __restrict__ gx) {
-  __shared__ float tile[kOcgMaxW][65];
+  __shared__ float4 tile[kOcgXC][65];
   __shared__ int src[kOcgMaxW][kOcgT];  // ∂ocol element offset of (x, tap) in the image, or -1
-  const int y = blockIdx.x, c0 = blockIdx.y * 64, b = blockIdx.z;
+  const int y = blockIdx.x, c0 = blockIdx.y * 256, b = blockIdx.z;
   const int cl = threadIdx.x & 63, xs = threadIdx.x >> 6;
-  const int c = c0 + cl, KK = g.kh * g.kw;
+  const int c = c0 + 4 * cl, KK = g.kh * g.kw;
   const int K = KK * g.C;
   for (int i = threadIdx.x; i < g.W * kOcgT; i += 256) {
     const int x = i / kOcgT, t = i - x * kOcgT;
@@ -2376,25 +2380,40 @@ __global__ __launch_bounds__(256) void ocg_col2im(Geo g, const float* __restrict
     src[x][t] = o;
   }
   __syncthreads();
-  const float* db = docol + (size_t)b * g.HW * K + min(c, g.C - 1);
-  for (int x = xs; x < g.W; x += 4) {
-    // every tap's load unconditional (a lane past C or a tap that does not reach (y, x) reads
-    // a valid element and drops it): no branch, so no wait per load
-    float v[kOcgT];
+  const float* db = docol + (size_t)b * g.HW * K + min(c, g.C - 4);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int x0 = 0; x0 < g.W; x0 += kOcgXC) {
+    const int nx = min(kOcgXC, g.W - x0);
+    for (int xl = xs; xl < nx; xl += 4) {
+      const int x = x0 + xl;
+      // every tap's load unconditional (a lane past C or a tap that does not reach (y, x)
+      // reads a valid element and drops it): no branch, so no wait per load
+      float4 v[kOcgT];
 #pragma unroll
-    for (int t = 0; t < kOcgT; ++t) v[t] = db[max(src[x][t], 0)];
-    float s = 0.f;
+      for (int t = 0; t < kOcgT; ++t)
+        v[t] = *reinterpret_cast<const float4*>(db + max(src[x][t], 0));
+      float4 s = z4;
 #pragma unroll
-    for (int t = 0; t < kOcgT; ++t) s += src[x][t] >= 0 ? v[t] : 0.f;  // tap order
-    // the sampling route's channels-last ∂x, read along the channels (coalesced)
-    tile[x][cl] = gxT_in && c < g.C ? gxT_in[(((size_t)b * g.H + y) * g.W + x) * g.C + c] + s : s;
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < 64 * g.W; i += 256) {
-    const int cc = i / g.W, x = i - cc * g.W;
-    if (c0 + cc >= g.C) continue;
-    const size_t o = (((size_t)b * g.C + c0 + cc) * g.H + y) * g.W + x;
-    gx[o] = gxT_in ? tile[x][cc] : gx[o] + tile[x][cc];
+      for (int t = 0; t < kOcgT; ++t)  // tap order
+        if (src[x][t] >= 0) s = make_float4(s.x + v[t].x, s.y + v[t].y, s.z + v[t].z, s.w + v[t].w);
+      if (gxT_in && c < g.C) {  // the sampling route's channels-last ∂x, along the channels
+        const float4 q =
+            *reinterpret_cast<const float4*>(gxT_in + (((size_t)b * g.H + y) * g.W + x) * g.C + c);
+        s = make_float4(q.x + s.x, q.y + s.y, q.z + s.z, q.w + s.w);
+      }
+      tile[xl][cl] = s;
+    }
+    __syncthreads();
+    // NCHW stores: runs of nx pixels per channel
+    for (int i = threadIdx.x; i < 256 * nx; i += 256) {
+      const int cc = i / nx, xl = i - cc * nx;
+      if (c0 + cc >= g.C) continue;
+      const float4 t4 = tile[xl][cc >> 2];
+      const float v = (cc & 3) == 0 ? t4.x : (cc & 3) == 1 ? t4.y : (cc & 3) == 2 ? t4.z : t4.w;
+      const size_t o = (((size_t)b * g.C + c0 + cc) * g.H + y) * g.W + x0 + xl;
+      gx[o] = gxT_in ? v : gx[o] + v;
+    }
+    __syncthreads();
   }
 }
 
@@ -2431,7 +2450,7 @@ hipError_t launch_ocg_wgrad_out(const Geo& g, const float* gwp, float* gw_off, h
 }
 hipError_t launch_ocg_col2im(const Geo& g, const float* docol, const float* gxT_in, float* gx,
                              hipStream_t s) {
-  hipLaunchKernelGGL(ocg_col2im, dim3(g.H, (g.C + 63) / 64, g.B), dim3(256), 0, s, g, docol,
+  hipLaunchKernelGGL(ocg_col2im, dim3(g.H, (g.C + 255) / 256, g.B), dim3(256), 0, s, g, docol,
                      gxT_in, gx);
   return hipGetLastError();
 }
