@@ -60,6 +60,9 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 #ifndef FUSED_STAGGER
 #define FUSED_STAGGER 0
 #endif
+#ifndef FUSED_W0EARLY
+#define FUSED_W0EARLY 1
+#endif
 // FUSED_PP = 1 (A/B builds): the forwards run as fwd_fused_bf16_pp (two tiles per workgroup
 // in ping-pong); 0: fwd_fused_bf16 (one tile per workgroup, the measured faster: DESIGN.md §4.8)
 #ifndef FUSED_PP
@@ -215,6 +218,24 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
   const int qlo = (int)floorf((float)h0 * (float)(g.W - 1) / (float)(g.Ho - 1)) - kMar;
   const bf16_t* const xb = xT + (size_t)b * g.HWi * g.C;
   const int N = g.N;
+
+  // window slice cs: kWPix pixels × 8 parts of 16 B (zeros outside the image)
+  auto win_load = [&](int cs, uint4 (&v)[(kWPix * 8 + 255) / 256]) {
+    constexpr int TOT = kWPix * 8, IT = (TOT + 255) / 256;
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      const int idx = tid + k * 256;
+      const int pix = idx >> 3, part = idx & 7;
+      const int rr = pix / kWQ, qq = pix - rr * kWQ;
+      const int r = rlo + rr, q = qlo + qq;
+      const bool ok = idx < TOT && r >= 0 && r < g.H && q >= 0 && q < g.W;
+      v[k] = ld16_if(xb + ((size_t)r * g.W + q) * g.C + kCS * cs + 8 * part, ok);
+    }
+  };
+  // FUSED_W0EARLY: slice 0's window loads go out before the records (r05: records 4.9 µs,
+  // then the slice-0 window 7.0 µs, one after the other, tools/fused_stamps.py)
+  uint4 w0v[(kWPix * 8 + 255) / 256];
+  if (FUSED_W0EARLY) win_load(0, w0v);
 
   // ---- records ----
   if (tid == 0) cnt[0] = 0;
@@ -406,14 +427,11 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
       // window slice: kWPix pixels × 8 parts of 16 B; overflow corners loaded alongside
       constexpr int TOT = kWPix * 8, IT = (TOT + 255) / 256;
       uint4 v[IT];
+      if (FUSED_W0EARLY && cs == 0) {  // (issued before the records)
 #pragma unroll
-      for (int k = 0; k < IT; ++k) {
-        const int idx = tid + k * 256;
-        const int pix = idx >> 3, part = idx & 7;
-        const int rr = pix / kWQ, qq = pix - rr * kWQ;
-        const int r = rlo + rr, q = qlo + qq;
-        const bool ok = idx < TOT && r >= 0 && r < g.H && q >= 0 && q < g.W;
-        v[k] = ld16_if(xb + ((size_t)r * g.W + q) * g.C + kCS * cs + 8 * part, ok);
+        for (int k = 0; k < IT; ++k) v[k] = w0v[k];
+      } else {
+        win_load(cs, v);
       }
       // overflow: novf entries × 8 units of 8 channels
       uint4 ov[2];
