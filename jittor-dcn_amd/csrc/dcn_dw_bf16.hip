@@ -66,7 +66,8 @@ typedef __attribute__((address_space(3))) void lvoid;
 #endif
 // DW_ABL (diagnostic A/B builds only, wrong results): 1 LDS reads without MFMAs, 2 the DMA
 // stream alone, 3 the column tiles read as contiguous [tile][pixel][256] blocks, 5 the column
-// DMAs only (no ∂outT stream), 6 no partial-plane stores
+// DMAs only (no ∂outT stream), 6 no partial-plane stores, 7 the DMA stream alone without the
+// stage barriers
 #ifndef DW_ABL
 #define DW_ABL 0
 #endif
@@ -230,7 +231,7 @@ __global__ __launch_bounds__(kDwWaves * 64, 1) void dw_stream_bf16(
   // launch: the ∂outT rows past the end (DMA'd from the last row) are zeroed in the A
   // fragments, so their products vanish
   auto compute = [&](const char* slot, int nvalid) {
-#if DW_ABL == 2
+#if DW_ABL == 2 || DW_ABL == 7
     return;  // (diagnostic build: the DMA stream alone)
 #endif
 #pragma unroll
@@ -283,7 +284,9 @@ __global__ __launch_bounds__(kDwWaves * 64, 1) void dw_stream_bf16(
     vm_wait<(kDwAhead - 1) * kDwWaitG>();
     // every wave's DMAs of stage s landed; every wave finished reading stage s - 1, whose
     // slot (`refill`) the DMA of stage s + kDwAhead now refills
+#if DW_ABL != 7  // (7: diagnostic build, the DMA stream alone without the stage barriers)
     __builtin_amdgcn_s_barrier();
+#endif
     __builtin_amdgcn_sched_barrier(0);
     issue(s + kDwAhead, refill);
     __builtin_amdgcn_sched_barrier(0);
