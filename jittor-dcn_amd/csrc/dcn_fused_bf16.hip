@@ -61,7 +61,7 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 #define FUSED_STAGGER 0
 #endif
 #ifndef FUSED_W0EARLY
-#define FUSED_W0EARLY 1
+#define FUSED_W0EARLY 0
 #endif
 // FUSED_PP = 1 (A/B builds): the forwards run as fwd_fused_bf16_pp (two tiles per workgroup
 // in ping-pong); 0: fwd_fused_bf16 (one tile per workgroup, the measured faster: DESIGN.md §4.8)
@@ -232,8 +232,9 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
       v[k] = ld16_if(xb + ((size_t)r * g.W + q) * g.C + kCS * cs + 8 * part, ok);
     }
   };
-  // FUSED_W0EARLY: slice 0's window loads go out before the records (r05: records 4.9 µs,
-  // then the slice-0 window 7.0 µs, one after the other, tools/fused_stamps.py)
+  // FUSED_W0EARLY = 1 (A/B builds): slice 0's window loads before the records (r05: records 4.9 µs,
+  // then the slice-0 window 7.0 µs, one after the other); slower, 0.152-0.155 vs 0.142-0.143 ms
+  // (the window registers live across the records loop: 40 spills instead of 12)
   uint4 w0v[(kWPix * 8 + 255) / 256];
   if (FUSED_W0EARLY) win_load(0, w0v);
 
