@@ -16,6 +16,29 @@
 #include "dcn_device.h"
 #include "dcn_swizzle.h"
 
+// A/B switch: 1 = the r04 FOLD staging loop (one load latency per item) in
+// offset_conv_fwd_mfma_bf16_row<SPT, true>
+#ifndef OFFC_FOLD_SERIAL
+#define OFFC_FOLD_SERIAL 0
+#endif
+// A/B switch: 1 = the r04 weight prefetch (one tap ahead, first tap after the staging)
+#ifndef OFFC_W1
+#define OFFC_W1 0
+#endif
+// OFFC_STAMP = 1 (diagnostic A/B builds only): thread 0 of each workgroup of the folding
+// bf16 offset-conv forward records s_memrealtime (100 MHz) at its phase boundaries;
+// dcn_debug_offc_stamps copies them out (tools/offc_stamps.py)
+#ifndef OFFC_STAMP
+#define OFFC_STAMP 0
+#endif
+// A/B: offset_wgrad_bf16's x prefetch depth (steps) and ∂offset staging loads in flight
+#ifndef OFFW_PF
+#define OFFW_PF 3
+#endif
+#ifndef OFFW_SG
+#define OFFW_SG 8
+#endif
+
 namespace dcn {
 
 constexpr int kJB = 18;  // offset channels per pass (one pass for the reference's 3x3)
@@ -1108,6 +1131,19 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16(
 // block writes its own input row (window row ph: stride 1, Ho == H) to xT — the channels-last
 // copy K1 / the fused forward / K5 read — so x is read in one pass and the separate transpose
 // launch disappears, as offset_conv_fwd_mfma_xt does for fp32 (offset_fwd_bf16_fold_ok).
+#if OFFC_STAMP
+constexpr int kOStampWg = 4096, kOStamps = 8;
+__device__ unsigned long long g_offc_stamps[kOStampWg * kOStamps];
+#define OSTAMP(i)                                                                     \
+  do {                                                                                \
+    if (FOLD && threadIdx.x == 0 && ostamp_wg < kOStampWg)                            \
+      g_offc_stamps[ostamp_wg * kOStamps + (i)] = __builtin_amdgcn_s_memrealtime();    \
+  } while (0)
+#else
+#define OSTAMP(i) \
+  do {            \
+  } while (0)
+#endif
 template <int SPT, bool FOLD = false>
 __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
     Geo g, const bf16_t* __restrict__ xT, const bf16_t* __restrict__ wb, int Cp,
@@ -1123,6 +1159,24 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
   const int KH = g.kh, KK = g.kh * g.kw;
   bf16_t* L = reinterpret_cast<bf16_t*>(smem_row) + (size_t)w * KH * SWc * P;
   const int cw = w * SPT * 16;  // this wave's first channel
+#if OFFC_STAMP
+  const int ostamp_wg = blk.z * gridDim.x + blk.x;
+#endif
+  OSTAMP(0);
+  // B = weight fragments (L2-resident) in a 3-tap register ring; r05: the first two taps
+  // are requested before the window staging, so their latency hides behind it, and the
+  // loop keeps two taps in flight (one ahead waited an L2 latency per tap)
+  bf16x8_t bv[3][SPT];
+  auto ldb = [&](int t, bf16x8_t(&rb)[SPT]) {
+    const int tt = min(t, KK - 1);
+    const bf16_t* wp = wb + ((size_t)(tt * (Cp / 16) + w * SPT) * 64 + lane) * 8;
+#pragma unroll
+    for (int u = 0; u < SPT; ++u) rb[u] = ld_bf16x8(wp + 512 * u);
+  };
+#if !OFFC_W1
+  ldb(0, bv[0]);
+  ldb(1, bv[1]);
+#endif
   if constexpr (FOLD) {
     // zero the slice (image borders and the channel padding past C stay zero), then the
     // in-image part from NCHW rows: item = (channel pair, window row, 4-pixel chunk), two
@@ -1132,6 +1186,7 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
     __builtin_amdgcn_wave_barrier();
     const int NQ = g.W / 4, x0 = -g.pw;  // wo0 == 0 (tpr == 1)
     const int nit = 8 * SPT * KH * NQ;
+#if OFFC_FOLD_SERIAL
     const bf16_t* xb = x_nchw + (size_t)b * g.C * g.HWi;
     for (int it = lane; it < nit; it += 64) {
       const int q = it % NQ, rest = it / NQ;
@@ -1148,7 +1203,50 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
       d[2 * PW] = (u0.y & 0xffffu) | (u1.y << 16);
       d[3 * PW] = (u0.y >> 16) | (u1.y & 0xffff0000u);
     }
+#else
+    // r05: a lane's items all in flight at once (kF per batch: one batch for kh = 3,
+    // W <= 32, C = 256), through a buffer resource, so rows outside the image and channels
+    // past C read zeros and every LDS store is unconditional (the serial loop above waited
+    // one memory latency per item, ~10 per block at config 4). A slot past nit repeats item
+    // nit-1 (same value, same place).
+    const auto rxn = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(x_nchw + (size_t)b * g.C * g.HWi), 0,
+        (int)((size_t)g.C * g.HWi * 2), 0x00020000);
+    // quotients by NQ and KH as umulhi by ceil(2^32/d), exact here (it < 2^16); d = 1 wraps
+    // that multiplier to 0 and is taken apart
+    const unsigned mq = 0xffffffffu / (unsigned)NQ + 1u, mk = 0xffffffffu / (unsigned)KH + 1u;
+    constexpr int kF = 12;
+    for (int it0 = lane; it0 < nit; it0 += 64 * kF) {
+      uint2 u0[kF], u1[kF];
+      int dst[kF];
+#pragma unroll
+      for (int u = 0; u < kF; ++u) {
+        const int it = min(it0 + 64 * u, nit - 1);
+        const int rest = NQ == 1 ? it : (int)__umulhi((unsigned)it, mq), q = it - rest * NQ;
+        const int cp = KH == 1 ? rest : (int)__umulhi((unsigned)rest, mk), i = rest - cp * KH;
+        const int y = ho - g.ph + i, c = cw + 2 * cp;
+        const bool ok = y >= 0 && y < g.H && c < g.C;
+        const unsigned o = ok ? (unsigned)(((c * g.H + y) * g.W + 4 * q) * 2) : 0x80000000u;
+        const auto a = __builtin_amdgcn_raw_buffer_load_b64(rxn, o, 0, 0);
+        const auto a1 = __builtin_amdgcn_raw_buffer_load_b64(rxn, o + (unsigned)(g.HWi * 2), 0, 0);
+        u0[u] = make_uint2(a[0], a[1]);
+        u1[u] = make_uint2(a1[0], a1[1]);
+        dst[u] = (i * SWc + 4 * q - x0) * P + 2 * cp;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < kF; ++u) {
+        unsigned* d = reinterpret_cast<unsigned*>(L + dst[u]);
+        constexpr int PW = P / 2;  // pixel pitch in 32-bit words
+        d[0] = (u0[u].x & 0xffffu) | (u1[u].x << 16);
+        d[PW] = (u0[u].x >> 16) | (u1[u].x & 0xffff0000u);
+        d[2 * PW] = (u0[u].y & 0xffffu) | (u1[u].y << 16);
+        d[3 * PW] = (u0[u].y >> 16) | (u1[u].y & 0xffff0000u);
+      }
+    }
+#endif
     __builtin_amdgcn_wave_barrier();
+    OSTAMP(1);
     // input row ho (window row ph) -> xT[b][ho][px][cw ..]: 16-B runs of 8 channels
     const int ir = g.ph;
     const int nch = min(16 * SPT, g.C - cw);
@@ -1158,6 +1256,7 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
       const uint4 v = *reinterpret_cast<const uint4*>(L + (ir * SWc + px - x0) * P + 8 * ch8);
       *reinterpret_cast<uint4*>(xT_out + (((size_t)b * g.H + ho) * g.W + px) * g.C + cw + 8 * ch8) = v;
     }
+    OSTAMP(2);
   } else {
     const auto rx = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<bf16_t*>(xT + (size_t)b * g.HWi * g.C), 0, (int)((size_t)g.HWi * g.C * 2),
@@ -1193,15 +1292,8 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
   f32x16 acc;
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-  bf16x8_t bv[2][SPT];
   // lanes past the row's last pixel (Wo < 32) read the last pixel's window (discarded)
   const int rc = min(r, (SWc - 1 - (g.kw - 1) * g.dw) / g.sw);
-  auto ldb = [&](int t, bf16x8_t(&rb)[SPT]) {
-    const int tt = min(t, KK - 1);
-    const bf16_t* wp = wb + ((size_t)(tt * (Cp / 16) + w * SPT) * 64 + lane) * 8;
-#pragma unroll
-    for (int u = 0; u < SPT; ++u) rb[u] = ld_bf16x8(wp + 512 * u);
-  };
   auto mma = [&](int t, const bf16x8_t(&rb)[SPT]) {
     const int i = t / g.kw, k = t - i * g.kw;
     const bf16_t* ap = L + (i * SWc + rc * g.sw + k * g.dw) * P + 8 * hh;
@@ -1212,6 +1304,7 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
     for (int u = 0; u < SPT; ++u)
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[u], rb[u], acc, 0, 0, 0);
   };
+#if OFFC_W1
   ldb(0, bv[0]);
   for (int t = 0; t < KK; t += 2) {
     ldb(t + 1, bv[1]);
@@ -1220,11 +1313,25 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
     ldb(t + 2, bv[0]);
     mma(t + 1, bv[1]);
   }
+#else
+  for (int t = 0; t < KK; t += 3) {
+    ldb(t + 2, bv[2]);
+    mma(t, bv[0]);
+    if (t + 1 >= KK) break;
+    ldb(t + 3, bv[0]);
+    mma(t + 1, bv[1]);
+    if (t + 2 >= KK) break;
+    ldb(t + 4, bv[1]);
+    mma(t + 2, bv[2]);
+  }
+#endif
   // fold the 4 channel partials in wave order through the (now free) window LDS
   __syncthreads();
+  OSTAMP(3);
   f32x16* red = reinterpret_cast<f32x16*>(smem_row);
   if (w > 0) red[(w - 1) * 64 + lane] = acc;
   __syncthreads();
+  OSTAMP(4);
   if (w != 0) return;
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
@@ -1246,6 +1353,7 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
       off[o] = f2bf(v);  // exact: v is a bf16 value
     }
   }
+  OSTAMP(5);
 }
 
 // LDS bytes of offset_conv_fwd_mfma_bf16_row (0: the row kernel does not apply)
@@ -1356,9 +1464,9 @@ __global__ __launch_bounds__(256) void woff_to_ck_bf16(const bf16_t* __restrict_
   if (i < C * KT16) swz_ck(w, wc, J, J8, C, KK, KT16, i);
 }
 
+template <int kU = 8>
 __device__ __forceinline__ void stage_goff8(const Geo& g, const float* __restrict__ goff, int b,
                                             int y0, int SR, int SW, int J8, int PJ, float* S) {
-  constexpr int kU = 8;
   const int plane = SR * SW, n = plane * J8;
   const unsigned mp = 0xffffffffu / (unsigned)plane + 1u, ms = 0xffffffffu / (unsigned)SW + 1u;
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(goff + (size_t)b * g.J * g.HW),
@@ -1588,7 +1696,7 @@ __global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __
   const unsigned xl0 = (unsigned)((r * g.HWi + y0 * g.W + 8 * hh) * 2);
   const unsigned xl1 = xl0 + (unsigned)(32 * g.HWi * 2);
   const int nsteps = (npx + 15) / 16;
-  constexpr int kPf = 3;
+  constexpr int kPf = OFFW_PF;
   bf16x8_t ra0[kPf], ra1[kPf];
   auto lda = [&](int i, int d) {
     const bool in = i < nsteps && 16 * i + 8 * hh < npx;
@@ -1601,7 +1709,7 @@ __global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __
 #pragma unroll
   for (int d = 0; d < kPf - 1; ++d) lda(d, d);
   if (ci > 0) __syncthreads();  // the previous chunk's staged rows are no longer read
-  stage_goff8(g, goff, b, y0, nrows + (g.kh - 1) * g.dh, SW, J8, PJ, S);
+  stage_goff8<OFFW_SG>(g, goff, b, y0, nrows + (g.kh - 1) * g.dh, SW, J8, PJ, S);
   __syncthreads();
   // (row, column) in the chunk of this lane's first pixel q = 16i + 8hh: q and W are
   // multiples of 4, so pixels q..q+3 share a row, as do q+4..q+7
@@ -2456,3 +2564,13 @@ hipError_t launch_ocg_col2im(const Geo& g, const float* docol, const float* gxT_
 }
 
 }  // namespace dcn
+
+#if OFFC_STAMP
+// (diagnostic builds only) the stamps of the last folding bf16 offset-conv forward
+extern "C" int dcn_debug_offc_stamps(unsigned long long* host, int n) {
+  if (n > dcn::kOStampWg) n = dcn::kOStampWg;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dcn::g_offc_stamps),
+                             sizeof(unsigned long long) * dcn::kOStamps * n, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
