@@ -32,6 +32,20 @@
 #define OFFC_STAMP 0
 #endif
 // A/B: offset_wgrad_bf16's x prefetch depth (steps) and ∂offset staging loads in flight
+// A/B (r05, config 4): the ∂W_off kernel on pre-split records gathered as bf16 pairs measured
+// 0.092-0.0926 ms for the offset backward against 0.0913-0.0916 on fp32 split in the loop
+// (its 32 two-byte LDS reads per step cost more than the split), so 0
+#ifndef OFFW_PRESPLIT
+#define OFFW_PRESPLIT 0
+#endif
+// r05 (config 4): the ∂x kernel on pre-split records, offset backward 0.0944-0.0951 ->
+// 0.092-0.0926 ms (k loop 11.3 -> 7.9 us per workgroup, tools/offc_stamps.py)
+#ifndef OFFD_PRESPLIT
+#define OFFD_PRESPLIT 1
+#endif
+#ifndef OFFD_EPI
+#define OFFD_EPI 0
+#endif
 #ifndef OFFW_PF
 #define OFFW_PF 3
 #endif
@@ -1494,6 +1508,43 @@ __device__ __forceinline__ void stage_goff8(const Geo& g, const float* __restric
   }
 }
 
+// stage_goff8 with each value written pre-split: Sb[(sr·SW + sc)·PB + j] = hi = bf16(v) and
+// Sb[... + J8 + j] = lo = bf16(v - hi) (PB = 2·PJ bf16: the fp32 layout's bytes, so the same
+// pixel stride and 16-B alignment), split8's bits exactly; r05: the ∂x kernel read fp32 and
+// split in its k loop, once per wave and tap reuse (≈ 70 of its 125 VALU per step: the loop
+// was VALU-bound at twice its MFMA time)
+template <int kU = 8>
+__device__ __forceinline__ void stage_goff8_split(const Geo& g, const float* __restrict__ goff,
+                                                  int b, int y0, int SR, int SW, int J8, int PB,
+                                                  bf16_t* Sb) {
+  const int plane = SR * SW, n = plane * J8;
+  const unsigned mp = 0xffffffffu / (unsigned)plane + 1u, ms = 0xffffffffu / (unsigned)SW + 1u;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(goff + (size_t)b * g.J * g.HW),
+                                                    0, (int)((size_t)g.J * g.HW * 4), 0x00020000);
+  for (int i0 = threadIdx.x; i0 < n; i0 += blockDim.x * kU) {
+    float v[kU];
+    int dst[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int idx = min(i0 + u * (int)blockDim.x, n - 1);
+      const int j = (int)__umulhi((unsigned)idx, mp), rem = idx - j * plane;
+      const int sr = (int)__umulhi((unsigned)rem, ms), sc = rem - sr * SW;
+      const int ho = y0 + sr - (g.kh - 1) * g.dh + g.ph, wo = sc - (g.kw - 1) * g.dw + g.pw;
+      const bool ok = j < g.J && ho >= 0 && ho < g.Ho && wo >= 0 && wo < g.Wo;
+      const unsigned o = ok ? (unsigned)((j * g.HW + ho * g.Wo + wo) * 4) : 0x80000000u;
+      v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o, 0, 0));
+      dst[u] = rem * PB + j;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const __bf16 h = (__bf16)v[u];
+      Sb[dst[u]] = __builtin_bit_cast(bf16_t, h);
+      Sb[dst[u] + J8] = __builtin_bit_cast(bf16_t, (__bf16)(v[u] - (float)h));
+    }
+  }
+}
+
 __device__ __forceinline__ int toff8(const Geo& g, int t, int SW, int PJ) {
   const int i = t / g.kw, k = t - i * g.kw;
   return ((g.kh - 1 - i) * g.dh * SW + (g.kw - 1 - k) * g.dw) * PJ;
@@ -1514,6 +1565,19 @@ __device__ __forceinline__ void split8(const float (&v)[8], bf16x8_t& hi, bf16x8
 // bf16 NCHW (the API's grad_x). r04: the epilogue reads and writes through buffer resources
 // (32-bit offsets), which cut 160 VGPRs + 64 AGPRs to 121 registers: 4 workgroups per CU
 // instead of 2, so config 4's 832 workgroups run in one round.
+#if OFFC_STAMP
+__device__ unsigned long long g_offd_stamps[kOStampWg * kOStamps];
+__device__ unsigned long long g_offw_stamps[kOStampWg * kOStamps];
+#define BSTAMP(arr, wg, i)                                                     \
+  do {                                                                         \
+    if (threadIdx.x == 0 && (wg) < kOStampWg)                                  \
+      arr[(wg) * kOStamps + (i)] = __builtin_amdgcn_s_memrealtime();           \
+  } while (0)
+#else
+#define BSTAMP(arr, wg, i) \
+  do {                     \
+  } while (0)
+#endif
 __global__ __launch_bounds__(256, 3) void offset_dgrad_bf16(Geo g, const bf16_t* __restrict__ wc,
                                                         int KT16, const float* __restrict__ goff,
                                                         const float* __restrict__ gxT_in,
@@ -1544,15 +1608,36 @@ __global__ __launch_bounds__(256, 3) void offset_dgrad_bf16(Geo g, const bf16_t*
   };
 #pragma unroll
   for (int d = 0; d < kPf - 1; ++d) lda(d, d);
+  BSTAMP(g_offd_stamps, bid, 0);
+#if OFFD_PRESPLIT
+  // pre-split hi/lo records (PB = 2·PJ bf16 per pixel) and, past the staged rows, the k-step
+  // table: tab[2·ks + hh] = the bf16 offset of step ks's 8 k of half hh (toff8 + j0), or -1
+  // for the K padding (zero operands)
+  const int PB = 2 * PJ;
+  bf16_t* Sb = reinterpret_cast<bf16_t*>(S);
+  int* tab = reinterpret_cast<int*>(S + (size_t)((kDgPx - 1) / g.W + 2 + (g.kh - 1) * g.dh) * SW * PJ);
+  stage_goff8_split(g, goff, b, y0, y1 - y0 + 1 + (g.kh - 1) * g.dh, SW, J8, PB, Sb);
+  if (threadIdx.x < 2 * NKS) {
+    const int k = 8 * (int)threadIdx.x;
+    const int t = k / J8, j0 = k - t * J8;
+    tab[threadIdx.x] = k < KT ? toff8(g, t, SW, PB) + j0 : -1;
+  }
+#else
   stage_goff8(g, goff, b, y0, y1 - y0 + 1 + (g.kh - 1) * g.dh, SW, J8, PJ, S);
+#endif
   __syncthreads();
+  BSTAMP(g_offd_stamps, bid, 1);
   const bool live = cw < g.C;  // (C < 256: idle waves still meet the epilogue barrier)
   int base[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int p = p0 + min(32 * u + r, np - 1);
     const int y = p / g.W, x = p - y * g.W;
+#if OFFD_PRESPLIT
+    base[u] = ((y - y0) * SW + x) * PB;
+#else
     base[u] = ((y - y0) * SW + x) * PJ;
+#endif
   }
   f32x16 acc[2][2];
 #pragma unroll
@@ -1567,6 +1652,36 @@ __global__ __launch_bounds__(256, 3) void offset_dgrad_bf16(Geo g, const bf16_t*
       const int ks = ks0 + d;
       lda(ks + kPf - 1, (d + kPf - 1) % kPf);
       __builtin_amdgcn_sched_barrier(0);
+#if OFFD_PRESPLIT
+      if (ks < NKS) {  // wave-uniform
+        const int e = tab[2 * ks + hh];
+        bf16x8_t bh[2], bl[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const bf16_t* sp = Sb + base[u] + max(e, 0);
+          bh[u] = *reinterpret_cast<const bf16x8_t*>(sp);
+          bl[u] = *reinterpret_cast<const bf16x8_t*>(sp + J8);
+        }
+        if (16 * ks + 16 > KT) {  // wave-uniform: only the last step can hold K padding
+          const unsigned keep = e >= 0 ? 0xffffffffu : 0u;
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            uint4 h = __builtin_bit_cast(uint4, bh[u]), l = __builtin_bit_cast(uint4, bl[u]);
+            h.x &= keep, h.y &= keep, h.z &= keep, h.w &= keep;
+            l.x &= keep, l.y &= keep, l.z &= keep, l.w &= keep;
+            bh[u] = __builtin_bit_cast(bf16x8_t, h);
+            bl[u] = __builtin_bit_cast(bf16x8_t, l);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra0[d], bh[u], acc[0][u], 0, 0, 0);
+          acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra1[d], bh[u], acc[1][u], 0, 0, 0);
+          acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra0[d], bl[u], acc[0][u], 0, 0, 0);
+          acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra1[d], bl[u], acc[1][u], 0, 0, 0);
+        }
+      }
+#else
       if (ks < NKS) {  // wave-uniform
         const int k = 16 * ks + 8 * hh;  // this lane's 8 k: one tap, channels j0..j0+7
         const bool kin = k < KT;  // the K padding step: zero operands (Wc is 0 there too)
@@ -1592,12 +1707,14 @@ __global__ __launch_bounds__(256, 3) void offset_dgrad_bf16(Geo g, const bf16_t*
           acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra1[d], bl[u], acc[1][u], 0, 0, 0);
         }
       }
+#endif
     }
   }
   // ∂x = the sampling route (channels-last gxT_in) + D, as bf16 NCHW. gxT_in is read as
   // whole 256-B pixel rows (this wave's 64 channels) into LDS and read back per D lane
   // (pixel r, channel of register i); the bf16 stores are 64-B pixel runs per channel.
   __syncthreads();  // every wave is done with S: its space holds the transposes
+  BSTAMP(g_offd_stamps, bid, 2);
   if (!live) return;
   float* T = S + w * 32 * kDgTP;
   const auto rgx = __builtin_amdgcn_make_buffer_rsrc(gx + (size_t)b * g.C * g.HWi, 0,
@@ -1605,10 +1722,29 @@ __global__ __launch_bounds__(256, 3) void offset_dgrad_bf16(Geo g, const bf16_t*
   const auto rgt = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(gxT_in + (size_t)b * g.HWi * g.C), 0, (int)((size_t)g.HWi * g.C * 4),
       0x00020000);
+#if OFFD_EPI
+  // r05: both halves' 16 gxT loads in flight together (the r04 order waited four times)
+  float4 tva[2][2][4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int pl = min(32 * u + 4 * (4 * h2 + it) + (lane >> 4), np - 1);
+        const auto q = __builtin_amdgcn_raw_buffer_load_b128(
+            rgt, (unsigned)(((p0 + pl) * g.C + cw + 4 * (lane & 15)) * 4), 0, 0);
+        tva[u][h2][it] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]),
+                                     __uint_as_float(q[2]), __uint_as_float(q[3]));
+      }
+#endif
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
 #pragma unroll
     for (int h2 = 0; h2 < 2; ++h2) {
+#if OFFD_EPI
+      const float4(&tv)[4] = tva[u][h2];
+#else
       float4 tv[4];
 #pragma unroll
       for (int it = 0; it < 4; ++it) {
@@ -1618,6 +1754,7 @@ __global__ __launch_bounds__(256, 3) void offset_dgrad_bf16(Geo g, const bf16_t*
         tv[it] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]),
                              __uint_as_float(q[3]));
       }
+#endif
 #pragma unroll
       for (int it = 0; it < 4; ++it)
         *reinterpret_cast<float4*>(T + (4 * (4 * h2 + it) + (lane >> 4)) * kDgTP + 4 * (lane & 15)) = tv[it];
@@ -1641,6 +1778,7 @@ __global__ __launch_bounds__(256, 3) void offset_dgrad_bf16(Geo g, const bf16_t*
     }
     __builtin_amdgcn_wave_barrier();  // the next half overwrites T
   }
+  BSTAMP(g_offd_stamps, bid, 3);
 }
 
 // ∂w_off partials: block = (chunk of rowsB input rows of one image, 64 channels); wave w
@@ -1675,7 +1813,11 @@ __global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __
     const int kk = 32 * (w + 4 * u) + r;
     const bool kok = kk < KT;
     const int t = kk / J8, j = kk - t * J8;
+#if OFFW_PRESPLIT
+    kofs[u] = kok ? toff8(g, t, SW, 2 * PJ) + j : 0;  // bf16 units of the pre-split records
+#else
     kofs[u] = kok ? toff8(g, t, SW, PJ) + j : 0;
+#endif
     kmask[u] = kok ? 0xffffffffu : 0u;
   }
   // the block sums cpb consecutive chunks (of any images) into one partial: fewer partial
@@ -1708,9 +1850,17 @@ __global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __
   };
 #pragma unroll
   for (int d = 0; d < kPf - 1; ++d) lda(d, d);
+  if (ci == 0) BSTAMP(g_offw_stamps, blockIdx.y * gridDim.x + blockIdx.x, 0);
+  if (ci == 1) BSTAMP(g_offw_stamps, blockIdx.y * gridDim.x + blockIdx.x, 2);
   if (ci > 0) __syncthreads();  // the previous chunk's staged rows are no longer read
+#if OFFW_PRESPLIT
+  stage_goff8_split<OFFW_SG>(g, goff, b, y0, nrows + (g.kh - 1) * g.dh, SW, J8, 2 * PJ,
+                             reinterpret_cast<bf16_t*>(S));
+#else
   stage_goff8<OFFW_SG>(g, goff, b, y0, nrows + (g.kh - 1) * g.dh, SW, J8, PJ, S);
+#endif
   __syncthreads();
+  if (ci < 2) BSTAMP(g_offw_stamps, blockIdx.y * gridDim.x + blockIdx.x, 1 + 2 * ci);
   // (row, column) in the chunk of this lane's first pixel q = 16i + 8hh: q and W are
   // multiples of 4, so pixels q..q+3 share a row, as do q+4..q+7
   int yq = (8 * hh) / g.W, xq = 8 * hh - yq * g.W;
@@ -1724,6 +1874,37 @@ __global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __
         const int q = 16 * i + 8 * hh;
         // pixels past the chunk read a staged row in range (S[0..]) and are masked to zero
         const bool ok0 = q < npx, ok1 = q + 4 < npx;
+#if OFFW_PRESPLIT
+        // r05: pre-split records (stage_goff8_split), so the step only gathers bf16 pairs:
+        // 64 -> ~20 VALU per step. The padding K columns (kmask) need no zeroing here: their
+        // accumulator columns are never stored, and MFMA columns do not mix.
+        const int PB = 2 * PJ;
+        const unsigned short* Sb = reinterpret_cast<const unsigned short*>(S);
+        const int s0 = ok0 ? (yq * SW + xq) * PB : 0;
+        const int s1 = !ok1 ? 0 : xq + 4 < g.W ? s0 + 4 * PB : (yq + 1) * SW * PB;
+        bf16x8_t bh[2], bl[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          uint4 hq, lq;
+          const unsigned short* a0 = Sb + s0 + kofs[u];
+          const unsigned short* a1 = Sb + s1 + kofs[u];
+          hq.x = (unsigned)a0[0] | ((unsigned)a0[PB] << 16);
+          hq.y = (unsigned)a0[2 * PB] | ((unsigned)a0[3 * PB] << 16);
+          hq.z = (unsigned)a1[0] | ((unsigned)a1[PB] << 16);
+          hq.w = (unsigned)a1[2 * PB] | ((unsigned)a1[3 * PB] << 16);
+          lq.x = (unsigned)a0[J8] | ((unsigned)a0[PB + J8] << 16);
+          lq.y = (unsigned)a0[2 * PB + J8] | ((unsigned)a0[3 * PB + J8] << 16);
+          lq.z = (unsigned)a1[J8] | ((unsigned)a1[PB + J8] << 16);
+          lq.w = (unsigned)a1[2 * PB + J8] | ((unsigned)a1[3 * PB + J8] << 16);
+          if (16 * i + 16 > npx) {  // wave-uniform: only a chunk's last step can be ragged
+            const unsigned m0 = ok0 ? 0xffffffffu : 0u, m1 = ok1 ? 0xffffffffu : 0u;
+            hq.x &= m0, hq.y &= m0, hq.z &= m1, hq.w &= m1;
+            lq.x &= m0, lq.y &= m0, lq.z &= m1, lq.w &= m1;
+          }
+          bh[u] = __builtin_bit_cast(bf16x8_t, hq);
+          bl[u] = __builtin_bit_cast(bf16x8_t, lq);
+        }
+#else
         const int s0 = ok0 ? (yq * SW + xq) * PJ : 0;
         const int s1 = !ok1 ? 0 : xq + 4 < g.W ? s0 + 4 * PJ : (yq + 1) * SW * PJ;
         const unsigned m0 = ok0 ? 0xffffffffu : 0u, m1 = ok1 ? 0xffffffffu : 0u;
@@ -1739,6 +1920,7 @@ __global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __
           }
           split8(v, bh[u], bl[u]);
         }
+#endif
         xq += 16;
         while (xq >= g.W) xq -= g.W, ++yq;
 #pragma unroll
@@ -1752,6 +1934,7 @@ __global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __
     }
   }
   }  // chunks
+  BSTAMP(g_offw_stamps, blockIdx.y * gridDim.x + blockIdx.x, 4);
   // partials in MFMA fragment order (each lane's 16 accumulators are 64 contiguous bytes,
   // a wave's tile one 4 KiB run): part[(((chunk·CG + cg)·NT + tile)·2 + m)·64 + lane][16]
   // with NT = ceil(KT/32) tiles; wgrad_frag_reduce folds the chunks and scatters to ∂w_off
@@ -1772,6 +1955,7 @@ __global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __
                         acc[m][u][4 * q + 3]);
     }
   }
+  BSTAMP(g_offw_stamps, blockIdx.y * gridDim.x + blockIdx.x, 5);
 }
 
 // ∂w_off[j][c][t] = Σ_chunk (fragment-ordered partials of offset_wgrad_bf16), chunks in
@@ -1815,7 +1999,8 @@ static size_t wgrad_frag_part_floats(const Geo& g, const MfmaStage& ms) {
 static void bwd_bf16_lds(const Geo& g, const MfmaStage& ms, size_t* lds_w, size_t* lds_x) {
   const size_t row = (size_t)ms.SW * pj8(g.J) * sizeof(float);
   *lds_w = (size_t)(ms.rowsB + (g.kh - 1) * g.dh) * row;
-  *lds_x = std::max((size_t)ms.SRx * row, (size_t)4 * 32 * kDgTP * sizeof(float));
+  // (+ offset_dgrad_bf16's k-step table past the staged rows: 2 ints per step, <= 16 steps)
+  *lds_x = std::max((size_t)ms.SRx * row + 32 * sizeof(int), (size_t)4 * 32 * kDgTP * sizeof(float));
 }
 bool offset_bwd_bf16_ok(const Geo& g) {
   MfmaStage ms;
@@ -2571,6 +2756,14 @@ extern "C" int dcn_debug_offc_stamps(unsigned long long* host, int n) {
   if (n > dcn::kOStampWg) n = dcn::kOStampWg;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(dcn::g_offc_stamps),
                              sizeof(unsigned long long) * dcn::kOStamps * n, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+// which: 0 = the folding forward, 1 = offset_dgrad_bf16, 2 = offset_wgrad_bf16
+extern "C" int dcn_debug_offc_stamps2(int which, unsigned long long* host, int n) {
+  if (n > dcn::kOStampWg) n = dcn::kOStampWg;
+  const void* sym = which == 1 ? HIP_SYMBOL(dcn::g_offd_stamps)
+                  : which == 2 ? HIP_SYMBOL(dcn::g_offw_stamps) : HIP_SYMBOL(dcn::g_offc_stamps);
+  return hipMemcpyFromSymbol(host, sym, sizeof(unsigned long long) * dcn::kOStamps * n, 0,
                              hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -500,6 +500,9 @@ static bool xpose_f4_ok(const float* in, const float* out, int C, int P) {
 // folded over the 8 lanes of its channel row by a fixed xor tree, one partial per (block,
 // channel) in tsum[c][image·gridDim.x + blockIdx.x] (r05: ∂b and the transpose were two passes
 // over ∂out, 9.2 + 13.7 us at config 4).
+#ifndef XB_ALL
+#define XB_ALL 1
+#endif
 constexpr int kXbSub = 4;
 static int xpose_b8_blocks_x(int P) { return (P + 64 * kXbSub - 1) / (64 * kXbSub); }
 
@@ -521,6 +524,29 @@ __global__ __launch_bounds__(256) void xpose_b8(const bf16_t* __restrict__ in,
   const int tid = threadIdx.x, lr = tid >> 3, lq = tid & 7;
   const int pb = blockIdx.x * 64 * kXbSub;
   const int nsub = min(kXbSub, (P - pb + 63) / 64);
+#if XB_ALL
+  // r05: every sub-tile's loads in flight from the start (through a buffer resource: pixels
+  // past P read zeros); one tile ahead waited a memory latency per tile
+  const auto rin = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(ib), 0,
+                                                     (int)((size_t)C * P * 2), 0x00020000);
+  uint4 ra[kXbSub][2];
+#pragma unroll
+  for (int sb = 0; sb < kXbSub; ++sb) {
+    const int p = pb + 64 * sb + 8 * lq;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const unsigned o = p < P && sb < nsub ? (unsigned)(((c0 + lr + 32 * k) * P + p) * 2) : 0x80000000u;
+      const auto q = __builtin_amdgcn_raw_buffer_load_b128(rin, o, 0, 0);
+      ra[sb][k] = make_uint4(q[0], q[1], q[2], q[3]);
+    }
+  }
+  float cs[2] = {0.f, 0.f};
+#pragma unroll
+  for (int sub = 0; sub < kXbSub; ++sub) {
+    if (sub >= nsub) break;  // block-uniform
+    const int p0 = pb + 64 * sub;
+    const uint4(&r)[2] = ra[sub];
+#else
   uint4 r[2];
   auto load = [&](int p0) {
     const int p = p0 + 8 * lq;
@@ -533,6 +559,7 @@ __global__ __launch_bounds__(256) void xpose_b8(const bf16_t* __restrict__ in,
   load(pb);
   for (int sub = 0; sub < nsub; ++sub) {
     const int p0 = pb + 64 * sub;
+#endif
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       unsigned* row = reinterpret_cast<unsigned*>(&t[lr + 32 * k][8 * lq]);
@@ -540,7 +567,9 @@ __global__ __launch_bounds__(256) void xpose_b8(const bf16_t* __restrict__ in,
       if (SUMS) cs[k] += sum8_bf16(r[k]);  // zeros past P
     }
     __syncthreads();
+#if !XB_ALL
     if (sub + 1 < nsub) load(p0 + 64);  // in flight while this tile is written
+#endif
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int pr = lr + 32 * k, p = p0 + pr;
@@ -569,7 +598,9 @@ __global__ __launch_bounds__(256) void xpose_b8(const bf16_t* __restrict__ in,
 }
 
 static bool xpose_b8_ok(const bf16_t* in, const bf16_t* out, int C, int P) {
-  return P % 8 == 0 && C % 64 == 0 && ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0;
+  // (one image's C·P bf16 values are addressed through a buffer resource: 32-bit offsets)
+  return P % 8 == 0 && C % 64 == 0 && ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
+         (size_t)C * P * 2 < ((size_t)1 << 31);
 }
 
 // One wave per channel: lane l sums partials i ≡ l (mod 64) (all loads in flight
