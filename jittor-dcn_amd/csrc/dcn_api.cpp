@@ -18,6 +18,11 @@
 #include "dcn_host.h"
 #include "dcn_internal.h"
 
+// A/B: the bf16 offset backward's ∂x kernel on the side stream beside ∂W_off
+#ifndef OFFB_CONC
+#define OFFB_CONC 1
+#endif
+
 using dcn::Geo;
 
 namespace {
@@ -811,9 +816,15 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
     // bf16 grad_x directly (transpose of the sampling route + the offset-conv route)
     HIP_TRY(dcn::launch_offset_conv_bwd_bf16(g, x, w_off, goff32, F32(L.gxT), BF(L.wb16),
                                              F32(L.goffT), gx, F32(L.gwo32), F32(L.gbo32), st,
-                                             nullptr, nullptr, nullptr, true));
+#if OFFB_CONC
+                                             h->aux, h->fork_ev, h->join_ev,
+#else
+                                             nullptr, nullptr, nullptr,
+#endif
+                                             true));
     // (r02: the Wc swizzle and ∂b_off sums on the side stream beside ∂W_off measured slower,
-    // offset bwd 0.115 -> 0.121 ms at config 4: concurrent kernels slow each other)
+    // offset bwd 0.115 -> 0.121 ms at config 4: concurrent kernels slow each other; r05: the
+    // ∂x kernel there beside ∂W_off is faster, 0.0914-0.092 -> 0.0896-0.0901 ms, OFFB_CONC)
   } else if (dcn::offset_bwd_chunkable(g)) {
     // f32 MFMA on the bf16 xT (exact products of the bf16 values) and the fp32 ∂offset
     HIP_TRY(dcn::launch_offset_bwd_prep(g, F32(L.woff32), F32(L.wt), st));

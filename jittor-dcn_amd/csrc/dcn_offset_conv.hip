@@ -35,6 +35,11 @@
 // A/B (r05, config 4): the ∂W_off kernel on pre-split records gathered as bf16 pairs measured
 // 0.092-0.0926 ms for the offset backward against 0.0913-0.0916 on fp32 split in the loop
 // (its 32 two-byte LDS reads per step cost more than the split), so 0
+// r05 (config 4): the ∂x kernel on the side stream beside ∂W_off + its fold (they share
+// only their inputs): offset backward 0.0914-0.092 -> 0.0896-0.0901 ms
+#ifndef OFFB_CONC
+#define OFFB_CONC 1
+#endif
 #ifndef OFFW_PRESPLIT
 #define OFFW_PRESPLIT 0
 #endif
@@ -2058,11 +2063,20 @@ hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16
   const long E = (long)(g.C / 64) * ((KK * J8 + 31) / 32) * 2 * 1024;
   hipLaunchKernelGGL(wgrad_frag_reduce, dim3((unsigned)((E + 63) / 64)), dim3(1024), 0, s, g,
                      part, nblk, gw_off);
+#if OFFB_CONC
+  // (A/B) ∂x on the side stream, concurrent with ∂W_off + its fold on the main one
+  if (aux)
+    hipLaunchKernelGGL(offset_dgrad_bf16, dim3(g.B * ms.spi), dim3(256), lds_x, aux, g, wc, KT16,
+                       goff, gxT_in, gx, ms.spi);
+#endif
   if (aux) {
     e = hipEventRecord(join, aux);
     if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
     if (e != hipSuccess) return e;
   }
+#if OFFB_CONC
+  if (!aux)
+#endif
   hipLaunchKernelGGL(offset_dgrad_bf16, dim3(g.B * ms.spi), dim3(256), lds_x, s, g, wc, KT16, goff,
                      gxT_in, gx, ms.spi);
   return hipGetLastError();
