@@ -22,6 +22,12 @@
 #define OFFC_FOLD_SERIAL 0
 #endif
 // A/B switch: 1 = the r04 weight prefetch (one tap ahead, first tap after the staging)
+#ifndef OFFC_KF2
+#define OFFC_KF2 14
+#endif
+#ifndef OFFC_ROWS
+#define OFFC_ROWS 2
+#endif
 #ifndef OFFC_W1
 #define OFFC_W1 0
 #endif
@@ -1163,7 +1169,10 @@ __device__ unsigned long long g_offc_stamps[kOStampWg * kOStamps];
   do {            \
   } while (0)
 #endif
-template <int SPT, bool FOLD = false>
+// ROWS (FOLD only, r05): output rows per block; the window holds kh + ROWS - 1 input rows,
+// so x leaves L2 (kh + ROWS - 1) / ROWS times instead of kh times, and each weight fragment
+// loaded serves ROWS rows (config 4 measured the staging as the bandwidth-bound phase).
+template <int SPT, bool FOLD = false, int ROWS = 1>
 __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
     Geo g, const bf16_t* __restrict__ xT, const bf16_t* __restrict__ wb, int Cp,
     const float* __restrict__ b_off, float* __restrict__ off32, bf16_t* __restrict__ off,
@@ -1173,10 +1182,13 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const Block3 blk = xcd_block();
-  const int ho = blk.x / tpr, wo0 = (blk.x - ho * tpr) * 32, b = blk.z;
+  static_assert(ROWS == 1 || FOLD, "row blocks stage through the fold path");
+  const int hb = blk.x / tpr, wo0 = (blk.x - hb * tpr) * 32, b = blk.z;
+  const int ho = hb * ROWS;  // first output row
   const int r = lane & 31, hh = lane >> 5;
   const int KH = g.kh, KK = g.kh * g.kw;
-  bf16_t* L = reinterpret_cast<bf16_t*>(smem_row) + (size_t)w * KH * SWc * P;
+  const int KHR = KH + ROWS - 1;  // staged window rows
+  bf16_t* L = reinterpret_cast<bf16_t*>(smem_row) + (size_t)w * KHR * SWc * P;
   const int cw = w * SPT * 16;  // this wave's first channel
 #if OFFC_STAMP
   const int ostamp_wg = blk.z * gridDim.x + blk.x;
@@ -1192,19 +1204,22 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
 #pragma unroll
     for (int u = 0; u < SPT; ++u) rb[u] = ld_bf16x8(wp + 512 * u);
   };
-#if !OFFC_W1
-  ldb(0, bv[0]);
-  ldb(1, bv[1]);
-#endif
+  // (two-row blocks: one tap ahead, loaded after the staging — their 8 MFMAs per tap cover
+  // more of the L2 latency, and the registers are the occupancy limit)
+  constexpr bool kW1 = OFFC_W1 || ROWS > 1;
+  if constexpr (!kW1) {
+    ldb(0, bv[0]);
+    ldb(1, bv[1]);
+  }
   if constexpr (FOLD) {
     // zero the slice (image borders and the channel padding past C stay zero), then the
     // in-image part from NCHW rows: item = (channel pair, window row, 4-pixel chunk), two
     // 8-B loads (channels c, c+1) -> four 32-bit LDS stores of (c, c+1) per pixel
-    const int nz = KH * SWc * P / 8;
+    const int nz = KHR * SWc * P / 8;
     for (int i = lane; i < nz; i += 64) reinterpret_cast<uint4*>(L)[i] = make_uint4(0u, 0u, 0u, 0u);
     __builtin_amdgcn_wave_barrier();
     const int NQ = g.W / 4, x0 = -g.pw;  // wo0 == 0 (tpr == 1)
-    const int nit = 8 * SPT * KH * NQ;
+    const int nit = 8 * SPT * KHR * NQ;
 #if OFFC_FOLD_SERIAL
     const bf16_t* xb = x_nchw + (size_t)b * g.C * g.HWi;
     for (int it = lane; it < nit; it += 64) {
@@ -1233,8 +1248,8 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
         (int)((size_t)g.C * g.HWi * 2), 0x00020000);
     // quotients by NQ and KH as umulhi by ceil(2^32/d), exact here (it < 2^16); d = 1 wraps
     // that multiplier to 0 and is taken apart
-    const unsigned mq = 0xffffffffu / (unsigned)NQ + 1u, mk = 0xffffffffu / (unsigned)KH + 1u;
-    constexpr int kF = 12;
+    const unsigned mq = 0xffffffffu / (unsigned)NQ + 1u, mk = 0xffffffffu / (unsigned)KHR + 1u;
+    constexpr int kF = ROWS == 1 ? 12 : OFFC_KF2;
     for (int it0 = lane; it0 < nit; it0 += 64 * kF) {
       uint2 u0[kF], u1[kF];
       int dst[kF];
@@ -1242,7 +1257,7 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
       for (int u = 0; u < kF; ++u) {
         const int it = min(it0 + 64 * u, nit - 1);
         const int rest = NQ == 1 ? it : (int)__umulhi((unsigned)it, mq), q = it - rest * NQ;
-        const int cp = KH == 1 ? rest : (int)__umulhi((unsigned)rest, mk), i = rest - cp * KH;
+        const int cp = KHR == 1 ? rest : (int)__umulhi((unsigned)rest, mk), i = rest - cp * KHR;
         const int y = ho - g.ph + i, c = cw + 2 * cp;
         const bool ok = y >= 0 && y < g.H && c < g.C;
         const unsigned o = ok ? (unsigned)(((c * g.H + y) * g.W + 4 * q) * 2) : 0x80000000u;
@@ -1266,14 +1281,19 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
 #endif
     __builtin_amdgcn_wave_barrier();
     OSTAMP(1);
-    // input row ho (window row ph) -> xT[b][ho][px][cw ..]: 16-B runs of 8 channels
-    const int ir = g.ph;
+    // input rows ho.. (window rows ph..) -> xT[b][ho][px][cw ..]: 16-B runs of 8 channels
     const int nch = min(16 * SPT, g.C - cw);
-    for (int it = lane; it < g.W * (16 * SPT / 8); it += 64) {
-      const int ch8 = it % (16 * SPT / 8), px = it / (16 * SPT / 8);
-      if (8 * ch8 >= nch) continue;
-      const uint4 v = *reinterpret_cast<const uint4*>(L + (ir * SWc + px - x0) * P + 8 * ch8);
-      *reinterpret_cast<uint4*>(xT_out + (((size_t)b * g.H + ho) * g.W + px) * g.C + cw + 8 * ch8) = v;
+#pragma unroll
+    for (int rr = 0; rr < ROWS; ++rr) {
+      if (ho + rr >= g.H) break;  // block-uniform
+      const int ir = g.ph + rr;
+      for (int it = lane; it < g.W * (16 * SPT / 8); it += 64) {
+        const int ch8 = it % (16 * SPT / 8), px = it / (16 * SPT / 8);
+        if (8 * ch8 >= nch) continue;
+        const uint4 v = *reinterpret_cast<const uint4*>(L + (ir * SWc + px - x0) * P + 8 * ch8);
+        *reinterpret_cast<uint4*>(xT_out + (((size_t)b * g.H + ho + rr) * g.W + px) * g.C + cw +
+                                  8 * ch8) = v;
+      }
     }
     OSTAMP(2);
   } else {
@@ -1308,31 +1328,36 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
   // the wave reads only its own slice: LDS ops of one wave run in order, so only the
   // compiler must keep the reads below the writes
   __builtin_amdgcn_wave_barrier();
-  f32x16 acc;
+  f32x16 acc[ROWS];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  for (int rr = 0; rr < ROWS; ++rr)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[rr][i] = 0.f;
   // lanes past the row's last pixel (Wo < 32) read the last pixel's window (discarded)
   const int rc = min(r, (SWc - 1 - (g.kw - 1) * g.dw) / g.sw);
   auto mma = [&](int t, const bf16x8_t(&rb)[SPT]) {
     const int i = t / g.kw, k = t - i * g.kw;
-    const bf16_t* ap = L + (i * SWc + rc * g.sw + k * g.dw) * P + 8 * hh;
-    bf16x8_t a[SPT];
 #pragma unroll
-    for (int u = 0; u < SPT; ++u) a[u] = ld_bf16x8(ap + 16 * u);
+    for (int rr = 0; rr < ROWS; ++rr) {
+      const bf16_t* ap = L + ((i + rr) * SWc + rc * g.sw + k * g.dw) * P + 8 * hh;
+      bf16x8_t a[SPT];
 #pragma unroll
-    for (int u = 0; u < SPT; ++u)
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[u], rb[u], acc, 0, 0, 0);
+      for (int u = 0; u < SPT; ++u) a[u] = ld_bf16x8(ap + 16 * u);
+#pragma unroll
+      for (int u = 0; u < SPT; ++u)
+        acc[rr] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[u], rb[u], acc[rr], 0, 0, 0);
+    }
   };
-#if OFFC_W1
-  ldb(0, bv[0]);
-  for (int t = 0; t < KK; t += 2) {
-    ldb(t + 1, bv[1]);
-    mma(t, bv[0]);
-    if (t + 1 >= KK) break;
-    ldb(t + 2, bv[0]);
-    mma(t + 1, bv[1]);
-  }
-#else
+  if constexpr (kW1) {
+    ldb(0, bv[0]);
+    for (int t = 0; t < KK; t += 2) {
+      ldb(t + 1, bv[1]);
+      mma(t, bv[0]);
+      if (t + 1 >= KK) break;
+      ldb(t + 2, bv[0]);
+      mma(t + 1, bv[1]);
+    }
+  } else {
   for (int t = 0; t < KK; t += 3) {
     ldb(t + 2, bv[2]);
     mma(t, bv[0]);
@@ -1343,28 +1368,49 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
     ldb(t + 4, bv[1]);
     mma(t + 2, bv[2]);
   }
-#endif
+  }
   // fold the 4 channel partials in wave order through the (now free) window LDS
   __syncthreads();
   OSTAMP(3);
   f32x16* red = reinterpret_cast<f32x16*>(smem_row);
-  if (w > 0) red[(w - 1) * 64 + lane] = acc;
-  __syncthreads();
-  OSTAMP(4);
-  if (w != 0) return;
+  f32x16 sum;
+  if constexpr (ROWS == 1) {
+    if (w > 0) red[(w - 1) * 64 + lane] = acc[0];
+    __syncthreads();
+    OSTAMP(4);
+    if (w != 0) return;
+    sum = acc[0];
 #pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    const f32x16 o = red[q * 64 + lane];
+    for (int q = 0; q < 3; ++q) {
+      const f32x16 o = red[q * 64 + lane];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] += o[i];
+      for (int i = 0; i < 16; ++i) sum[i] += o[i];
+    }
+  } else {
+    // every wave's partial of row rr at red[rr][w]; wave rr folds its row in wave order
+    // (((w0 + w1) + w2) + w3: the ROWS = 1 order, same bits)
+#pragma unroll
+    for (int rr = 0; rr < ROWS; ++rr) red[(rr * 4 + w) * 64 + lane] = acc[rr];
+    __syncthreads();
+    OSTAMP(4);
+    if (w >= ROWS || ho + w >= g.Ho) return;
+    sum = red[(w * 4) * 64 + lane];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+      const f32x16 o = red[(w * 4 + q) * 64 + lane];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sum[i] += o[i];
+    }
   }
-  float(*T)[33] = reinterpret_cast<float(*)[33]>(smem_row + 3 * 64 * sizeof(f32x16));
+  const int rw = ROWS == 1 ? 0 : w;  // the output row this wave writes (ho + rw)
+  float(*T)[33] = reinterpret_cast<float(*)[33]>(smem_row + 4 * ROWS * 64 * sizeof(f32x16) +
+                                                  (size_t)rw * 32 * 33 * sizeof(float));
   const float bj = r < g.J ? b_off[r] : 0.f;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) T[r][(i & 3) + 8 * (i >> 2) + 4 * hh] = bf2f(f2bf(acc[i] + bj));
+  for (int i = 0; i < 16; ++i) T[r][(i & 3) + 8 * (i >> 2) + 4 * hh] = bf2f(f2bf(sum[i] + bj));
   __builtin_amdgcn_wave_barrier();
   if (wo0 + r < g.Wo) {
-    const int pp = ho * g.Wo + wo0 + r;
+    const int pp = (ho + rw) * g.Wo + wo0 + r;
     for (int j = hh; j < g.J; j += 2) {
       const float v = T[j][r];
       const size_t o = ((size_t)b * g.J + j) * g.HW + pp;
@@ -1376,13 +1422,14 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
 }
 
 // LDS bytes of offset_conv_fwd_mfma_bf16_row (0: the row kernel does not apply)
-static size_t fwd_bf16_row_lds(const Geo& g, int* SWc) {
+static size_t fwd_bf16_row_lds(const Geo& g, int* SWc, int rows = 1) {
   if (g.Wo < 16) return 0;
   const int spt = (g.C + 63) / 64;
   *SWc = (std::min(32, g.Wo) - 1) * g.sw + (g.kw - 1) * g.dw + 1;
-  const size_t win = (size_t)4 * g.kh * *SWc * (16 * spt + 8) * 2;
-  const size_t need = std::max(win, (size_t)3 * 64 * 64 + 32 * 33 * 4);
-  return need <= 64 * 1024 ? need : 0;
+  const size_t win = (size_t)4 * (g.kh + rows - 1) * *SWc * (16 * spt + 8) * 2;
+  // the partial fold: 4 waves' 64-B fragments per row, then one 32x33 fp32 tile per row
+  const size_t need = std::max(win, (size_t)rows * (4 * 64 * 64 + 32 * 33 * 4));
+  return need <= (rows == 1 ? 64 : 128) * 1024 ? need : 0;
 }
 
 bool offset_fwd_mfma_bf16_ok(const Geo& g) {
@@ -1427,6 +1474,27 @@ hipError_t launch_offset_conv_fwd_bf16(const Geo& g, const bf16_t* xT, const bf1
                          x_nchw, const_cast<bf16_t*>(xT));
     };
     if (x_nchw) {  // f3: x read once, xT written by the same blocks
+      int SW2 = 0;
+      const size_t lds2 = OFFC_ROWS > 1 ? fwd_bf16_row_lds(g, &SW2, OFFC_ROWS) : 0;
+      if (lds2) {  // OFFC_ROWS output rows per block (tpr == 1 on the fold path)
+        const dim3 grid2((g.Ho + OFFC_ROWS - 1) / OFFC_ROWS, 1, g.B);
+        auto go2 = [&](auto kern) -> hipError_t {
+          if (lds2 > 64 * 1024) {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)lds2);
+            if (e != hipSuccess) return e;
+          }
+          hipLaunchKernelGGL(kern, grid2, dim3(256), lds2, s, g, xT, wb, Cp, b_off, off32, off,
+                             tpr, SW2, x_nchw, const_cast<bf16_t*>(xT));
+          return hipGetLastError();
+        };
+        constexpr int R = OFFC_ROWS > 1 ? OFFC_ROWS : 2;
+        if (spt == 1) return go2(offset_conv_fwd_mfma_bf16_row<1, true, R>);
+        if (spt == 2) return go2(offset_conv_fwd_mfma_bf16_row<2, true, R>);
+        if (spt == 3) return go2(offset_conv_fwd_mfma_bf16_row<3, true, R>);
+        return go2(offset_conv_fwd_mfma_bf16_row<4, true, R>);
+      }
       if (spt == 1) go(offset_conv_fwd_mfma_bf16_row<1, true>);
       else if (spt == 2) go(offset_conv_fwd_mfma_bf16_row<2, true>);
       else if (spt == 3) go(offset_conv_fwd_mfma_bf16_row<3, true>);
