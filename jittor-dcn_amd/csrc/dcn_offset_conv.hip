@@ -57,6 +57,9 @@
 #ifndef OFFD_EPI
 #define OFFD_EPI 0
 #endif
+#ifndef OFFW_SB
+#define OFFW_SB 1
+#endif
 #ifndef OFFW_PF
 #define OFFW_PF 3
 #endif
@@ -1942,7 +1945,9 @@ __global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __
     for (int d = 0; d < kPf; ++d) {
       const int i = i0 + d;
       lda(i + kPf - 1, (d + kPf - 1) % kPf);
+#if OFFW_SB
       __builtin_amdgcn_sched_barrier(0);
+#endif
       if (i < nsteps) {  // wave-uniform
         const int q = 16 * i + 8 * hh;
         // pixels past the chunk read a staged row in range (S[0..]) and are masked to zero
