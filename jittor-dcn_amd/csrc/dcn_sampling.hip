@@ -644,15 +644,22 @@ __global__ __launch_bounds__(kBinT) void bins_chunk_sort(Geo g, const float* __r
 // pass 1 sums each bin over the chunks, a block scan over the bins gives start[bin], pass 2
 // replaces H[c][bin] by start[bin] + the runs of the earlier chunks. Bins beyond 4096 are
 // handled in rounds, carrying the running total.
-__global__ __launch_bounds__(1024) void bins_scan_table(int NB, int nch, int* __restrict__ H,
-                                                        int* __restrict__ start) {
-  __shared__ int wsum[17];  // exclusive wave prefixes, then the block total
+// (r05: the block size is a template parameter; BINS_SCAN_T picks it: a smaller block fits
+// beside the ∂W GEMM workgroups it runs next to on the side stream)
+#ifndef BINS_SCAN_T
+#define BINS_SCAN_T 1024
+#endif
+template <int T = 1024>
+__global__ __launch_bounds__(T) void bins_scan_table(int NB, int nch, int* __restrict__ H,
+                                                     int* __restrict__ start) {
+  constexpr int NW = T / 64;
+  __shared__ int wsum[NW + 1];  // exclusive wave prefixes, then the block total
   const int bg = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int NBp = bins_nbp(NB);
   int* Hs = H + (size_t)bg * nch * NBp;
   int* st = start + (size_t)bg * (NB + 1);
   int carry = 0;
-  for (int b0 = 0; b0 < NBp; b0 += 4096) {
+  for (int b0 = 0; b0 < NBp; b0 += 4 * T) {
     const int bb = b0 + 4 * tid;
     const bool act = bb < NBp;
     int4 tot = make_int4(0, 0, 0, 0);
@@ -673,16 +680,16 @@ __global__ __launch_bounds__(1024) void bins_scan_table(int NB, int nch, int* __
     __syncthreads();
     if (tid == 0) {
       int acc = 0;
-      for (int i = 0; i < 16; ++i) {
+      for (int i = 0; i < NW; ++i) {
         const int t = wsum[i];
         wsum[i] = acc;
         acc += t;
       }
-      wsum[16] = acc;
+      wsum[NW] = acc;
     }
     __syncthreads();
     const int e = carry + v - local + wsum[wv];
-    carry += wsum[16];
+    carry += wsum[NW];
     int run[4] = {e, e + tot.x, e + tot.x + tot.y, e + tot.x + tot.y + tot.z};
     if (act) {
 #pragma unroll
@@ -1617,7 +1624,8 @@ hipError_t launch_bins(const Geo& g, const float* off, void* bins_ws, float* gof
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(bins_chunk_sort, dim3(nch, (unsigned)seg), dim3(kBinT), 0, s, g, off, b0, nch,
                      NB, kbits, P.H, P.R, P.sorted, fused ? nullptr : P.rec);
-  hipLaunchKernelGGL(bins_scan_table, dim3((unsigned)seg), dim3(1024), 0, s, NB, nch, P.H, P.start);
+  hipLaunchKernelGGL(bins_scan_table<BINS_SCAN_T>, dim3((unsigned)seg), dim3(BINS_SCAN_T), 0, s, NB,
+                     nch, P.H, P.start);
   hipLaunchKernelGGL(bins_emit, dim3((NB + 255) / 256, (unsigned)seg), dim3(256), 0, s, g, nch, NB,
                      P.H, P.R, P.start, P.sorted, fused ? P.brec : nullptr, P.slist);
   if (fused) {
