@@ -23,7 +23,7 @@ for _ in range(3):
 fn = h.lib.dcn_debug_offc_stamps2
 fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
 KERNELS = [
-    ("forward", 64 * 28, ["window staged", "xT row written", "k loop + barrier", "fold barrier",
+    ("forward", 64 * 14, ["window staged", "xT row written", "k loop + barrier", "fold barrier",
                           "epilogue"]),
     ("dgrad", 64 * 13, ["goff staged", "k loop + barrier", "epilogue"]),
     ("wgrad", 128 * 4, ["staged 0", "chunk 0 steps", "staged 1", "chunk 1 steps", "partials"]),
