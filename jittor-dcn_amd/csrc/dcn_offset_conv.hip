@@ -57,6 +57,11 @@
 #ifndef OFFD_EPI
 #define OFFD_EPI 0
 #endif
+// r05 (config 4): two channel groups per ∂W_off workgroup, offset backward 0.0921-0.0933 ->
+// 0.0899-0.0908 ms (the shared ∂offset staging is half the instructions per channel)
+#ifndef OFFW_CGB
+#define OFFW_CGB 2
+#endif
 #ifndef OFFW_SB
 #define OFFW_SB 1
 #endif
@@ -1860,7 +1865,10 @@ __global__ __launch_bounds__(256, 3) void offset_dgrad_bf16(Geo g, const bf16_t*
 // ∂w_off partials: block = (chunk of rowsB input rows of one image, 64 channels); wave w
 // owns N-tiles w and w+4 of the KT16/32 (t, j) tiles x both 32-channel M-tiles.
 // part[chunk][c][j·KK + t] (the f32 kernel's format: wgrad_mfma_reduce folds it).
-__global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __restrict__ x,
+// CGB (r05): 64-channel groups per workgroup (4 waves each) sharing one staging of the
+// ∂offset rows (the staging was instruction-bound, a third of the workgroup's time)
+template <int CGB = 1>
+__global__ __launch_bounds__(256 * CGB) void offset_wgrad_bf16(Geo g, const bf16_t* __restrict__ x,
                                                         const float* __restrict__ goff,
                                                         float* __restrict__ part, int rowsB,
                                                         int cpi, int cpb) {
@@ -1868,9 +1876,10 @@ __global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __
   const int J8 = j8(g.J), KK = g.kh * g.kw, KT = KK * J8;
   const int SW = g.W + (g.kw - 1) * g.dw;
   const int PJ = pj8(g.J);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = (threadIdx.x >> 6) & 3, cgl = threadIdx.x >> 8;
   const int r = lane & 31, hh = lane >> 5;
-  const int cb = blockIdx.y * 64;
+  const int cgi = blockIdx.y * CGB + cgl;  // this wave's 64-channel group
+  const int cb = cgi * 64;
   const int nchunk = g.B * cpi;
   f32x16 acc[2][2];
 #pragma unroll
@@ -2024,7 +2033,7 @@ __global__ __launch_bounds__(256) void offset_wgrad_bf16(Geo g, const bf16_t* __
     if (tile >= NT) continue;  // wave-uniform
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
-      float* pp = part + (((((size_t)blockIdx.x * CG + blockIdx.y) * NT + tile) * 2 + m) * 64 + lane) * 16;
+      float* pp = part + (((((size_t)blockIdx.x * CG + cgi) * NT + tile) * 2 + m) * 64 + lane) * 16;
       if (!kmask[u]) continue;  // a padding K column: the fold never reads it
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -2131,7 +2140,11 @@ hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16
   // chunks per workgroup (config 4: 1 -> 48 + 11 us, 2 -> 42 + 7, 4 -> 53 + 6 for ∂W_off + fold)
   const int cpb = 2;
   const int nblk = (g.B * ms.cpi + cpb - 1) / cpb;
-  hipLaunchKernelGGL(offset_wgrad_bf16, dim3(nblk, g.C / 64), dim3(256), lds_w, s, g, x, goff,
+  if (OFFW_CGB == 2 && (g.C / 64) % 2 == 0)
+    hipLaunchKernelGGL(offset_wgrad_bf16<2>, dim3(nblk, g.C / 128), dim3(512), lds_w, s, g, x, goff,
+                       part, ms.rowsB, ms.cpi, cpb);
+  else
+  hipLaunchKernelGGL(offset_wgrad_bf16<1>, dim3(nblk, g.C / 64), dim3(256), lds_w, s, g, x, goff,
                      part, ms.rowsB, ms.cpi, cpb);
   const long E = (long)(g.C / 64) * ((KK * J8 + 31) / 32) * 2 * 1024;
   hipLaunchKernelGGL(wgrad_frag_reduce, dim3((unsigned)((E + 63) / 64)), dim3(1024), 0, s, g,

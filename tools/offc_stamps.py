@@ -26,7 +26,7 @@ KERNELS = [
     ("forward", 64 * 14, ["window staged", "xT row written", "k loop + barrier", "fold barrier",
                           "epilogue"]),
     ("dgrad", 64 * 13, ["goff staged", "k loop + barrier", "epilogue"]),
-    ("wgrad", 128 * 4, ["staged 0", "chunk 0 steps", "staged 1", "chunk 1 steps", "partials"]),
+    ("wgrad", 128 * 2, ["staged 0", "chunk 0 steps", "staged 1", "chunk 1 steps", "partials"]),
 ]
 for which, (name, n, phases) in enumerate(KERNELS):
     buf = (ctypes.c_ulonglong * (n * 8))()
