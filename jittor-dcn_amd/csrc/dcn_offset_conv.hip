@@ -59,6 +59,9 @@
 #endif
 // r05 (config 4): two channel groups per ∂W_off workgroup, offset backward 0.0921-0.0933 ->
 // 0.0899-0.0908 ms (the shared ∂offset staging is half the instructions per channel)
+#ifndef STAGE_NOSC
+#define STAGE_NOSC 1
+#endif
 #ifndef OFFW_CGB
 #define OFFW_CGB 2
 #endif
@@ -559,7 +562,11 @@ __device__ __forceinline__ void stage_goff(const Geo& g, const float* __restrict
       const int j = (int)__umulhi((unsigned)idx, mp), rem = idx - j * plane;
       const int sr = (int)__umulhi((unsigned)rem, ms), sc = rem - sr * SW;
       const int ho = y0 + sr - (g.kh - 1) * g.dh + g.ph, wo = sc - (g.kw - 1) * g.dw + g.pw;
+#if STAGE_NOSC
+      const bool ok = ((unsigned)ho < (unsigned)g.Ho) & ((unsigned)wo < (unsigned)g.Wo);
+#else
       const bool ok = ho >= 0 && ho < g.Ho && wo >= 0 && wo < g.Wo;
+#endif
       const unsigned o = ok ? (unsigned)((j * g.HW + ho * g.Wo + wo) * 4) : 0x80000000u;
       v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o, 0, 0));
       dst[u] = rem * g.J + j;
@@ -1575,7 +1582,13 @@ __device__ __forceinline__ void stage_goff8(const Geo& g, const float* __restric
       const int j = (int)__umulhi((unsigned)idx, mp), rem = idx - j * plane;
       const int sr = (int)__umulhi((unsigned)rem, ms), sc = rem - sr * SW;
       const int ho = y0 + sr - (g.kh - 1) * g.dh + g.ph, wo = sc - (g.kw - 1) * g.dw + g.pw;
+#if STAGE_NOSC
+      // bitwise, not short-circuit: && made hipcc wrap every element's load in its own
+      // exec-masked branch (~29 instructions per element, r05)
+      const bool ok = (j < g.J) & ((unsigned)ho < (unsigned)g.Ho) & ((unsigned)wo < (unsigned)g.Wo);
+#else
       const bool ok = j < g.J && ho >= 0 && ho < g.Ho && wo >= 0 && wo < g.Wo;
+#endif
       const unsigned o = ok ? (unsigned)((j * g.HW + ho * g.Wo + wo) * 4) : 0x80000000u;
       v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o, 0, 0));
       dst[u] = rem * PJ + j;
@@ -1611,7 +1624,13 @@ __device__ __forceinline__ void stage_goff8_split(const Geo& g, const float* __r
       const int j = (int)__umulhi((unsigned)idx, mp), rem = idx - j * plane;
       const int sr = (int)__umulhi((unsigned)rem, ms), sc = rem - sr * SW;
       const int ho = y0 + sr - (g.kh - 1) * g.dh + g.ph, wo = sc - (g.kw - 1) * g.dw + g.pw;
+#if STAGE_NOSC
+      // bitwise, not short-circuit: && made hipcc wrap every element's load in its own
+      // exec-masked branch (~29 instructions per element, r05)
+      const bool ok = (j < g.J) & ((unsigned)ho < (unsigned)g.Ho) & ((unsigned)wo < (unsigned)g.Wo);
+#else
       const bool ok = j < g.J && ho >= 0 && ho < g.Ho && wo >= 0 && wo < g.Wo;
+#endif
       const unsigned o = ok ? (unsigned)((j * g.HW + ho * g.Wo + wo) * 4) : 0x80000000u;
       v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o, 0, 0));
       dst[u] = rem * PB + j;
