@@ -22,6 +22,11 @@
 #define OFFC_FOLD_SERIAL 0
 #endif
 // A/B switch: 1 = the r04 weight prefetch (one tap ahead, first tap after the staging)
+// r05 (config 4): two-row workgroups on the 3-tap weight ring, offset forward 0.0362-0.0369
+// -> 0.0338-0.0342 ms (one wave per SIMD at 296 registers, but no L2 wait per tap)
+#ifndef OFFC_RING2
+#define OFFC_RING2 1
+#endif
 #ifndef OFFC_KF2
 #define OFFC_KF2 14
 #endif
@@ -1221,8 +1226,9 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
   };
   // (two-row blocks: one tap ahead, loaded after the staging — their 8 MFMAs per tap cover
   // more of the L2 latency, and the registers are the occupancy limit)
-  constexpr bool kW1 = OFFC_W1 || ROWS > 1;
-  if constexpr (!kW1) {
+  // OFFC_RING2 (A/B): two-row workgroups on the 3-tap ring too, loaded after the staging
+  constexpr bool kW1 = OFFC_W1 || (ROWS > 1 && !OFFC_RING2);
+  if constexpr (!kW1 && ROWS == 1) {
     ldb(0, bv[0]);
     ldb(1, bv[1]);
   }
@@ -1339,6 +1345,10 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
       for (int u = 0; u < kU; ++u)
         if (dst[u] >= 0) *reinterpret_cast<uint4*>(L + dst[u]) = v[u];
     }
+  }
+  if constexpr (!kW1 && ROWS > 1) {
+    ldb(0, bv[0]);
+    ldb(1, bv[1]);
   }
   // the wave reads only its own slice: LDS ops of one wave run in order, so only the
   // compiler must keep the reads below the writes
