@@ -56,6 +56,11 @@
 #endif
 // r05 (config 4): the ∂x kernel on pre-split records, offset backward 0.0944-0.0951 ->
 // 0.092-0.0926 ms (k loop 11.3 -> 7.9 us per workgroup, tools/offc_stamps.py)
+// ∂x kernel: Wc fragments kPf - 1 k-steps ahead (r05, config 4: 3 -> 5, offset backward
+// 0.0913-0.0921 -> 0.0895-0.0905 ms; 135 registers)
+#ifndef OFFD_PF
+#define OFFD_PF 5
+#endif
 #ifndef OFFD_PRESPLIT
 #define OFFD_PRESPLIT 1
 #endif
@@ -1709,7 +1714,7 @@ __global__ __launch_bounds__(256, 3) void offset_dgrad_bf16(Geo g, const bf16_t*
   const int wt = cw < g.C ? w : 0;  // idle waves (C < 256) load wave 0's (in range)
   const bf16_t* wr0 = wc + ((size_t)(2 * wt) * NKS * 64 + lane) * 8;  // M-tiles 2w, 2w+1
   const bf16_t* wr1 = wr0 + (size_t)NKS * 512;
-  constexpr int kPf = 3;
+  constexpr int kPf = OFFD_PF;
   bf16x8_t ra0[kPf], ra1[kPf];
   auto lda = [&](int ks, int d) {
     const int kc = min(ks, NKS - 1);
