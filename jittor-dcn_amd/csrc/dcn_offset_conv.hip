@@ -58,6 +58,11 @@
 // 0.092-0.0926 ms (k loop 11.3 -> 7.9 us per workgroup, tools/offc_stamps.py)
 // ∂x kernel: Wc fragments kPf - 1 k-steps ahead (r05, config 4: 3 -> 5, offset backward
 // 0.0913-0.0921 -> 0.0895-0.0905 ms; 135 registers)
+// fp32 ∂x kernel (offset_dgrad_mfma): weight fragments kPf steps ahead (r05, config 3: 3 and 4
+// measured no faster than 2)
+#ifndef OFFDM_PF
+#define OFFDM_PF 2
+#endif
 #ifndef OFFD_PF
 #define OFFD_PF 5
 #endif
@@ -1005,7 +1010,7 @@ __global__ __launch_bounds__(256, 4) void offset_dgrad_mfma(Geo g, const float* 
     for (int m = 0; m < 4; ++m)
       a[m] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, lo + 64 * m, so, 0));
   };
-  constexpr int kPf = 2;
+  constexpr int kPf = OFFDM_PF;
   float ra[kPf][4];
 #pragma unroll
   for (int d = 0; d < kPf; ++d) lda(d, ra[d]);
