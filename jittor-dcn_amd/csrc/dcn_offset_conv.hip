@@ -77,6 +77,9 @@
 #ifndef STAGE_NOSC
 #define STAGE_NOSC 1
 #endif
+#ifndef OFFW_CPB
+#define OFFW_CPB 2
+#endif
 #ifndef OFFW_CGB
 #define OFFW_CGB 2
 #endif
@@ -2177,7 +2180,7 @@ hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16
   size_t lds_w, lds_x;
   bwd_bf16_lds(g, ms, &lds_w, &lds_x);
   // chunks per workgroup (config 4: 1 -> 48 + 11 us, 2 -> 42 + 7, 4 -> 53 + 6 for ∂W_off + fold)
-  const int cpb = 2;
+  const int cpb = OFFW_CPB;
   const int nblk = (g.B * ms.cpi + cpb - 1) / cpb;
   if (OFFW_CGB == 2 && (g.C / 64) % 2 == 0)
     hipLaunchKernelGGL(offset_wgrad_bf16<2>, dim3(nblk, g.C / 128), dim3(512), lds_w, s, g, x, goff,
