@@ -49,6 +49,9 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 #endif
 // FUSED_AFIRST = 1 (A/B builds; no change measured): each step's weight-
 // fragment loads are issued ahead of the column stores of the step before (0: r04's order)
+#ifndef FUSED_WINBUF
+#define FUSED_WINBUF 1
+#endif
 #ifndef FUSED_AFIRST
 #define FUSED_AFIRST 0
 #endif
@@ -220,6 +223,13 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
   const int N = g.N;
 
   // window slice cs: kWPix pixels × 8 parts of 16 B (zeros outside the image)
+#if FUSED_WINBUF
+  // r05: through a buffer resource (a position outside the image reads 0 by the range check):
+  // the conditional loads of ld16_if were exec-masked branches, and hipcc waited for all loads
+  // in flight (vmcnt(0)) before several of them
+  const auto rxb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(xb), 0,
+                                                     (int)((size_t)g.HWi * g.C * 2), 0x00020000);
+#endif
   auto win_load = [&](int cs, uint4 (&v)[(kWPix * 8 + 255) / 256]) {
     constexpr int TOT = kWPix * 8, IT = (TOT + 255) / 256;
 #pragma unroll
@@ -228,8 +238,15 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
       const int pix = idx >> 3, part = idx & 7;
       const int rr = pix / kWQ, qq = pix - rr * kWQ;
       const int r = rlo + rr, q = qlo + qq;
+#if FUSED_WINBUF
+      const bool ok = (idx < TOT) & ((unsigned)r < (unsigned)g.H) & ((unsigned)q < (unsigned)g.W);
+      const unsigned o = ok ? (unsigned)(((r * g.W + q) * g.C + kCS * cs + 8 * part) * 2) : 0x80000000u;
+      const auto qv = __builtin_amdgcn_raw_buffer_load_b128(rxb, o, 0, 0);
+      v[k] = make_uint4(qv[0], qv[1], qv[2], qv[3]);
+#else
       const bool ok = idx < TOT && r >= 0 && r < g.H && q >= 0 && q < g.W;
       v[k] = ld16_if(xb + ((size_t)r * g.W + q) * g.C + kCS * cs + 8 * part, ok);
+#endif
     }
   };
   // FUSED_W0EARLY = 1 (A/B builds): slice 0's window loads before the records (r05: records 4.9 µs,
@@ -1200,7 +1217,8 @@ bool fused_fwd_bf16_ok(const Geo& g) {
   const long lim = 1l << 31;
   return g.dt == DCN_BF16 && g.G == 1 && g.N <= kMaxN && g.C % kCS == 0 && g.O % kOT == 0 &&
          g.Ho >= 2 && g.Wo >= 2 && (long)g.O * g.K < lim &&
-         (long)g.HW * g.K * 2 < lim;  // an image's columns: 32-bit buffer byte offsets
+         (long)g.HW * g.K * 2 < lim &&  // an image's columns: 32-bit buffer byte offsets
+         (long)g.HWi * g.C * 2 < lim;   // an image's xT (the window loads, FUSED_WINBUF)
 }
 
 // r03 (tools/r03_fb_geo.py, fwd+bwd per step): fused faster wherever all
