@@ -237,6 +237,44 @@ def load_fused_traffic(bf16_cfg4_glob="r*_pmc_hbm_config4.json"):
     return None, None
 
 
+def load_mfma_busy(config):
+    """Counter-measured MFMA utilisation per scope (gemm_fwd, gemm_dw, gemm_dcol, offset_fwd,
+    offset_bwd) from the newest committed profiles/r*_mfma_busy_config{N}.json
+    (tools/pmc_mfma.sh + tools/mfma_summary.py: SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x
+    GRBM_GUI_ACTIVE / 8), one rocprofv3 pass). Returns (scopes dict, relative path) or
+    ({}, None)."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_mfma_busy_config{config}.json")))
+    for path in reversed(paths):
+        try:
+            with open(path) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if doc.get("scopes"):
+            return doc["scopes"], os.path.relpath(path, ROOT)
+    return {}, None
+
+
+def annotate_busy(entries, config):
+    """Add the counter-measured MFMA utilisation beside every MFMA-bound roofline entry
+    (VERDICT r05 item 3): `mfma_busy` (fraction of the matrix pipes' cycles busy while the
+    kernel ran, at the clock it ran at) and `busy_source` (file:scope), in the style of
+    `traffic_source`. The flop-based `frac` uses the HIP-event time and the 2.5 PF / 157.3 TF
+    spec peak at its nominal clock, so the two differ by the clock the chip held (reported as
+    `busy_clock_ghz`) and by MFMA work on padding."""
+    scopes, src = load_mfma_busy(config)
+    for e in entries or ():
+        if not e or e.get("bound") != "mfma":
+            continue
+        sc = e.get("scope") or e["kernel"].split(" ")[0]
+        v = scopes.get(sc)
+        e["mfma_busy"] = v.get("mfma_busy") if v else None
+        e["busy_clock_ghz"] = v.get("clock_ghz") if v else None
+        e["busy_source"] = f"{src}:{sc}" if v else None
+    return entries
+
+
 class Workload:
     """One BASELINE configuration's replicated parameters and packed gradient buffer on
     `dev` (synthetic, SURVEY §8(d): offset conv σ = 1/sqrt(C·9) so Δ ~ N(0,1) px; the same
@@ -287,6 +325,7 @@ def fused_roofline(kernel_ms, B, Ho, Wo, N, C, O_):
         "kernel": "dcn::fwd_fused_bf16 (f2: bilinear gather into bf16 MFMA + bias, "
                   "columns stored for the backward)",
         "bound": "mfma",
+        "scope": "gemm_fwd",
         "achieved": round(fl / (ms * 1e-3) / 1e12, 1),
         "peak": 2500.0,
         "unit": "TFLOP/s",
@@ -331,11 +370,13 @@ def config4_leg(args, world, rank, wl, rt, make_step, timed, kernel_times, fwd_p
         "global_batch": B * world,
         "kernel_ms": km,
         "fwd_paths_ms_per_step": paths,
-        "rooflines_other": other_rooflines(km, B, C, O_, cfg["H"], cfg["W"], N, Ho, Wo, J, True,
-                                           False),
+        "rooflines_other": annotate_busy(
+            other_rooflines(km, B, C, O_, cfg["H"], cfg["W"], N, Ho, Wo, J, True, False)
+            + [e for e in scope_rooflines(km, cfg, B, Ho, Wo)
+               if e["kernel"] in ("offset_fwd", "offset_bwd")], 4),
     }
     if km.get("gemm_fwd") and not km.get("im2col"):
-        res["roofline"] = fused_roofline(km, B, Ho, Wo, N, C, O_)
+        res["roofline"] = annotate_busy([fused_roofline(km, B, Ho, Wo, N, C, O_)], 4)[0]
     else:  # the unfused schedule ran (K1 bf16 is the forward's HBM kernel)
         k1_ms = km.get("im2col")
         k1_b = k1_bytes(B, C, cfg["H"], cfg["W"], N, Ho, Wo, elem=2, J=J)
@@ -433,8 +474,8 @@ def extra_config_leg(num, args, wl, rt, make_step, timed, kernel_times, sync, cp
         "samples_per_step": B * Ho * Wo * N,
         "graph_ms_per_step": round(gms, 4) if gms else None,
         "kernel_ms": km,
-        "roofline": roofs[0] if roofs else None,
-        "rooflines_other": roofs[1:],
+        "roofline": annotate_busy(roofs[:1], num)[0] if roofs else None,
+        "rooflines_other": annotate_busy(roofs[1:], num),
         "cpu_baseline": None,
     }
     if cpu is not None:
@@ -810,6 +851,10 @@ def main():
             if num == 2 and not args.no_cpu_baseline:
                 cpu = cpu_baseline_framework(CONFIGS[2], min(args.cpu_budget, 8.0),
                                              name="config2")
+            elif num == 5 and not args.no_cpu_baseline:
+                # dilation / deform groups: the torch restatement of the reference's op
+                # sequence has neither, so the C/OpenMP port (oracle/dcn_ref.c) is the baseline
+                cpu = cpu_baseline(CONFIGS[5], min(args.cpu_budget, 8.0), name="config5")
             extra[num] = extra_config_leg(num, args, wlx, rt, make_step, timed, kernel_times,
                                           lambda: torch.cuda.synchronize(dev), cpu, graph_timed)
             del wlx
@@ -860,8 +905,10 @@ def main():
             },
             "kernel_ms": kernel_ms,
             "launch": graph_note or "eager (one launch per kernel)",
-            "rooflines_other": other_rooflines(kernel_ms, B, C, O_, H, W, N, Ho, Wo, J, bf16,
-                                               fwd_only),
+            "rooflines_other": annotate_busy(
+                other_rooflines(kernel_ms, B, C, O_, H, W, N, Ho, Wo, J, bf16, fwd_only)
+                + [e for e in scope_rooflines(kernel_ms, cfg, B, Ho, Wo)
+                   if e["kernel"] in ("offset_fwd", "offset_bwd")], args.config),
             "alt": alt,
             "fwd_paths_ms_per_step": fwd_paths,
             "strong_scaling": strong_res,
@@ -874,7 +921,8 @@ def main():
         if bf16 and not k1_ms and kernel_ms.get("gemm_fwd"):
             # DCN_FWD_AUTO ran the fused forward: K1 does not exist as a
             # launch; the dominant forward kernel is the fused one (gather + GEMM + bias)
-            res["roofline"] = fused_roofline(kernel_ms, B, Ho, Wo, N, C, O_)
+            res["roofline"] = annotate_busy([fused_roofline(kernel_ms, B, Ho, Wo, N, C, O_)],
+                                            args.config)[0]
         if world == 1 and not bf16 and not args.no_host_path:
             res["host_path"] = host_path_rate(cfg, args.config)
         if world == 1 and not args.no_cpu_baseline:

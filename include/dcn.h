@@ -158,11 +158,15 @@ int dcn_forward_ex(dcn_handle* h, const dcn_desc* d, const float* x,
                    const float* b, float* out, float* off, void* ws,
                    size_t ws_bytes, int flags);
 
-#define DCN_BWD_COL_IN_WS 1 /* ws still holds forward's columns. For DCN_BF16 the handle
-                              records the workspaces its forwards wrote columns into (at most
-                              256, the oldest dropped first); a backward on any other
-                              workspace (a NO_COLUMNS / FUSED_NOCOL forward, a dropped record,
-                              another handle's forward) recomputes them. */
+#define DCN_BWD_COL_IN_WS 1 /* ws still holds forward's columns: the caller must not let
+                              anything write into ws between this handle's forward and this
+                              backward (another handle's forward, an fp32 forward, a forward of
+                              another geometry on the same ws). For DCN_BF16 the handle records
+                              the workspaces its own forwards wrote columns into (a bare
+                              pointer per workspace, at most 256, the oldest dropped first); a
+                              backward on a workspace it holds no record for (a NO_COLUMNS /
+                              FUSED_NOCOL forward, a dropped record) recomputes them, but the
+                              record does not notice a foreign write into a recorded ws. */
 
 /* Autodiff of DeformConv2d.execute as triggered by optimizer.backward
  * (train.py:414). Overwrites grad_x, grad_w, grad_b (if has_bias),

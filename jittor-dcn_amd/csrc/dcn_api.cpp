@@ -1143,6 +1143,7 @@ int offset_conv_fwd_gemm(dcn_handle* h, const Geo& g, const float* xT, const flo
   sp.ta = true;
   sp.m = g.J; sp.n = P; sp.k = K;
   sp.lda = K; sp.ldb = K; sp.ldc = g.J;
+  sp.native_f32 = true;
   GEMM_TRY(h, sp, wp, ocol, offT);
   HIP_TRY(dcn::launch_ocg_offt_to_off(g, offT, b_off, off, h->stream));
   return DCN_OK;
@@ -1162,6 +1163,7 @@ int offset_conv_bwd_gemm(dcn_handle* h, const Geo& g, const float* xT, const flo
     sp.tb = true;
     sp.m = K; sp.n = g.J; sp.k = P;
     sp.lda = K; sp.ldb = g.J; sp.ldc = K;
+    sp.native_f32 = true;
     GEMM_TRY(h, sp, ocol, goffT, gwp);
   }
   HIP_TRY(dcn::launch_ocg_wgrad_out(g, gwp, gw_off, h->stream));
@@ -1170,6 +1172,7 @@ int offset_conv_bwd_gemm(dcn_handle* h, const Geo& g, const float* xT, const flo
     dcn::GemmSpec sp;
     sp.m = K; sp.n = P; sp.k = g.J;
     sp.lda = K; sp.ldb = g.J; sp.ldc = K;
+    sp.native_f32 = true;
     GEMM_TRY(h, sp, wp, goffT, ocol);
   }
   HIP_TRY(dcn::launch_ocg_col2im(g, ocol, gxT_in, gx, h->stream));

@@ -246,7 +246,7 @@ int gemm_run(GemmEngine* e, const GemmSpec& s, const void* A, const void* B, voi
              hipStream_t st, std::string* err) {
   // split-bf16 arithmetic for fp32 operands when selected (the bf16 tensor path keeps the
   // vendor bf16 GEMMs); shapes the split kernel cannot stage fall back to native f32
-  if (e->math && gemm_split_ok(s, A, B, C)) {
+  if (e->math && !s.native_f32 && gemm_split_ok(s, A, B, C)) {
     const hipError_t r = launch_gemm_split(e->math, s, static_cast<const float*>(A),
                                            static_cast<const float*>(B), static_cast<float*>(C),
                                            st);
@@ -287,7 +287,21 @@ int gemm_run(GemmEngine* e, const GemmSpec& s, const void* A, const void* B, voi
     if (!have) {
       if (tune(e, s, A, B, C, st, p, err) != 0) return -1;
       std::lock_guard<std::mutex> lk(g_choice_mu);
-      g_choice.emplace(gk, Choice{p.backend, p.algo, p.ms});
+      // two handles may tune the same key at once: the first stored choice wins, and a handle
+      // whose own pick differs adopts it (same kernel process-wide, bit for bit)
+      const auto ins = g_choice.emplace(gk, Choice{p.backend, p.algo, p.ms});
+      const Choice& c = ins.first->second;
+      if (!ins.second &&
+          (c.backend != p.backend ||
+           (c.backend == 1 && std::memcmp(&c.algo, &p.algo, sizeof(p.algo)) != 0))) {
+        if (c.backend == 1 && p.backend != 1 && !lt_describe(e, s, p)) {
+          *err = "hipBLASLt plan for a shape tuned by another handle";
+          return -1;
+        }
+        p.backend = c.backend;
+        p.ms = c.ms;
+        if (c.backend == 1) p.algo = c.algo;
+      }
     }
     it = e->plans.emplace(key_of(s), p).first;
   }
@@ -296,7 +310,7 @@ int gemm_run(GemmEngine* e, const GemmSpec& s, const void* A, const void* B, voi
 }
 
 int gemm_backend_of(GemmEngine* e, const GemmSpec& s) {
-  if (e->math && !s.bf16_ab && !s.bf16_c) return 2;
+  if (e->math && !s.native_f32 && !s.bf16_ab && !s.bf16_c) return 2;
   auto it = e->plans.find(key_of(s));
   return it == e->plans.end() ? -1 : it->second.backend;
 }

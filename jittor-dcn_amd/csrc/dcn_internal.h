@@ -285,6 +285,10 @@ struct GemmSpec {
   int batch = 1;
   bool bf16_ab = false;  // A and B are bf16 (DCN_BF16); compute is always fp32
   bool bf16_c = false;   // C is bf16 (else fp32)
+  // native f32 MFMA whatever the handle's dcn_math: the math mode covers only the three GEMMs
+  // of the op (include/dcn.h); the offset conv's GEMMs set this (their outputs are sampling
+  // coordinates, so split-bf16 rounding there would move floors)
+  bool native_f32 = false;
 };
 struct GemmEngine;
 int gemm_engine_create(GemmEngine** out, std::string* err);

@@ -185,6 +185,23 @@ def test_offset_conv_gemm_vs_valu_kernels(gpu_handle, geo):
     _check_all(out1, off1, g1, ro, roff, rg, "offset-conv GEMM path")
 
 
+@pytest.mark.parametrize("math", [3, 6])
+def test_offset_conv_gemm_native_under_split_math(gpu_handle, math):
+    """dcn_set_math covers the op's three GEMMs only (include/dcn.h). The offset
+    conv's own GEMMs (ocg path: stride / dilation != 1) stay native f32 under every math mode,
+    so the offsets are bit for bit the native-mode ones (the gradients are not: ∂col is one of
+    the three GEMMs)."""
+    c = _rand_case(512, B=4, C=512, O_=64, H=14, W=14, s=(2, 2), p=(1, 1), dil=(2, 2), G=4)
+    h = gpu_handle
+    _, off0, _ = _device_fwd_bwd(h, c)
+    h.set_math(math)
+    try:
+        _, off1, _ = _device_fwd_bwd(h, c)
+    finally:
+        h.set_math(0)
+    np.testing.assert_array_equal(off1, off0, err_msg=f"offsets under dcn_set_math({math})")
+
+
 # ---- data-parallel exchange hooks on one rank -------------------------------------------
 
 def test_fp32_backward_with_attached_comm_single_rank(gpu_handle):
