@@ -34,9 +34,6 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
-#ifndef FP32_BINS_SERIAL
-#define FP32_BINS_SERIAL 0  // (A/B builds: the fp32 bins on the main stream right before K5)
-#endif
 #define HIP_TRY(expr)                                                                        \
   do {                                                                                       \
     hipError_t e_ = (expr);                                                                  \
@@ -477,12 +474,9 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
                   bool col_valid) {
   // the sample bins depend only on the offsets: build them on the side stream while the
   // main stream runs the ∂W / ∂col GEMMs
-  // (r02 A/B: the bins serialised before K5 instead: step 7.06 against 7.00-7.02 ms;
-  // FP32_BINS_SERIAL = 1 A/B builds repeat it on the r03+ bins kernels)
-  if (!FP32_BINS_SERIAL) {
-    DCN_TRY(fork_aux(h));
-    HIP_TRY(dcn::launch_bins(g, off, bins, goff, 0, g.B, h->aux));
-  }
+  // (r02 A/B: the bins serialised before K5 instead: step 7.06 against 7.00-7.02 ms)
+  DCN_TRY(fork_aux(h));
+  HIP_TRY(dcn::launch_bins(g, off, bins, goff, 0, g.B, h->aux));
   if (!col_valid) {
     {
       ProfScope ps(h, DCN_K_XPOSE);
@@ -582,7 +576,6 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
     }
   }
   DCN_TRY(join_aux(h));  // bins ready
-  if (FP32_BINS_SERIAL) HIP_TRY(dcn::launch_bins(g, off, bins, goff, 0, g.B, h->stream));
   {
     // K5 overwrites grad_x (sampling route) and grad_off
     ProfScope ps(h, DCN_K_COL2IM);

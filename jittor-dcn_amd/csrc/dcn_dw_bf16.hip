@@ -42,40 +42,21 @@ typedef __attribute__((address_space(1))) void gvoid;
 typedef __attribute__((address_space(3))) void lvoid;
 
 // Pipeline shape (compile-time; the A/B builds of DESIGN.md §4 set them with -D): DW_PX
-// pixels per stage (16 or 32), DW_RING LDS stages, DW_NT = 1 streams the column DMAs with the
-// non-temporal policy (the columns are read once; ∂outT is re-read by every column tile).
+// pixels per stage (16 or 32), DW_RING LDS stages. (The round-5 variants: non-temporal column
+// DMAs, DMAs issued before the stage barrier, a scheduling pin after the MFMAs, and the
+// diagnostic ablations are gone; their A/B results are in DESIGN.md §4 and
+// profiles/r05_dw_ab.txt.)
 #ifndef DW_PX
 #define DW_PX 32
 #endif
 #ifndef DW_RING
 #define DW_RING 4
 #endif
-#ifndef DW_NT
-#define DW_NT 0
-#endif
-// DW_EARLY = 1: each step issues its DMAs BEFORE waiting at the stage barrier, into the slot
-// of stage s - 2 (every wave finished reading it before the previous barrier), so the refill
-// does not wait for the slowest wave; kDwRing - 2 stages ahead instead of kDwRing - 1.
-// DW_PIN = 1: a scheduling barrier after each stage's MFMAs keeps them ahead of the next
-// stage's wait and barrier (hipcc otherwise sinks them past the barrier, delaying the DMAs).
-#ifndef DW_EARLY
-#define DW_EARLY 0
-#endif
-#ifndef DW_PIN
-#define DW_PIN 0
-#endif
-// DW_ABL (diagnostic A/B builds only, wrong results): 1 LDS reads without MFMAs, 2 the DMA
-// stream alone, 3 the column tiles read as contiguous [tile][pixel][256] blocks, 5 the column
-// DMAs only (no ∂outT stream), 6 no partial-plane stores, 7 the DMA stream alone without the
-// stage barriers
-#ifndef DW_ABL
-#define DW_ABL 0
-#endif
 constexpr int kDwO = 256;                          // output channels: the tile's rows
 constexpr int kDwN = 256;                          // ∂W columns per tile
 constexpr int kDwPx = DW_PX;                       // pixels per stage
 constexpr int kDwRing = DW_RING;                   // LDS stages
-constexpr int kDwAhead = kDwRing - 1 - DW_EARLY;   // stages issued ahead of the one consumed
+constexpr int kDwAhead = kDwRing - 1;       // stages issued ahead of the one consumed
 constexpr int kDwRowB = 512;                       // one pixel row of either operand (256 bf16)
 constexpr int kDwOpB = kDwPx * kDwRowB;            // 16 KiB per operand per 32-pixel stage
 constexpr int kDwStageB = 2 * kDwOpB;              // A (∂outT) then B (columns)
@@ -88,7 +69,6 @@ constexpr int kDwWaves = 8;
 constexpr int kDwLoaders = DW_LOADERS;
 static_assert(kDwLoaders == 2 || kDwLoaders == 4 || kDwLoaders == 8, "loader waves");
 constexpr int kDwGlds = kDwStageB / (kDwLoaders * 1024);  // DMA instructions per loader per stage
-constexpr int kDwWaitG = DW_ABL == 5 ? kDwGlds / 2 : kDwGlds;  // ... that the waits count
 constexpr int kDwOpI = kDwPx / 2;                  // DMA instructions per operand (2 rows each)
 static_assert(kDwPx == 16 || kDwPx == 32, "stage = one or two 16-pixel k-steps");
 static_assert(kDwRing >= 3 && kDwRing <= 8, "ring depth");
@@ -165,34 +145,21 @@ __global__ __launch_bounds__(kDwWaves * 64, 1) void dw_stream_bf16(
   // uniform); lane L writes physical chunk L & 31 of row 2i + (L >> 5), i.e. fetches logical
   // chunk (L & 31) ^ 4·(row & 3). Byte offsets are 32-bit (dw_stream_bf16_ok).
   const int lrow = lane >> 5, lpc = lane & 31;
-#if DW_ABL == 3  // (diagnostic build: each column tile read as if stored [tile][pixel][256])
-  const char* opbase[2] = {reinterpret_cast<const char*>(goutT),
-                           reinterpret_cast<const char*>(col) + (size_t)tile * npix * kDwRowB};
-  const unsigned opstride[2] = {(unsigned)kDwRowB, (unsigned)kDwRowB};
-#else
   const char* opbase[2] = {reinterpret_cast<const char*>(goutT),
                            reinterpret_cast<const char*>(col) + (size_t)tile * kDwN * 2};
   const unsigned opstride[2] = {(unsigned)kDwRowB, (unsigned)K * 2u};
-#endif
   auto issue = [&](int j, char* slot) {
     if (w >= kDwLoaders) return;  // wave-uniform
     j = min(j, nst - 1);  // past the range: re-read its last stage (L2), never read back
 #pragma unroll
     for (int u = 0; u < kDwGlds; ++u) {
       const int ii = u * kDwLoaders + w, op = ii / kDwOpI, i = ii % kDwOpI;
-#if DW_ABL == 5  // (diagnostic build: the column DMAs only, no ∂outT stream)
-      if (op == 0) continue;
-#endif
       const int row = 2 * i + lrow;
       const unsigned ch = (unsigned)(lpc ^ (4 * (row & 3)));
       const int p = min(px0 + j * kDwPx + row, npix - 1);  // past the end: re-read the last row
       const char* src = opbase[op] + ((unsigned)p * opstride[op] + ch * 16u);
-      if (op == 0 || !DW_NT)
-        __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(slot + op * kDwOpB + i * 1024),
-                                         16, 0, 0);
-      else  // aux 2: the non-temporal policy (MI355X_MICROARCH.md nt-weights)
-        __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(slot + op * kDwOpB + i * 1024),
-                                         16, 0, 2);
+      __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(slot + op * kDwOpB + i * 1024),
+                                       16, 0, 0);
     }
   };
 
@@ -231,9 +198,6 @@ __global__ __launch_bounds__(kDwWaves * 64, 1) void dw_stream_bf16(
   // launch: the ∂outT rows past the end (DMA'd from the last row) are zeroed in the A
   // fragments, so their products vanish
   auto compute = [&](const char* slot, int nvalid) {
-#if DW_ABL == 2 || DW_ABL == 7
-    return;  // (diagnostic build: the DMA stream alone)
-#endif
 #pragma unroll
     for (int ks = 0; ks < kDwPx / 16; ++ks) {
       const char* base = slot + ks * 16 * kDwRowB;
@@ -251,15 +215,11 @@ __global__ __launch_bounds__(kDwWaves * 64, 1) void dw_stream_bf16(
           for (int e = 0; e < 8; ++e)
             if (r0 + (e & 3) + 4 * (e >> 2) >= nvalid) a[mi][e] = (__bf16)0.f;
       }
-#if DW_ABL == 1  // (diagnostic build: LDS reads, no MFMAs)
-      asm volatile("" ::"v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(b[0]), "v"(b[1]));
-#else
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni)
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
-#endif
     }
   };
 
@@ -269,32 +229,16 @@ __global__ __launch_bounds__(kDwWaves * 64, 1) void dw_stream_bf16(
   // every step and on every path: hipcc's own wait before a slot's first read then never
   // drains the queue)
   auto step = [&](int s, char* cur, char* refill) {
-#if DW_EARLY
-    // every wave finished reading stage s - 2 before the previous step's barrier
-    issue(s + kDwAhead, refill);
-    __builtin_amdgcn_sched_barrier(0);
-    // this wave's DMAs of stage s have landed once only those of s + 1 .. s + kDwAhead are
-    // pending
-    vm_wait<kDwAhead * kDwWaitG>();
-    __builtin_amdgcn_s_barrier();  // every wave's DMAs of stage s landed
-    __builtin_amdgcn_sched_barrier(0);
-#else
     // this wave's DMAs of stage s have landed once only those of s + 1 .. s + kDwAhead - 1
     // are pending
-    vm_wait<(kDwAhead - 1) * kDwWaitG>();
+    vm_wait<(kDwAhead - 1) * kDwGlds>();
     // every wave's DMAs of stage s landed; every wave finished reading stage s - 1, whose
     // slot (`refill`) the DMA of stage s + kDwAhead now refills
-#if DW_ABL != 7  // (7: diagnostic build, the DMA stream alone without the stage barriers)
     __builtin_amdgcn_s_barrier();
-#endif
     __builtin_amdgcn_sched_barrier(0);
     issue(s + kDwAhead, refill);
     __builtin_amdgcn_sched_barrier(0);
-#endif
     compute(cur, min(kDwPx, npix - (px0 + s * kDwPx)));
-#if DW_PIN
-    __builtin_amdgcn_sched_barrier(0);
-#endif
   };
   // (slot k + kDwAhead is refilled while slot k is read; the loops are fully unrolled, so
   // every slot pointer is a compile-time LDS object)
@@ -321,11 +265,7 @@ __global__ __launch_bounds__(kDwWaves * 64, 1) void dw_stream_bf16(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int o = 128 * wo + 32 * mi + drow(r, hh);
-#if DW_ABL == 6  // (diagnostic build: no partial-plane stores)
-        asm volatile("" ::"v"(acc[mi][ni][r]));
-#else
         dst[(size_t)o * K + 64 * wk + 32 * ni + n] = acc[mi][ni][r];
-#endif
       }
 }
 

@@ -37,65 +37,9 @@ namespace {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
-// FUSED_LINES = 1: the stored columns leave as whole 128-B lines (store_cols); 0: r04's
-// per-unit half-line stores (A/B builds only)
-#ifndef FUSED_LINES
-#define FUSED_LINES 1
-#endif
-// FUSED_NT = 0: the column stores with the default cache policy instead of non-temporal
-// (A/B: whether L2 merges the two half-line writes of FUSED_LINES = 0 before write-back)
-#ifndef FUSED_NT
-#define FUSED_NT 1
-#endif
-// FUSED_AFIRST = 1 (A/B builds; no change measured): each step's weight-
-// fragment loads are issued ahead of the column stores of the step before (0: r04's order)
-#ifndef FUSED_WINBUF
-#define FUSED_WINBUF 1
-#endif
-#ifndef FUSED_AFIRST
-#define FUSED_AFIRST 0
-#endif
-// FUSED_ABL (diagnostic A/B builds only, wrong results), bit flags: 1 no gather, 2 no MFMAs,
-// 4 no column stores, 8 no weight-fragment loads, 16 no k loop
-#ifndef FUSED_ABL
-#define FUSED_ABL 0
-#endif
-#ifndef FUSED_STAGGER
-#define FUSED_STAGGER 0
-#endif
-#ifndef FUSED_W0EARLY
-#define FUSED_W0EARLY 0
-#endif
-// FUSED_PP = 1 (A/B builds): the forwards run as fwd_fused_bf16_pp (two tiles per workgroup
-// in ping-pong); 0: fwd_fused_bf16 (one tile per workgroup, the measured faster: DESIGN.md §4.8)
-#ifndef FUSED_PP
-#define FUSED_PP 0
-#endif
-// FUSED_STAMP = 1 (diagnostic A/B builds only): thread 0 of each workgroup of the storing
-// forward records s_memrealtime (100 MHz) at its phase boundaries; dcn_debug_fused_stamps
-// copies them out (tools/fused_stamps.py)
-#ifndef FUSED_STAMP
-#define FUSED_STAMP 0
-#endif
-#if FUSED_STAMP
-constexpr int kStampWg = 4096, kStamps = 8;
-__device__ unsigned long long g_fused_stamps[kStampWg * kStamps];
-#define STAMP(i)                                                                      \
-  do {                                                                                \
-    if (STORE && threadIdx.x == 0 && stamp_wg < kStampWg)                             \
-      g_fused_stamps[stamp_wg * kStamps + (i)] = __builtin_amdgcn_s_memrealtime();     \
-  } while (0)
-#else
-#define STAMP(i) \
-  do {           \
-  } while (0)
-#endif
 template <typename T>
 __device__ __forceinline__ void col_store(T v, T* p) {
-  if (FUSED_NT)
-    __builtin_nontemporal_store(v, p);
-  else
-    *p = v;
+  __builtin_nontemporal_store(v, p);
 }
 constexpr int kTH = 7, kTW = 16;  // output tile rows (h) × columns (w)
 constexpr int kPB = kTH * kTW / 16;  // 16-slot MFMA column blocks
@@ -205,16 +149,6 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
   const Block3 blk = xcd_block();
   const int b = blk.y;
   const int th_i = blk.x / tw_n, tw_i = blk.x - th_i * tw_n;
-  const int stamp_wg = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
-  (void)stamp_wg;
-  STAMP(0);
-#if FUSED_STAGGER
-  // (A/B builds) the second half of the grid, dispatched as each CU's second workgroup,
-  // starts FUSED_STAGGER × 64 cycles late, so the two workgroups of a CU run out of phase
-  if (stamp_wg >= (int)(gridDim.x * gridDim.y * gridDim.z) / 2) {
-    for (int i = 0; i < FUSED_STAGGER / 16; ++i) __builtin_amdgcn_s_sleep(16);
-  }
-#endif
   const int h0 = th_i * kTH, w0 = tw_i * kTW;
   const int o0 = blk.z * kOT + 64 * wave;
   const int rlo = (int)floorf((float)w0 * (float)(g.H - 1) / (float)(g.Wo - 1)) - kMar;
@@ -223,13 +157,11 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
   const int N = g.N;
 
   // window slice cs: kWPix pixels × 8 parts of 16 B (zeros outside the image)
-#if FUSED_WINBUF
   // r05: through a buffer resource (a position outside the image reads 0 by the range check):
   // the conditional loads of ld16_if were exec-masked branches, and hipcc waited for all loads
   // in flight (vmcnt(0)) before several of them
   const auto rxb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(xb), 0,
                                                      (int)((size_t)g.HWi * g.C * 2), 0x00020000);
-#endif
   auto win_load = [&](int cs, uint4 (&v)[(kWPix * 8 + 255) / 256]) {
     constexpr int TOT = kWPix * 8, IT = (TOT + 255) / 256;
 #pragma unroll
@@ -238,22 +170,14 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
       const int pix = idx >> 3, part = idx & 7;
       const int rr = pix / kWQ, qq = pix - rr * kWQ;
       const int r = rlo + rr, q = qlo + qq;
-#if FUSED_WINBUF
       const bool ok = (idx < TOT) & ((unsigned)r < (unsigned)g.H) & ((unsigned)q < (unsigned)g.W);
       const unsigned o = ok ? (unsigned)(((r * g.W + q) * g.C + kCS * cs + 8 * part) * 2) : 0x80000000u;
       const auto qv = __builtin_amdgcn_raw_buffer_load_b128(rxb, o, 0, 0);
       v[k] = make_uint4(qv[0], qv[1], qv[2], qv[3]);
-#else
-      const bool ok = idx < TOT && r >= 0 && r < g.H && q >= 0 && q < g.W;
-      v[k] = ld16_if(xb + ((size_t)r * g.W + q) * g.C + kCS * cs + 8 * part, ok);
-#endif
     }
   };
-  // FUSED_W0EARLY = 1 (A/B builds): slice 0's window loads before the records (r05: records 4.9 µs,
-  // then the slice-0 window 7.0 µs, one after the other); slower, 0.152-0.155 vs 0.142-0.143 ms
-  // (the window registers live across the records loop: 40 spills instead of 12)
-  uint4 w0v[(kWPix * 8 + 255) / 256];
-  if (FUSED_W0EARLY) win_load(0, w0v);
+  // (r05 A/B: slice 0's window loaded before the records instead, slower: 0.152-0.155 vs
+  // 0.142-0.143 ms, the window registers live across the records loop)
 
   // ---- records ----
   if (tid == 0) cnt[0] = 0;
@@ -283,7 +207,6 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
   }
   __syncthreads();
   const int novf = min(cnt[0], kOvf);
-  STAMP(1);
 
   // ---- per-thread production units: u = tid, tid + 256 (u < kUnits): slot u>>2, 8-ch group u&3
   // (wave-uniform count: waves 0-2 hold two unit sets, wave 3 one)
@@ -310,18 +233,14 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
 
   const int NKS = g.K / 32;
   const int spq = 2 * N;  // steps per slice
-  const int nslices = (FUSED_ABL & 16) ? 0 : g.C / kCS;  // (16: diagnostic build)
+  const int nslices = g.C / kCS;
   // A fragments of step s of slice cs: k = n·C + 64·cs + 32·half
   auto load_a = [&](int cs, int s, uint4 (&a)[4]) {
     const int ks = ((s >> 1) * g.C + kCS * cs + 32 * (s & 1)) >> 5;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-#if FUSED_ABL & 8  // (diagnostic build: no weight loads)
-      a[i] = make_uint4(ks, i, lane, 0);
-#else
       a[i] = *reinterpret_cast<const uint4*>(
           wfr + ((size_t)(((o0 >> 4) + i) * NKS + ks) * 64 + lane) * 8);
-#endif
   };
   // gather step s of slice cs into B buffer buf (and, with STORE, the column rows)
   auto produce = [&](int cs, int s, int buf) {
@@ -332,12 +251,7 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
         const int slot = uslot[k], cg = ucg[k];
         const int meta = recm[slot * kMaxN + n];
         uint4 o = make_uint4(0u, 0u, 0u, 0u);
-#if FUSED_ABL & 1  // (diagnostic build: no gather, the B tile is the record words)
-        o = make_uint4((unsigned)meta, (unsigned)slot, (unsigned)n, 0u);
-        if (false) {
-#else
         if (meta >= 0) {
-#endif
           const float4 wv = recw[slot * kMaxN + n];
           const char* wp = win + meta * kWPitch + hh * 64 + cg * 16;
           const uint4 ua = *reinterpret_cast<const uint4*>(wp);
@@ -357,18 +271,6 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
           }
         }
         *reinterpret_cast<uint4*>(bt + buf * kSlots * kBPitch + slot * kBPitch + cg * 16) = o;
-#if !FUSED_LINES
-        // (A/B build) r04's column stores: each unit's 16 B as it is produced, so a 128-B line
-        // is written in two halves one step apart
-        if (STORE) {
-          const int h = h0 + slot / kTW, w = w0 + slot % kTW;
-          if (h < g.Ho && w < g.Wo)
-            col_store(
-                as_v(o), reinterpret_cast<v4u*>(colT + (size_t)b * g.HW * g.K +
-                                                (unsigned)(h * g.Wo + w) * (unsigned)g.K +
-                                                (n * g.C + kCS * cs + 32 * hh + 8 * cg)));
-        }
-#endif
       }
     }
   };
@@ -377,34 +279,6 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
   // and this wave's next production comes after this in program order)
   auto store_cols = [&](int cs, int n) {
     const int j = lane & 7;
-#if FUSED_AFIRST
-    // a fixed count of store instructions on every path (buffer stores; the lanes of slots
-    // past the tile or the map get an offset past the image's columns, which the buffer
-    // range check drops): the compiler can then count the A loads issued before them exactly
-    // instead of waiting for everything (a store inside a branch may or may not be counted)
-    const auto rsc = __builtin_amdgcn_make_buffer_rsrc(colT + (size_t)b * g.HW * g.K, 0,
-                                                       (int)((size_t)g.HW * g.K * 2), 0x00020000);
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int sl = 16 * wave + 64 * k + 8 * i + (lane >> 3);  // >= kSlots: wave 3, k = 1
-        const int slr = min(sl, kSlots - 1);
-        const v4u v = *reinterpret_cast<const v4u*>(bt + (j >> 2) * kSlots * kBPitch +
-                                                    slr * kBPitch + (j & 3) * 16);
-        const int h = h0 + slr / kTW, w = w0 + slr % kTW;
-        const unsigned o = (sl < kSlots && h < g.Ho && w < g.Wo)
-                               ? ((unsigned)(h * g.Wo + w) * (unsigned)g.K +
-                                  (unsigned)(n * g.C + kCS * cs + 8 * j)) * 2u
-                               : 0x80000000u;
-#if FUSED_ABL & 4  // (diagnostic build: no column stores)
-        asm volatile("" ::"v"(v), "v"(o));
-#else
-        __builtin_amdgcn_raw_buffer_store_b128(v, rsc, o, 0, FUSED_NT ? 2 : 0);
-#endif
-      }
-    return;
-#endif
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       if (k < nu) {
@@ -428,13 +302,9 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
 #pragma unroll
     for (int pb = 0; pb < kPB; ++pb) {
       const bf16x8_t bv = as_frag(*reinterpret_cast<const uint4*>(bb + pb * 16 * kBPitch));
-#if FUSED_ABL & 2  // (diagnostic build: no MFMAs; operands kept live)
-      asm volatile("" ::"v"(bv), "v"(as_frag(a[0])), "v"(as_frag(a[1])), "v"(as_frag(a[2])), "v"(as_frag(a[3])));
-#else
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         acc[i][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a[i]), bv, acc[i][pb], 0, 0, 0);
-#endif
     }
   };
 
@@ -445,12 +315,7 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
       // window slice: kWPix pixels × 8 parts of 16 B; overflow corners loaded alongside
       constexpr int TOT = kWPix * 8, IT = (TOT + 255) / 256;
       uint4 v[IT];
-      if (FUSED_W0EARLY && cs == 0) {  // (issued before the records)
-#pragma unroll
-        for (int k = 0; k < IT; ++k) v[k] = w0v[k];
-      } else {
-        win_load(cs, v);
-      }
+      win_load(cs, v);
       // overflow: novf entries × 8 units of 8 channels
       uint4 ov[2];
 #pragma unroll
@@ -476,7 +341,6 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
       }
     }
     load_a(cs, 0, aE);
-    if (cs < 4) STAMP(2 + cs);
     __syncthreads();
     produce(cs, 0, 0);
     __syncthreads();
@@ -485,19 +349,11 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
       produce(cs, s + 1, 1);
       mfma_step(0, aE);
       __syncthreads();
-#if FUSED_AFIRST
-      // the A loads of step s + 2 go out before this step's column stores: vmcnt retires in
-      // issue order, so a wait for loads issued behind the stores would wait for the stores
-      load_a(cs, min(s + 2, spq - 1), aE);  // unconditional (clamped): a fixed vmcnt count
-      if (STORE && FUSED_LINES) store_cols(cs, s >> 1);
-      if (s + 2 < spq) produce(cs, s + 2, 0);
-#else
-      if (STORE && FUSED_LINES) store_cols(cs, s >> 1);
+      if (STORE) store_cols(cs, s >> 1);
       if (s + 2 < spq) {
         load_a(cs, s + 2, aE);
         produce(cs, s + 2, 0);
       }
-#endif
       mfma_step(1, aO);
       __syncthreads();
     }
@@ -510,7 +366,6 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
   // 16·pb + (lane & 15), o = 16·i + 4·(lane >> 4) + r.
   constexpr int kEP = kSlots * 2 + 16;  // bytes per output-channel row of the staged tile
   static_assert(kOT * kEP <= kLdsOvfT, "staged output tile fits the freed LDS");
-  STAMP(6);
   __syncthreads();  // every wave is past its last B-tile read
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -532,380 +387,6 @@ __global__ __launch_bounds__(256, 2) void fwd_fused_bf16(Geo g, const bf16_t* __
     const int h = h0 + th, wc = w0 + 8 * half;
     if (h >= g.Ho || wc >= g.Wo) continue;
     const uint4 v = *reinterpret_cast<const uint4*>(lds + ol * kEP + (16 * th + 8 * half) * 2);
-    bf16_t* op = out + ((size_t)b * g.O + ob0 + ol) * g.HW + (size_t)h * g.Wo + wc;
-    if (wc + 8 <= g.Wo && ((reinterpret_cast<uintptr_t>(op) & 7) == 0)) {
-      *reinterpret_cast<uint2*>(op) = make_uint2(v.x, v.y);
-      *reinterpret_cast<uint2*>(op + 4) = make_uint2(v.z, v.w);
-    } else {
-      const unsigned e[4] = {v.x, v.y, v.z, v.w};
-      for (int j = 0; j < 8 && wc + j < g.Wo; ++j)
-        op[j] = (bf16_t)((e[j >> 1] >> (16 * (j & 1))) & 0xffffu);
-    }
-  }
-  STAMP(7);
-}
-
-// ---------------------------------------------------------------------------------------
-// r05: the same forward, two tiles per workgroup in ping-pong (FUSED_PP = 1 builds; slower than
-// fwd_fused_bf16 as measured, 0.175 vs 0.145 ms at config 4, kept for A/B: DESIGN.md §4.8).
-// fwd_fused_bf16 runs its gather and its MFMAs in the same phase on every wave of a CU (both
-// workgroups on a CU start together and run the same program), so on each SIMD the two waves
-// gather at the same time and multiply at the same time: the diagnostic builds measured the
-// gather (+28 µs) and the MFMAs (+24 µs) as purely additive, and the k loop at 1.36 µs per
-// 32-channel step against 0.43 µs of MFMA issue. Here one workgroup of 8 waves holds two
-// tiles, group 0 = waves 0-3 and group 1 = waves 4-7 (each SIMD hosts one wave of each), each
-// group with its own window / B tile / records in LDS. Between two workgroup barriers one
-// group gathers while the other multiplies, then they swap (cdna_hip_programming.md's 8-wave
-// ping-pong; MI355X_MICROARCH.md "Two waves per SIMD"): every wave runs gather(t), barrier,
-// multiply(t), barrier, group 1 one barrier behind group 0. A step is one tap of one
-// 32-channel slice (a [112 slots][32 channels] B tile, one k-step), so every B tile is
-// written once and read once between two barriers and one buffer per group suffices.
-// A gather segment is a single wave's VALU stream on its SIMD, so its instruction count sets
-// the pace: the window is kept in fp32 (the bf16 xT widened once per slice when it is staged),
-// which removes the 32 unpacking instructions of each 8-channel unit (52 -> 20 per unit).
-// A multiply segment issues the next step's weight fragments ahead of its own column stores
-// (half lines) and, at the last step of a slice,
-// stages the next slice's window (global loads issued at the segment's start, widened and
-// written to LDS after the MFMAs). Arithmetic and bits are fwd_fused_bf16's (same records,
-// same fp32 blend of the same corner values, same MFMA order per accumulator).
-constexpr int kPpCS = 32;                  // channels per slice (and per step)
-constexpr int kPpWPitch = kPpCS * 4 + 16;  // window: bytes per pixel (fp32 + 16 B pad)
-constexpr int kPpBPitch = kPpCS * 2 + 16;  // B tile: bytes per slot (bf16 + 16 B pad)
-constexpr int kPpUnits = kSlots * (kPpCS / 8);  // 8-channel units per step (448)
-constexpr int kPpWin = 0;
-constexpr int kPpB = kPpWin + kWPix * kPpWPitch;
-constexpr int kPpRecW = kPpB + kSlots * kPpBPitch;
-constexpr int kPpRecM = kPpRecW + kSlots * kMaxN * 16;
-constexpr int kPpOvfT = kPpRecM + kSlots * kMaxN * 4;
-constexpr int kPpOvfD = kPpOvfT + kOvf * 16;
-constexpr int kPpCnt = kPpOvfD + kOvf * kPpCS * 2;
-constexpr int kPpGroup = (kPpCnt + 16 + 127) / 128 * 128;  // one group's LDS
-constexpr int kPpEP = kSlots * 2 + 16;                      // epilogue: bytes per channel row
-constexpr int kPpWParts = kWPix * (kPpCS / 8);              // window: 16-B bf16 source parts
-constexpr int kPpWIt = (kPpWParts + 255) / 256;             // ... per thread
-static_assert(2 * kPpGroup <= 160 * 1024, "two tile groups in one workgroup's LDS");
-static_assert(kOT * kPpEP <= kPpGroup, "the staged output tile fits the group's LDS");
-
-// blend of 8 channels from fp32 corners (the op order of blend2: w0·a, then fmas of b, c, d)
-__device__ __forceinline__ unsigned blend2f(float4 wv, f32x2v a, f32x2v b, f32x2v c, f32x2v d) {
-  f32x2v v = f32x2v{wv.x, wv.x} * a;
-  v = __builtin_elementwise_fma(f32x2v{wv.y, wv.y}, b, v);
-  v = __builtin_elementwise_fma(f32x2v{wv.z, wv.z}, c, v);
-  v = __builtin_elementwise_fma(f32x2v{wv.w, wv.w}, d, v);
-  return (unsigned)f2bf(v.x) | ((unsigned)f2bf(v.y) << 16);
-}
-__device__ __forceinline__ f32x2v lo2v(float4 v) { return f32x2v{v.x, v.y}; }
-__device__ __forceinline__ f32x2v hi2v(float4 v) { return f32x2v{v.z, v.w}; }
-
-template <bool STORE>
-__global__ __launch_bounds__(512, 1) void fwd_fused_bf16_pp(Geo g, const bf16_t* __restrict__ xT,
-                                                            const float* __restrict__ off,
-                                                            const bf16_t* __restrict__ wfr,
-                                                            const float* __restrict__ bias,
-                                                            bf16_t* __restrict__ out,
-                                                            bf16_t* __restrict__ colT, int th_n,
-                                                            int tw_n, int ntiles) {
-  __shared__ __attribute__((aligned(1024))) char lds_all[2 * kPpGroup];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int grp = __builtin_amdgcn_readfirstlane(tid >> 8);  // wave-uniform
-  const int tg = tid & 255, wv = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
-  char* const lds = lds_all + grp * kPpGroup;
-  char* const win = lds + kPpWin;
-  char* const bt = lds + kPpB;
-  float4* const recw = reinterpret_cast<float4*>(lds + kPpRecW);
-  int* const recm = reinterpret_cast<int*>(lds + kPpRecM);
-  int4* const ovft = reinterpret_cast<int4*>(lds + kPpOvfT);
-  char* const ovfd = lds + kPpOvfD;
-  int* const cnt = reinterpret_cast<int*>(lds + kPpCnt);
-
-  // tile = ((ob·B + b)·th_n + th_i)·tw_n + tw_i; a workgroup takes tiles 2·wg and 2·wg + 1
-  // (neighbours: their windows overlap in L2); consecutive wg on one XCD
-  const unsigned nwg = gridDim.x, bid = blockIdx.x, q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
-  const int wg = (int)((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8);
-  const int tile = 2 * wg + grp;
-  const bool act = tile < ntiles;  // (an odd tile count leaves group 1 of the last wg idle)
-  const int tl = act ? tile : 0;
-  const int tw_i = tl % tw_n, th_i = (tl / tw_n) % th_n, b = (tl / (tw_n * th_n)) % g.B,
-            ob = tl / (tw_n * th_n * g.B);
-  const int h0 = th_i * kTH, w0 = tw_i * kTW;
-  const int o0 = ob * kOT + 64 * wv;
-  const int rlo = (int)floorf((float)w0 * (float)(g.H - 1) / (float)(g.Wo - 1)) - kMar;
-  const int qlo = (int)floorf((float)h0 * (float)(g.W - 1) / (float)(g.Ho - 1)) - kMar;
-  const bf16_t* const xb = xT + (size_t)b * g.HWi * g.C;
-  const int N = g.N, NKS = g.K / 32;
-  const int nslices = g.C / kPpCS, T = N * nslices;
-
-  // window slice cs: kWPix pixels × 4 parts of 8 bf16 channels (zeros outside the image) into
-  // registers, then widened to fp32 in LDS ([pixel][32 channels] at kPpWPitch)
-  auto win_load = [&](int cs, uint4 (&v)[kPpWIt]) {
-    int t2 = tg;
-    asm volatile("" : "+v"(t2));  // recomputed where used, not kept live across the loop
-#pragma unroll
-    for (int k = 0; k < kPpWIt; ++k) {
-      const int idx = t2 + k * 256;
-      const int pix = idx >> 2, part = idx & 3;
-      const int rr = pix / kWQ, qq = pix - rr * kWQ;
-      const int r = rlo + rr, q = qlo + qq;
-      const bool ok = idx < kPpWParts && r >= 0 && r < g.H && q >= 0 && q < g.W;
-      v[k] = ld16_if(xb + ((size_t)r * g.W + q) * g.C + kPpCS * cs + 8 * part, ok);
-    }
-  };
-  auto win_store = [&](const uint4 (&v)[kPpWIt]) {
-    int t2 = tg;
-    asm volatile("" : "+v"(t2));
-#pragma unroll
-    for (int k = 0; k < kPpWIt; ++k) {
-      const int idx = t2 + k * 256;
-      if (idx < kPpWParts) {
-        char* p = win + (idx >> 2) * kPpWPitch + (idx & 3) * 32;
-        const f32x2v a = unpack2(v[k].x), bq = unpack2(v[k].y), c = unpack2(v[k].z),
-                     d = unpack2(v[k].w);
-        *reinterpret_cast<float4*>(p) = make_float4(a.x, a.y, bq.x, bq.y);
-        *reinterpret_cast<float4*>(p + 16) = make_float4(c.x, c.y, d.x, d.y);
-      }
-    }
-  };
-  // overflow samples' 32-channel slices (novf entries × 4 units of 8 channels, bf16)
-  auto ovf_fill = [&](int cs, int novf) {
-    const int idx = tg;
-    if (idx < novf * 4) {
-      const int4 e = ovft[idx >> 2];
-      *reinterpret_cast<uint4*>(ovfd + (idx >> 2) * kPpCS * 2 + (idx & 3) * 16) =
-          gather_global(g, xb, e.x, e.y, kPpCS * cs + 8 * (idx & 3), recw[e.z]);
-    }
-  };
-
-  // ---- prologue: slice 0's window loads go out first, then the records (fwd_fused_bf16's)
-  {
-    uint4 wr[kPpWIt];
-    win_load(0, wr);
-    if (tg == 0) cnt[0] = 0;
-    __syncthreads();
-    if (act) {
-      for (int s = tg; s < kSlots * N; s += 256) {
-        const int p = s / N, n = s - p * N;
-        const int h = h0 + p / kTW, w = w0 + p % kTW;
-        int meta = kMZero;
-        float4 wq = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (h < g.Ho && w < g.Wo) {
-          const Tap t = sample_tap(g, off, b, 0, n, h * g.Wo + w);
-          if (t.ok) {
-            const float gr = 1.0f - t.fr, gc = 1.0f - t.fc;
-            wq = make_float4(gr * gc, gr * t.fc, t.fr * gc, t.fr * t.fc);
-            const int rr = t.r0 - rlo, qq = t.c0 - qlo;
-            if (rr >= 0 && rr + 1 < kWR && qq >= 0 && qq + 1 < kWQ) {
-              meta = rr * kWQ + qq;
-            } else {
-              const int j = atomicAdd(cnt, 1);  // any order: each entry is computed on its own
-              meta = -2 - j;
-              if (j < kOvf) ovft[j] = make_int4(t.r0, t.c0, p * kMaxN + n, 0);
-            }
-          }
-        }
-        recm[p * kMaxN + n] = meta;
-        recw[p * kMaxN + n] = wq;
-      }
-    }
-    win_store(wr);
-  }
-  __syncthreads();
-  const int novf = min(cnt[0], kOvf);
-  if (act) ovf_fill(0, novf);
-
-  f32x4 acc[4][kPB];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < kPB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // weight fragments of step t (tap n = t % N, slice cs = t / N): k-step (n·C + 32·cs) / 32
-  auto load_a = [&](int t, uint4 (&a)[4]) {
-    const int cs = t / N, n = t - cs * N;
-    const int ks = (n * g.C + kPpCS * cs) >> 5;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      a[i] = *reinterpret_cast<const uint4*>(
-          wfr + ((size_t)(((o0 >> 4) + i) * NKS + ks) * 64 + lane) * 8);
-  };
-  // gather segment of step t: its weight fragments, then the B tile: unit u = tg + 256k
-  // (u < 448): slot u >> 2, 8-channel group u & 3 (waves 0-2 of a group hold two units,
-  // wave 3 one). Every LDS read of a unit is issued before its blend (the record, then the
-  // eight 16-B corner pieces; a lane whose sample is not in the window reads pixel 0 and
-  // discards it).
-  auto produce = [&](int t) {
-    const int cs = t / N, n = t - cs * N;
-    int tgo = tg;
-    asm volatile("" : "+v"(tgo));
-    int meta[2];
-    float4 wq[2];
-    float4 cr[2][8];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int u = min(tgo + 256 * k, kPpUnits - 1), slot = u >> 2;
-      meta[k] = recm[slot * kMaxN + n];
-      wq[k] = recw[slot * kMaxN + n];
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int u = min(tgo + 256 * k, kPpUnits - 1), cg = u & 3;
-      const char* wp = win + max(meta[k], 0) * kPpWPitch + cg * 32;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const char* q = wp + (c == 0 ? 0 : c == 1 ? kPpWPitch : c == 2 ? kWQ * kPpWPitch
-                                                                       : (kWQ + 1) * kPpWPitch);
-        cr[k][2 * c] = *reinterpret_cast<const float4*>(q);
-        cr[k][2 * c + 1] = *reinterpret_cast<const float4*>(q + 16);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int u = tgo + 256 * k;
-      if (u < kPpUnits) {  // wave-uniform
-        const int slot = u >> 2, cg = u & 3, m = meta[k];
-        const float4 w4 = wq[k];
-        uint4 o = make_uint4(
-            blend2f(w4, lo2v(cr[k][0]), lo2v(cr[k][2]), lo2v(cr[k][4]), lo2v(cr[k][6])),
-            blend2f(w4, hi2v(cr[k][0]), hi2v(cr[k][2]), hi2v(cr[k][4]), hi2v(cr[k][6])),
-            blend2f(w4, lo2v(cr[k][1]), lo2v(cr[k][3]), lo2v(cr[k][5]), lo2v(cr[k][7])),
-            blend2f(w4, hi2v(cr[k][1]), hi2v(cr[k][3]), hi2v(cr[k][5]), hi2v(cr[k][7])));
-        if (m < 0) {  // no contribution, or an overflow sample
-          o = make_uint4(0u, 0u, 0u, 0u);
-          if (m != kMZero) {
-            const int j = -2 - m;
-            if (j < kOvf) {
-              o = *reinterpret_cast<const uint4*>(ovfd + j * kPpCS * 2 + cg * 16);
-            } else {  // more overflow samples than the area holds: corners from global memory
-              const int h = h0 + slot / kTW, w = w0 + slot % kTW;
-              const Tap tp = sample_tap(g, off, b, 0, n, h * g.Wo + w);
-              o = gather_global(g, xb, tp.r0, tp.c0, kPpCS * cs + 8 * cg, recw[slot * kMaxN + n]);
-            }
-          }
-        }
-        *reinterpret_cast<uint4*>(bt + slot * kPpBPitch + cg * 16) = o;
-      }
-    }
-  };
-  // step t's column pieces (slot, tap n, channels 32·cs .. +31: half a 128-B line), a fixed
-  // count of buffer stores per lane (slots past the tile or the map: an offset past the range)
-  const auto rsc = __builtin_amdgcn_make_buffer_rsrc(colT + (size_t)b * g.HW * g.K, 0,
-                                                     (int)((size_t)g.HW * g.K * 2), 0x00020000);
-  auto store_cols = [&](int t) {
-    const int cs = t / N, n = t - cs * N;
-    int tgo = tg;
-    asm volatile("" : "+v"(tgo));
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int u = tgo + 256 * k, sl = u >> 2, j = u & 3;
-      const int slr = min(sl, kSlots - 1);
-      const v4u v = *reinterpret_cast<const v4u*>(bt + slr * kPpBPitch + j * 16);
-      const int h = h0 + slr / kTW, w = w0 + slr % kTW;
-      const unsigned o = (sl < kSlots && h < g.Ho && w < g.Wo)
-                             ? ((unsigned)(h * g.Wo + w) * (unsigned)g.K +
-                                (unsigned)(n * g.C + kPpCS * cs + 8 * j)) * 2u
-                             : 0x80000000u;
-      __builtin_amdgcn_raw_buffer_store_b128(v, rsc, o, 0, FUSED_NT ? 2 : 0);
-    }
-  };
-  // multiply segment of step t: at a slice's last step the next slice's window loads first
-  // (this group read the old window for the last time in its previous segment), the MFMAs,
-  // the column stores, then (new slice) the window and the overflow slices into LDS
-  auto mult = [&](int t, const uint4 (&a)[4], uint4 (&an)[4]) {
-    const bool reload = (t + 1) % N == 0 && t + 1 < T;  // workgroup-uniform
-    uint4 wr[kPpWIt];
-    if (reload) win_load((t + 1) / N, wr);
-    const char* bb = bt + (lane & 15) * kPpBPitch + (lane >> 4) * 16;
-    bf16x8_t bv[kPB];
-#pragma unroll
-    for (int pb = 0; pb < kPB; ++pb)
-      bv[pb] = as_frag(*reinterpret_cast<const uint4*>(bb + pb * 16 * kPpBPitch));
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int pb = 0; pb < kPB; ++pb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        acc[i][pb] =
-            __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a[i]), bv[pb], acc[i][pb], 0, 0, 0);
-    // the next step's fragments before this step's stores: the wait for them at the next
-    // multiply segment then leaves the stores in flight (vmcnt retires in issue order)
-    load_a(min(t + 1, T - 1), an);
-    if (STORE) store_cols(t);
-    if (reload) {
-      win_store(wr);
-      ovf_fill((t + 1) / N, novf);
-    }
-  };
-
-  __syncthreads();  // windows, overflow slices and records of both groups in LDS
-#if FUSED_STAMP
-  // (diagnostic build) per group, wave 0: cycles in gather segments, multiply segments and
-  // barrier waits, summed over the loop (s_memtime), and the loop's wall time
-  unsigned long long c_prod = 0, c_mult = 0, c_bar = 0, c_t0 = __builtin_amdgcn_s_memtime(), c_a;
-#define PP_T0() c_a = __builtin_amdgcn_s_memtime()
-#define PP_ACC(v) (v) += __builtin_amdgcn_s_memtime() - c_a
-#else
-#define PP_T0() \
-  do {          \
-  } while (0)
-#define PP_ACC(v) \
-  do {            \
-  } while (0)
-#endif
-  // every wave runs gather(t), barrier, multiply(t), barrier; group 1 one barrier behind
-  // group 0, so each segment pairs one group's gather with the other's multiply
-  uint4 aE[4], aO[4];  // weight fragments of even / odd steps
-  load_a(0, aE);
-  if (grp == 1) __syncthreads();
-  auto step = [&](int t, const uint4 (&a)[4], uint4 (&an)[4]) {
-    PP_T0();
-    if (act) produce(t);
-    PP_ACC(c_prod);
-    PP_T0();
-    __syncthreads();
-    PP_ACC(c_bar);
-    PP_T0();
-    if (act) mult(t, a, an);
-    PP_ACC(c_mult);
-    PP_T0();
-    __syncthreads();
-    PP_ACC(c_bar);
-  };
-  for (int t = 0; t < T; t += 2) {
-    step(t, aE, aO);
-    if (t + 1 < T) step(t + 1, aO, aE);
-  }
-  if (grp == 0) __syncthreads();
-#if FUSED_STAMP
-  if (STORE && tg == 0 && blockIdx.x < kStampWg / 2) {
-    unsigned long long* st = g_fused_stamps + (blockIdx.x * 2 + grp) * kStamps;
-    st[0] = c_prod;
-    st[1] = c_mult;
-    st[2] = c_bar;
-    st[3] = __builtin_amdgcn_s_memtime() - c_t0;
-    st[4] = (unsigned long long)T;
-  }
-#endif
-
-  // ---- epilogue (fwd_fused_bf16's): bf16(acc + bias[o]) through the group's LDS as [o][slot]
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int ol = 64 * wv + 16 * i + 4 * (lane >> 4) + r;
-      const float bv = bias ? bias[ob * kOT + ol] : 0.f;
-#pragma unroll
-      for (int pb = 0; pb < kPB; ++pb)
-        *reinterpret_cast<bf16_t*>(lds + ol * kPpEP + (16 * pb + (lane & 15)) * 2) =
-            f2bf(acc[i][pb][r] + bv);
-    }
-  __syncthreads();
-  if (!act) return;  // (after the last barrier)
-  const int ob0 = ob * kOT;
-  for (int u = tg; u < kOT * kTH * 2; u += 256) {
-    const int half = u & 1, rest = u >> 1;
-    const int th = rest % kTH, ol = rest / kTH;
-    const int h = h0 + th, wc = w0 + 8 * half;
-    if (h >= g.Ho || wc >= g.Wo) continue;
-    const uint4 v = *reinterpret_cast<const uint4*>(lds + ol * kPpEP + (16 * th + 8 * half) * 2);
     bf16_t* op = out + ((size_t)b * g.O + ob0 + ol) * g.HW + (size_t)h * g.Wo + wc;
     if (wc + 8 <= g.Wo && ((reinterpret_cast<uintptr_t>(op) & 7) == 0)) {
       *reinterpret_cast<uint2*>(op) = make_uint2(v.x, v.y);
@@ -1218,7 +699,7 @@ bool fused_fwd_bf16_ok(const Geo& g) {
   return g.dt == DCN_BF16 && g.G == 1 && g.N <= kMaxN && g.C % kCS == 0 && g.O % kOT == 0 &&
          g.Ho >= 2 && g.Wo >= 2 && (long)g.O * g.K < lim &&
          (long)g.HW * g.K * 2 < lim &&  // an image's columns: 32-bit buffer byte offsets
-         (long)g.HWi * g.C * 2 < lim;   // an image's xT (the window loads, FUSED_WINBUF)
+         (long)g.HWi * g.C * 2 < lim;   // an image's xT (the window loads)
 }
 
 // r03 (tools/r03_fb_geo.py, fwd+bwd per step): fused faster wherever all
@@ -1243,17 +724,6 @@ hipError_t launch_fused_fwd_bf16(const Geo& g, const bf16_t* xT, const float* of
     hipLaunchKernelGGL(wf_to_frag16, dim3((unsigned)((nw / 8 + 255) / 256)), dim3(256), 0, s, w,
                        wfr, g.O, g.K);
   const int th_n = (g.Ho + kTH - 1) / kTH, tw_n = (g.Wo + kTW - 1) / kTW;
-  if (FUSED_PP) {
-    const int ntiles = th_n * tw_n * g.B * (g.O / kOT);
-    const dim3 grid((ntiles + 1) / 2);
-    if (colT)
-      hipLaunchKernelGGL(fwd_fused_bf16_pp<true>, grid, dim3(512), 0, s, g, xT, off, wfr, bias,
-                         out, colT, th_n, tw_n, ntiles);
-    else
-      hipLaunchKernelGGL(fwd_fused_bf16_pp<false>, grid, dim3(512), 0, s, g, xT, off, wfr, bias,
-                         out, colT, th_n, tw_n, ntiles);
-    return hipGetLastError();
-  }
   const dim3 grid(th_n * tw_n, g.B, g.O / kOT);
   if (colT)
     hipLaunchKernelGGL(fwd_fused_bf16<true>, grid, dim3(256), 0, s, g, xT, off, wfr, bias, out,
@@ -1304,13 +774,4 @@ hipError_t launch_fused_dw_bf16(const Geo& g, const bf16_t* xT, const float* off
 
 }  // namespace dcn
 
-#if FUSED_STAMP
-// (diagnostic builds only) the stamps of the last storing fused forward: n workgroups × 8
-extern "C" int dcn_debug_fused_stamps(unsigned long long* host, int n) {
-  if (n > dcn::kStampWg) n = dcn::kStampWg;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dcn::g_fused_stamps),
-                             sizeof(unsigned long long) * dcn::kStamps * n, 0,
-                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
-#endif
 

@@ -16,46 +16,24 @@
 #include "dcn_device.h"
 #include "dcn_swizzle.h"
 
-// A/B switch: 1 = the r04 FOLD staging loop (one load latency per item) in
-// offset_conv_fwd_mfma_bf16_row<SPT, true>
-#ifndef OFFC_FOLD_SERIAL
-#define OFFC_FOLD_SERIAL 0
-#endif
-// A/B switch: 1 = the r04 weight prefetch (one tap ahead, first tap after the staging)
 // r05 (config 4): two-row workgroups on the 3-tap weight ring, offset forward 0.0362-0.0369
 // -> 0.0338-0.0342 ms (one wave per SIMD at 296 registers, but no L2 wait per tap)
-#ifndef OFFC_RING2
-#define OFFC_RING2 1
-#endif
 #ifndef OFFC_KF2
 #define OFFC_KF2 14
 #endif
 #ifndef OFFC_ROWS
 #define OFFC_ROWS 2
 #endif
-#ifndef OFFC_W1
-#define OFFC_W1 0
-#endif
-// OFFC_STAMP = 1 (diagnostic A/B builds only): thread 0 of each workgroup of the folding
-// bf16 offset-conv forward records s_memrealtime (100 MHz) at its phase boundaries;
-// dcn_debug_offc_stamps copies them out (tools/offc_stamps.py)
-#ifndef OFFC_STAMP
-#define OFFC_STAMP 0
-#endif
-// A/B: offset_wgrad_bf16's x prefetch depth (steps) and ∂offset staging loads in flight
-// A/B (r05, config 4): the ∂W_off kernel on pre-split records gathered as bf16 pairs measured
+// r05 (config 4): the ∂W_off kernel on pre-split records gathered as bf16 pairs measured
 // 0.092-0.0926 ms for the offset backward against 0.0913-0.0916 on fp32 split in the loop
-// (its 32 two-byte LDS reads per step cost more than the split), so 0
+// (its 32 two-byte LDS reads per step cost more than the split), so it splits in the loop
 // r05 (config 4): the ∂x kernel on the side stream beside ∂W_off + its fold (they share
 // only their inputs): offset backward 0.0914-0.092 -> 0.0896-0.0901 ms
 #ifndef OFFB_CONC
 #define OFFB_CONC 1
 #endif
-#ifndef OFFW_PRESPLIT
-#define OFFW_PRESPLIT 0
-#endif
 // r05 (config 4): the ∂x kernel on pre-split records, offset backward 0.0944-0.0951 ->
-// 0.092-0.0926 ms (k loop 11.3 -> 7.9 us per workgroup, tools/offc_stamps.py)
+// 0.092-0.0926 ms (k loop 11.3 -> 7.9 us per workgroup, r05 phase stamps)
 // ∂x kernel: Wc fragments kPf - 1 k-steps ahead (r05, config 4: 3 -> 5, offset backward
 // 0.0913-0.0921 -> 0.0895-0.0905 ms; 135 registers)
 // fp32 ∂x kernel (offset_dgrad_mfma): weight fragments kPf steps ahead (r05, config 3: 3 and 4
@@ -65,12 +43,6 @@
 #endif
 #ifndef OFFD_PF
 #define OFFD_PF 5
-#endif
-#ifndef OFFD_PRESPLIT
-#define OFFD_PRESPLIT 1
-#endif
-#ifndef OFFD_EPI
-#define OFFD_EPI 0
 #endif
 // r05 (config 4): two channel groups per ∂W_off workgroup, offset backward 0.0921-0.0933 ->
 // 0.0899-0.0908 ms (the shared ∂offset staging is half the instructions per channel)
@@ -1189,19 +1161,6 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16(
 // block writes its own input row (window row ph: stride 1, Ho == H) to xT — the channels-last
 // copy K1 / the fused forward / K5 read — so x is read in one pass and the separate transpose
 // launch disappears, as offset_conv_fwd_mfma_xt does for fp32 (offset_fwd_bf16_fold_ok).
-#if OFFC_STAMP
-constexpr int kOStampWg = 4096, kOStamps = 8;
-__device__ unsigned long long g_offc_stamps[kOStampWg * kOStamps];
-#define OSTAMP(i)                                                                     \
-  do {                                                                                \
-    if (FOLD && threadIdx.x == 0 && ostamp_wg < kOStampWg)                            \
-      g_offc_stamps[ostamp_wg * kOStamps + (i)] = __builtin_amdgcn_s_memrealtime();    \
-  } while (0)
-#else
-#define OSTAMP(i) \
-  do {            \
-  } while (0)
-#endif
 // ROWS (FOLD only, r05): output rows per block; the window holds kh + ROWS - 1 input rows,
 // so x leaves L2 (kh + ROWS - 1) / ROWS times instead of kh times, and each weight fragment
 // loaded serves ROWS rows (config 4 measured the staging as the bandwidth-bound phase).
@@ -1223,10 +1182,6 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
   const int KHR = KH + ROWS - 1;  // staged window rows
   bf16_t* L = reinterpret_cast<bf16_t*>(smem_row) + (size_t)w * KHR * SWc * P;
   const int cw = w * SPT * 16;  // this wave's first channel
-#if OFFC_STAMP
-  const int ostamp_wg = blk.z * gridDim.x + blk.x;
-#endif
-  OSTAMP(0);
   // B = weight fragments (L2-resident) in a 3-tap register ring; r05: the first two taps
   // are requested before the window staging, so their latency hides behind it, and the
   // loop keeps two taps in flight (one ahead waited an L2 latency per tap)
@@ -1237,11 +1192,9 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
 #pragma unroll
     for (int u = 0; u < SPT; ++u) rb[u] = ld_bf16x8(wp + 512 * u);
   };
-  // (two-row blocks: one tap ahead, loaded after the staging — their 8 MFMAs per tap cover
-  // more of the L2 latency, and the registers are the occupancy limit)
-  // OFFC_RING2 (A/B): two-row workgroups on the 3-tap ring too, loaded after the staging
-  constexpr bool kW1 = OFFC_W1 || (ROWS > 1 && !OFFC_RING2);
-  if constexpr (!kW1 && ROWS == 1) {
+  // (two-row workgroups: the first two taps are requested after the staging, as the
+  // registers are the occupancy limit)
+  if constexpr (ROWS == 1) {
     ldb(0, bv[0]);
     ldb(1, bv[1]);
   }
@@ -1254,27 +1207,9 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
     __builtin_amdgcn_wave_barrier();
     const int NQ = g.W / 4, x0 = -g.pw;  // wo0 == 0 (tpr == 1)
     const int nit = 8 * SPT * KHR * NQ;
-#if OFFC_FOLD_SERIAL
-    const bf16_t* xb = x_nchw + (size_t)b * g.C * g.HWi;
-    for (int it = lane; it < nit; it += 64) {
-      const int q = it % NQ, rest = it / NQ;
-      const int i = rest % KH, cp = rest / KH;
-      const int y = ho - g.ph + i, c = cw + 2 * cp;
-      if (y < 0 || y >= g.H || c >= g.C) continue;
-      const bf16_t* p0 = xb + ((size_t)c * g.H + y) * g.W + 4 * q;
-      const uint2 u0 = *reinterpret_cast<const uint2*>(p0);
-      const uint2 u1 = *reinterpret_cast<const uint2*>(p0 + g.HWi);
-      unsigned* d = reinterpret_cast<unsigned*>(L + (i * SWc + 4 * q - x0) * P + 2 * cp);
-      constexpr int PW = P / 2;  // pixel pitch in 32-bit words
-      d[0] = (u0.x & 0xffffu) | (u1.x << 16);
-      d[PW] = (u0.x >> 16) | (u1.x & 0xffff0000u);
-      d[2 * PW] = (u0.y & 0xffffu) | (u1.y << 16);
-      d[3 * PW] = (u0.y >> 16) | (u1.y & 0xffff0000u);
-    }
-#else
     // r05: a lane's items all in flight at once (kF per batch: one batch for kh = 3,
     // W <= 32, C = 256), through a buffer resource, so rows outside the image and channels
-    // past C read zeros and every LDS store is unconditional (the serial loop above waited
+    // past C read zeros and every LDS store is unconditional (r04's serial loop waited
     // one memory latency per item, ~10 per block at config 4). A slot past nit repeats item
     // nit-1 (same value, same place).
     const auto rxn = __builtin_amdgcn_make_buffer_rsrc(
@@ -1312,9 +1247,7 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
         d[3 * PW] = (u0[u].y >> 16) | (u1[u].y & 0xffff0000u);
       }
     }
-#endif
     __builtin_amdgcn_wave_barrier();
-    OSTAMP(1);
     // input rows ho.. (window rows ph..) -> xT[b][ho][px][cw ..]: 16-B runs of 8 channels
     const int nch = min(16 * SPT, g.C - cw);
 #pragma unroll
@@ -1329,7 +1262,6 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
                                   8 * ch8) = v;
       }
     }
-    OSTAMP(2);
   } else {
     const auto rx = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<bf16_t*>(xT + (size_t)b * g.HWi * g.C), 0, (int)((size_t)g.HWi * g.C * 2),
@@ -1359,7 +1291,7 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
         if (dst[u] >= 0) *reinterpret_cast<uint4*>(L + dst[u]) = v[u];
     }
   }
-  if constexpr (!kW1 && ROWS > 1) {
+  if constexpr (ROWS > 1) {
     ldb(0, bv[0]);
     ldb(1, bv[1]);
   }
@@ -1386,16 +1318,6 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
         acc[rr] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[u], rb[u], acc[rr], 0, 0, 0);
     }
   };
-  if constexpr (kW1) {
-    ldb(0, bv[0]);
-    for (int t = 0; t < KK; t += 2) {
-      ldb(t + 1, bv[1]);
-      mma(t, bv[0]);
-      if (t + 1 >= KK) break;
-      ldb(t + 2, bv[0]);
-      mma(t + 1, bv[1]);
-    }
-  } else {
   for (int t = 0; t < KK; t += 3) {
     ldb(t + 2, bv[2]);
     mma(t, bv[0]);
@@ -1406,16 +1328,13 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
     ldb(t + 4, bv[1]);
     mma(t + 2, bv[2]);
   }
-  }
   // fold the 4 channel partials in wave order through the (now free) window LDS
   __syncthreads();
-  OSTAMP(3);
   f32x16* red = reinterpret_cast<f32x16*>(smem_row);
   f32x16 sum;
   if constexpr (ROWS == 1) {
     if (w > 0) red[(w - 1) * 64 + lane] = acc[0];
     __syncthreads();
-    OSTAMP(4);
     if (w != 0) return;
     sum = acc[0];
 #pragma unroll
@@ -1430,7 +1349,6 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
 #pragma unroll
     for (int rr = 0; rr < ROWS; ++rr) red[(rr * 4 + w) * 64 + lane] = acc[rr];
     __syncthreads();
-    OSTAMP(4);
     if (w >= ROWS || ho + w >= g.Ho) return;
     sum = red[(w * 4) * 64 + lane];
 #pragma unroll
@@ -1456,7 +1374,6 @@ __global__ __launch_bounds__(256) void offset_conv_fwd_mfma_bf16_row(
       off[o] = f2bf(v);  // exact: v is a bf16 value
     }
   }
-  OSTAMP(5);
 }
 
 // LDS bytes of offset_conv_fwd_mfma_bf16_row (0: the row kernel does not apply)
@@ -1688,19 +1605,6 @@ __device__ __forceinline__ void split8(const float (&v)[8], bf16x8_t& hi, bf16x8
 // bf16 NCHW (the API's grad_x). r04: the epilogue reads and writes through buffer resources
 // (32-bit offsets), which cut 160 VGPRs + 64 AGPRs to 121 registers: 4 workgroups per CU
 // instead of 2, so config 4's 832 workgroups run in one round.
-#if OFFC_STAMP
-__device__ unsigned long long g_offd_stamps[kOStampWg * kOStamps];
-__device__ unsigned long long g_offw_stamps[kOStampWg * kOStamps];
-#define BSTAMP(arr, wg, i)                                                     \
-  do {                                                                         \
-    if (threadIdx.x == 0 && (wg) < kOStampWg)                                  \
-      arr[(wg) * kOStamps + (i)] = __builtin_amdgcn_s_memrealtime();           \
-  } while (0)
-#else
-#define BSTAMP(arr, wg, i) \
-  do {                     \
-  } while (0)
-#endif
 __global__ __launch_bounds__(256, 3) void offset_dgrad_bf16(Geo g, const bf16_t* __restrict__ wc,
                                                         int KT16, const float* __restrict__ goff,
                                                         const float* __restrict__ gxT_in,
@@ -1731,8 +1635,6 @@ __global__ __launch_bounds__(256, 3) void offset_dgrad_bf16(Geo g, const bf16_t*
   };
 #pragma unroll
   for (int d = 0; d < kPf - 1; ++d) lda(d, d);
-  BSTAMP(g_offd_stamps, bid, 0);
-#if OFFD_PRESPLIT
   // pre-split hi/lo records (PB = 2·PJ bf16 per pixel) and, past the staged rows, the k-step
   // table: tab[2·ks + hh] = the bf16 offset of step ks's 8 k of half hh (toff8 + j0), or -1
   // for the K padding (zero operands)
@@ -1745,22 +1647,14 @@ __global__ __launch_bounds__(256, 3) void offset_dgrad_bf16(Geo g, const bf16_t*
     const int t = k / J8, j0 = k - t * J8;
     tab[threadIdx.x] = k < KT ? toff8(g, t, SW, PB) + j0 : -1;
   }
-#else
-  stage_goff8(g, goff, b, y0, y1 - y0 + 1 + (g.kh - 1) * g.dh, SW, J8, PJ, S);
-#endif
   __syncthreads();
-  BSTAMP(g_offd_stamps, bid, 1);
   const bool live = cw < g.C;  // (C < 256: idle waves still meet the epilogue barrier)
   int base[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int p = p0 + min(32 * u + r, np - 1);
     const int y = p / g.W, x = p - y * g.W;
-#if OFFD_PRESPLIT
     base[u] = ((y - y0) * SW + x) * PB;
-#else
-    base[u] = ((y - y0) * SW + x) * PJ;
-#endif
   }
   f32x16 acc[2][2];
 #pragma unroll
@@ -1775,7 +1669,6 @@ __global__ __launch_bounds__(256, 3) void offset_dgrad_bf16(Geo g, const bf16_t*
       const int ks = ks0 + d;
       lda(ks + kPf - 1, (d + kPf - 1) % kPf);
       __builtin_amdgcn_sched_barrier(0);
-#if OFFD_PRESPLIT
       if (ks < NKS) {  // wave-uniform
         const int e = tab[2 * ks + hh];
         bf16x8_t bh[2], bl[2];
@@ -1804,40 +1697,12 @@ __global__ __launch_bounds__(256, 3) void offset_dgrad_bf16(Geo g, const bf16_t*
           acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra1[d], bl[u], acc[1][u], 0, 0, 0);
         }
       }
-#else
-      if (ks < NKS) {  // wave-uniform
-        const int k = 16 * ks + 8 * hh;  // this lane's 8 k: one tap, channels j0..j0+7
-        const bool kin = k < KT;  // the K padding step: zero operands (Wc is 0 there too)
-        const int kc = kin ? k : 0;
-        const int t = kc / J8, j0 = kc - t * J8;
-        const unsigned keep = kin ? 0xffffffffu : 0u;
-        bf16x8_t bh[2], bl[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const float4* sp =
-              reinterpret_cast<const float4*>(S + base[u] + toff8(g, t, SW, PJ) + j0);
-          const float4 q0 = sp[0], q1 = sp[1];
-          float v[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = __uint_as_float(__float_as_uint(v[e]) & keep);
-          split8(v, bh[u], bl[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra0[d], bh[u], acc[0][u], 0, 0, 0);
-          acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra1[d], bh[u], acc[1][u], 0, 0, 0);
-          acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra0[d], bl[u], acc[0][u], 0, 0, 0);
-          acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ra1[d], bl[u], acc[1][u], 0, 0, 0);
-        }
-      }
-#endif
     }
   }
   // ∂x = the sampling route (channels-last gxT_in) + D, as bf16 NCHW. gxT_in is read as
   // whole 256-B pixel rows (this wave's 64 channels) into LDS and read back per D lane
   // (pixel r, channel of register i); the bf16 stores are 64-B pixel runs per channel.
   __syncthreads();  // every wave is done with S: its space holds the transposes
-  BSTAMP(g_offd_stamps, bid, 2);
   if (!live) return;
   float* T = S + w * 32 * kDgTP;
   const auto rgx = __builtin_amdgcn_make_buffer_rsrc(gx + (size_t)b * g.C * g.HWi, 0,
@@ -1845,29 +1710,10 @@ __global__ __launch_bounds__(256, 3) void offset_dgrad_bf16(Geo g, const bf16_t*
   const auto rgt = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(gxT_in + (size_t)b * g.HWi * g.C), 0, (int)((size_t)g.HWi * g.C * 4),
       0x00020000);
-#if OFFD_EPI
-  // r05: both halves' 16 gxT loads in flight together (the r04 order waited four times)
-  float4 tva[2][2][4];
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int h2 = 0; h2 < 2; ++h2)
-#pragma unroll
-      for (int it = 0; it < 4; ++it) {
-        const int pl = min(32 * u + 4 * (4 * h2 + it) + (lane >> 4), np - 1);
-        const auto q = __builtin_amdgcn_raw_buffer_load_b128(
-            rgt, (unsigned)(((p0 + pl) * g.C + cw + 4 * (lane & 15)) * 4), 0, 0);
-        tva[u][h2][it] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]),
-                                     __uint_as_float(q[2]), __uint_as_float(q[3]));
-      }
-#endif
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
 #pragma unroll
     for (int h2 = 0; h2 < 2; ++h2) {
-#if OFFD_EPI
-      const float4(&tv)[4] = tva[u][h2];
-#else
       float4 tv[4];
 #pragma unroll
       for (int it = 0; it < 4; ++it) {
@@ -1877,7 +1723,6 @@ __global__ __launch_bounds__(256, 3) void offset_dgrad_bf16(Geo g, const bf16_t*
         tv[it] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]),
                              __uint_as_float(q[3]));
       }
-#endif
 #pragma unroll
       for (int it = 0; it < 4; ++it)
         *reinterpret_cast<float4*>(T + (4 * (4 * h2 + it) + (lane >> 4)) * kDgTP + 4 * (lane & 15)) = tv[it];
@@ -1901,7 +1746,6 @@ __global__ __launch_bounds__(256, 3) void offset_dgrad_bf16(Geo g, const bf16_t*
     }
     __builtin_amdgcn_wave_barrier();  // the next half overwrites T
   }
-  BSTAMP(g_offd_stamps, bid, 3);
 }
 
 // ∂w_off partials: block = (chunk of rowsB input rows of one image, 64 channels); wave w
@@ -1940,11 +1784,7 @@ __global__ __launch_bounds__(256 * CGB) void offset_wgrad_bf16(Geo g, const bf16
     const int kk = 32 * (w + 4 * u) + r;
     const bool kok = kk < KT;
     const int t = kk / J8, j = kk - t * J8;
-#if OFFW_PRESPLIT
-    kofs[u] = kok ? toff8(g, t, SW, 2 * PJ) + j : 0;  // bf16 units of the pre-split records
-#else
     kofs[u] = kok ? toff8(g, t, SW, PJ) + j : 0;
-#endif
     kmask[u] = kok ? 0xffffffffu : 0u;
   }
   // the block sums cpb consecutive chunks (of any images) into one partial: fewer partial
@@ -1977,17 +1817,9 @@ __global__ __launch_bounds__(256 * CGB) void offset_wgrad_bf16(Geo g, const bf16
   };
 #pragma unroll
   for (int d = 0; d < kPf - 1; ++d) lda(d, d);
-  if (ci == 0) BSTAMP(g_offw_stamps, blockIdx.y * gridDim.x + blockIdx.x, 0);
-  if (ci == 1) BSTAMP(g_offw_stamps, blockIdx.y * gridDim.x + blockIdx.x, 2);
   if (ci > 0) __syncthreads();  // the previous chunk's staged rows are no longer read
-#if OFFW_PRESPLIT
-  stage_goff8_split<OFFW_SG>(g, goff, b, y0, nrows + (g.kh - 1) * g.dh, SW, J8, 2 * PJ,
-                             reinterpret_cast<bf16_t*>(S));
-#else
   stage_goff8<OFFW_SG>(g, goff, b, y0, nrows + (g.kh - 1) * g.dh, SW, J8, PJ, S);
-#endif
   __syncthreads();
-  if (ci < 2) BSTAMP(g_offw_stamps, blockIdx.y * gridDim.x + blockIdx.x, 1 + 2 * ci);
   // (row, column) in the chunk of this lane's first pixel q = 16i + 8hh: q and W are
   // multiples of 4, so pixels q..q+3 share a row, as do q+4..q+7
   int yq = (8 * hh) / g.W, xq = 8 * hh - yq * g.W;
@@ -2003,37 +1835,6 @@ __global__ __launch_bounds__(256 * CGB) void offset_wgrad_bf16(Geo g, const bf16
         const int q = 16 * i + 8 * hh;
         // pixels past the chunk read a staged row in range (S[0..]) and are masked to zero
         const bool ok0 = q < npx, ok1 = q + 4 < npx;
-#if OFFW_PRESPLIT
-        // r05: pre-split records (stage_goff8_split), so the step only gathers bf16 pairs:
-        // 64 -> ~20 VALU per step. The padding K columns (kmask) need no zeroing here: their
-        // accumulator columns are never stored, and MFMA columns do not mix.
-        const int PB = 2 * PJ;
-        const unsigned short* Sb = reinterpret_cast<const unsigned short*>(S);
-        const int s0 = ok0 ? (yq * SW + xq) * PB : 0;
-        const int s1 = !ok1 ? 0 : xq + 4 < g.W ? s0 + 4 * PB : (yq + 1) * SW * PB;
-        bf16x8_t bh[2], bl[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          uint4 hq, lq;
-          const unsigned short* a0 = Sb + s0 + kofs[u];
-          const unsigned short* a1 = Sb + s1 + kofs[u];
-          hq.x = (unsigned)a0[0] | ((unsigned)a0[PB] << 16);
-          hq.y = (unsigned)a0[2 * PB] | ((unsigned)a0[3 * PB] << 16);
-          hq.z = (unsigned)a1[0] | ((unsigned)a1[PB] << 16);
-          hq.w = (unsigned)a1[2 * PB] | ((unsigned)a1[3 * PB] << 16);
-          lq.x = (unsigned)a0[J8] | ((unsigned)a0[PB + J8] << 16);
-          lq.y = (unsigned)a0[2 * PB + J8] | ((unsigned)a0[3 * PB + J8] << 16);
-          lq.z = (unsigned)a1[J8] | ((unsigned)a1[PB + J8] << 16);
-          lq.w = (unsigned)a1[2 * PB + J8] | ((unsigned)a1[3 * PB + J8] << 16);
-          if (16 * i + 16 > npx) {  // wave-uniform: only a chunk's last step can be ragged
-            const unsigned m0 = ok0 ? 0xffffffffu : 0u, m1 = ok1 ? 0xffffffffu : 0u;
-            hq.x &= m0, hq.y &= m0, hq.z &= m1, hq.w &= m1;
-            lq.x &= m0, lq.y &= m0, lq.z &= m1, lq.w &= m1;
-          }
-          bh[u] = __builtin_bit_cast(bf16x8_t, hq);
-          bl[u] = __builtin_bit_cast(bf16x8_t, lq);
-        }
-#else
         const int s0 = ok0 ? (yq * SW + xq) * PJ : 0;
         const int s1 = !ok1 ? 0 : xq + 4 < g.W ? s0 + 4 * PJ : (yq + 1) * SW * PJ;
         const unsigned m0 = ok0 ? 0xffffffffu : 0u, m1 = ok1 ? 0xffffffffu : 0u;
@@ -2049,7 +1850,6 @@ __global__ __launch_bounds__(256 * CGB) void offset_wgrad_bf16(Geo g, const bf16
           }
           split8(v, bh[u], bl[u]);
         }
-#endif
         xq += 16;
         while (xq >= g.W) xq -= g.W, ++yq;
 #pragma unroll
@@ -2063,7 +1863,6 @@ __global__ __launch_bounds__(256 * CGB) void offset_wgrad_bf16(Geo g, const bf16
     }
   }
   }  // chunks
-  BSTAMP(g_offw_stamps, blockIdx.y * gridDim.x + blockIdx.x, 4);
   // partials in MFMA fragment order (each lane's 16 accumulators are 64 contiguous bytes,
   // a wave's tile one 4 KiB run): part[(((chunk·CG + cg)·NT + tile)·2 + m)·64 + lane][16]
   // with NT = ceil(KT/32) tiles; wgrad_frag_reduce folds the chunks and scatters to ∂w_off
@@ -2084,7 +1883,6 @@ __global__ __launch_bounds__(256 * CGB) void offset_wgrad_bf16(Geo g, const bf16
                         acc[m][u][4 * q + 3]);
     }
   }
-  BSTAMP(g_offw_stamps, blockIdx.y * gridDim.x + blockIdx.x, 5);
 }
 
 // ∂w_off[j][c][t] = Σ_chunk (fragment-ordered partials of offset_wgrad_bf16), chunks in
@@ -2892,20 +2690,3 @@ hipError_t launch_ocg_col2im(const Geo& g, const float* docol, const float* gxT_
 
 }  // namespace dcn
 
-#if OFFC_STAMP
-// (diagnostic builds only) the stamps of the last folding bf16 offset-conv forward
-extern "C" int dcn_debug_offc_stamps(unsigned long long* host, int n) {
-  if (n > dcn::kOStampWg) n = dcn::kOStampWg;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dcn::g_offc_stamps),
-                             sizeof(unsigned long long) * dcn::kOStamps * n, 0,
-                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
-// which: 0 = the folding forward, 1 = offset_dgrad_bf16, 2 = offset_wgrad_bf16
-extern "C" int dcn_debug_offc_stamps2(int which, unsigned long long* host, int n) {
-  if (n > dcn::kOStampWg) n = dcn::kOStampWg;
-  const void* sym = which == 1 ? HIP_SYMBOL(dcn::g_offd_stamps)
-                  : which == 2 ? HIP_SYMBOL(dcn::g_offw_stamps) : HIP_SYMBOL(dcn::g_offc_stamps);
-  return hipMemcpyFromSymbol(host, sym, sizeof(unsigned long long) * dcn::kOStamps * n, 0,
-                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
-#endif

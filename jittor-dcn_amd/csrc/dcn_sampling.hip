@@ -39,26 +39,6 @@ void set_force_generic(int on) { g_force_generic = on; }
 #define BINS_CHUNKED 0  // (an A/B build sets 1: tools/ab.sh)
 #endif
 static int g_bins_chunked = BINS_CHUNKED;
-// K5_STAMP = 1 (diagnostic A/B builds only): thread 0 of every bf16 col2im_tile workgroup
-// records s_memrealtime at its phase boundaries; dcn_debug_k5_stamps copies them out
-#ifndef K5_STAMP
-#define K5_STAMP 0
-#endif
-#if K5_STAMP
-constexpr int kK5StampWg = 4096;
-__device__ unsigned long long g_k5_stamps[kK5StampWg * 8];
-#define K5ST(i)                                                                              \
-  do {                                                                                       \
-    if (sizeof(XT) == 2 && threadIdx.x == 0) {                                               \
-      const unsigned wgl = blockIdx.x + gridDim.x * blockIdx.z;                              \
-      if (wgl < kK5StampWg) g_k5_stamps[wgl * 8 + (i)] = __builtin_amdgcn_s_memrealtime();    \
-    }                                                                                        \
-  } while (0)
-#else
-#define K5ST(i) \
-  do {          \
-  } while (0)
-#endif
 void set_bins_chunked(int on) { g_bins_chunked = on; }
 int get_force_generic() { return g_force_generic; }
 
@@ -941,7 +921,6 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const Block3 blk = xcd_block();
-  K5ST(0);
   const int bl = blk.z, b = b0 + bl;
   const int tr_i = blk.x / tq_n, tq_i = blk.x - tr_i * tq_n;
   const int R0 = tr_i * kTR, Q0 = tq_i * kTQ;
@@ -1059,7 +1038,6 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
     if (tid + k * kC2iThreads < WIN) lds[tid + k * kC2iThreads] = wv[k];
   for (int k = tid; k < ZR; k += kC2iThreads) lwin[k] = WinT{};
   lds_barrier();
-  K5ST(1);
   // the samples [rlo, rhi) of bin columns BJ0..BJ1-1, segment by segment (the first segment
   // already loaded and issued)
   auto phase = [&](auto BJ0, auto BJ1, int rlo, int rhi) __attribute__((always_inline)) {
@@ -1168,7 +1146,6 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
     rowhi_c = rhi0;
     phase(std::integral_constant<int, 0>(), std::integral_constant<int, 1>(), rowlo, rhi0);
   }
-  K5ST(2);
   if (act && tq_i > 0 && cok) {  // bin column Q0 is done: its left boundary partials
     const size_t rs = (size_t)tq_n * 2 * g.C;  // pixel-row stride
     float* cp = cpart + (size_t)bl * g.H * rs + (size_t)tq_i * 2 * g.C + c;
@@ -1183,7 +1160,6 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
     }
     phase(std::integral_constant<int, 1>(), std::integral_constant<int, kTQ + 1>(), mid, rowhi);
   }
-  K5ST(3);
   __syncthreads();  // window no longer read: reuse the LDS for the upper rows
   if (w >= 1)
 #pragma unroll
@@ -1196,7 +1172,7 @@ __global__ __launch_bounds__((kTR + 1) * 64) __attribute__((amdgpu_waves_per_eu(
       if (Q0 + j < g.W)
         *reinterpret_cast<float4*>(gxT + (((size_t)b * g.H + r) * g.W + Q0 + j) * g.C + c) =
             add4(dn[j], lds_[(w * kTQ + j) * 64 + lane]);
-  }  K5ST(4);
+  }
 }
 
 // ∂xT of the last pixel column of each tile column but the last += the boundary partials the
@@ -1796,12 +1772,4 @@ hipError_t launch_col2im_bf16(const Geo& g, const bf16_t* xT, const float* off,
 
 }  // namespace dcn
 
-#if K5_STAMP
-// (diagnostic builds only) the stamps of the last bf16 K5 launch: n workgroups × 8
-extern "C" int dcn_debug_k5_stamps(unsigned long long* host, int n) {
-  if (n > dcn::kK5StampWg) n = dcn::kK5StampWg;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dcn::g_k5_stamps), sizeof(unsigned long long) * 8 * n, 0,
-                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
-#endif
 
