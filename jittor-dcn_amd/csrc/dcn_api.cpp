@@ -22,6 +22,9 @@
 #ifndef OFFB_CONC
 #define OFFB_CONC 1
 #endif
+#ifndef OFFB_CONC_F32
+#define OFFB_CONC_F32 1  // (A/B builds: 0 = the fp32 offset-conv ∂x after ∂W_off, r05's order)
+#endif
 
 using dcn::Geo;
 
@@ -701,9 +704,12 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
     if (dcol_k) pb.add(dcn::prep_dcol(g.K, w, BF(L.wz)));
     HIP_TRY(dcn::launch_prep_bf16(pb, st));
   }
+  // the sample bins (K5's input) on the side stream from here on. (r06 A/B at config 4: the
+  // sort's 64 workgroups hold 100 KiB of LDS each and keep ≈60 of dw_stream_bf16's 252
+  // one-per-CU workgroups waiting ≈25 µs; launched after ∂W instead, beside the ∂col product,
+  // ∂W's scope went 0.101 -> 0.096 ms but ∂col's 0.079 -> 0.106 ms, so they stay here.)
   DCN_TRY(fork_aux(h));
-  HIP_TRY(dcn::launch_bins(g, off32, base + L.bins, goff32, 0, g.B,
-                           h->aux));
+  HIP_TRY(dcn::launch_bins(g, off32, base + L.bins, goff32, 0, g.B, h->aux));
   // f2 without a column matrix (DCN_FWD_FUSED_NOCOL): ∂W with the columns recomputed from
   // xT inside the MFMA kernel, so the ∂columns are the only large buffer of the step
   const bool dw_fused = !col_valid && h->fwd_path == DCN_FWD_FUSED_NOCOL &&
@@ -1287,7 +1293,8 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
       HIP_TRY(dcn::launch_offset_conv_bwd(g, x, F(L.xT), w_off, goff, F(L.goffT), F(L.wt), grad_x,
                                           grad_w_off, nullptr,
                                           dcn::get_force_generic() ? nullptr : F(L.gxT),
-                                          h->stream));
+                                          h->stream, OFFB_CONC_F32 ? h->aux : nullptr,
+                                          h->fork_ev, h->join_ev));
     }
     DCN_TRY(join_aux(h));
   }

@@ -127,7 +127,8 @@ hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16
 hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
                                   const float* w_off, const float* goff, float* goffT, float* wt2,
                                   float* gx, float* gw_off, float* gb_off, const float* gxT_in,
-                                  hipStream_t s);
+                                  hipStream_t s, hipStream_t aux = nullptr,
+                                  hipEvent_t fork = nullptr, hipEvent_t join = nullptr);
 // The MFMA offset-conv backward (stride 1) in pieces, so that batch chunk k's ∂W_off / ∂x
 // can run on a side stream beside chunk k+1's col2im: prep (w_off transpose) once,
 // chunk(b0, nb) per image range (after that range's ∂offset exists), finish once (∂W_off
@@ -150,7 +151,8 @@ hipError_t launch_offset_bwd_prep(const Geo& g, const float* w_off, float* wt2, 
 // xT: the fp32 channels-last x, or (xT_bf16) the bf16 one of DCN_BF16.
 hipError_t launch_offset_bwd_chunk(const Geo& g, const void* xT, bool xT_bf16, const float* goff,
                                    float* goffT, const float* wt2, float* gx,
-                                   const float* gxT_in, int b0, int nb, hipStream_t s);
+                                   const float* gxT_in, int b0, int nb, hipStream_t s,
+                                   hipStream_t s_dx = nullptr);
 hipError_t launch_offset_bwd_finish(const Geo& g, const float* goff, const float* goffT,
                                     float* gw_off, float* gb_off, hipStream_t s);
 // dcn_reduce.hip conversions: bf16 <-> f32 (RNE), and the bf16 rounding of a f32 tensor

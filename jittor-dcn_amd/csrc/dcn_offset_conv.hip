@@ -2396,10 +2396,12 @@ hipError_t launch_offset_bwd_prep(const Geo& g, const float* w_off, float* wt2, 
 // xT: fp32 channels-last x, or (xT_bf16) the bf16 one.
 hipError_t launch_offset_bwd_chunk(const Geo& g, const void* xT, bool xT_bf16, const float* goff,
                                    float* goffT, const float* wt2, float* gx,
-                                   const float* gxT_in, int b0, int nb, hipStream_t s) {
+                                   const float* gxT_in, int b0, int nb, hipStream_t s,
+                                   hipStream_t s_dx) {
   MfmaStage ms;
   if (!mfma_stage(g, &ms)) return hipErrorInvalidValue;
   if (nb <= 0) return hipSuccess;
+  if (!s_dx) s_dx = s;
   const int TJ = g.J * g.kh * g.kw, NT = (TJ + 15) / 16;
   dim3 grid(nb * ms.cpi, (g.C + 63) / 64);
   auto wg = [&](auto kern, auto* xp) {
@@ -2429,7 +2431,7 @@ hipError_t launch_offset_bwd_chunk(const Geo& g, const void* xT, bool xT_bf16, c
     else if (NT <= 8) w4 ? wg(offset_wgrad_mfma<2, true>, xf) : wg(offset_wgrad_mfma<2, false>, xf);
     else w4 ? wg(offset_wgrad_mfma<3, true>, xf) : wg(offset_wgrad_mfma<3, false>, xf);
   }
-  hipLaunchKernelGGL(offset_dgrad_mfma, dim3(nb * ms.spi), dim3(256), ms.lds_x, s, g, wt2,
+  hipLaunchKernelGGL(offset_dgrad_mfma, dim3(nb * ms.spi), dim3(256), ms.lds_x, s_dx, g, wt2,
                      pad_c(g.C), goff, gx, gxT_in, ms.spi, b0 * ms.spi);
   return hipGetLastError();
 }
@@ -2450,15 +2452,27 @@ hipError_t launch_offset_bwd_finish(const Geo& g, const float* goff, const float
 hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
                                   const float* w_off, const float* goff, float* goffT, float* wt2,
                                   float* gx, float* gw_off, float* gb_off, const float* gxT_in,
-                                  hipStream_t s) {
+                                  hipStream_t s, hipStream_t aux, hipEvent_t fork,
+                                  hipEvent_t join) {
   const int KK = g.kh * g.kw;
   bool generic = false;
   DCN_KK_DISPATCH(KK, (void)KKc);
   if (!generic && offset_bwd_chunkable(g)) {
     hipError_t e = launch_offset_bwd_prep(g, w_off, wt2, s);
+    // r06 (aux given): the ∂x kernel on the side stream beside ∂W_off and its reduction, as
+    // the bf16 backward does since r05 (the two share only their inputs; each alone keeps the
+    // f32 MFMA busy ≈0.6 of its time, profiles/r06a_mfma_busy_config3.json)
+    if (e == hipSuccess && aux) {
+      e = hipEventRecord(fork, s);
+      if (e == hipSuccess) e = hipStreamWaitEvent(aux, fork, 0);
+    }
     if (e == hipSuccess)
-      e = launch_offset_bwd_chunk(g, xT, false, goff, goffT, wt2, gx, gxT_in, 0, g.B, s);
+      e = launch_offset_bwd_chunk(g, xT, false, goff, goffT, wt2, gx, gxT_in, 0, g.B, s, aux);
     if (e == hipSuccess) e = launch_offset_bwd_finish(g, goff, goffT, gw_off, gb_off, s);
+    if (e == hipSuccess && aux) {
+      e = hipEventRecord(join, aux);
+      if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
+    }
     return e;
   }
   if (gb_off) launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);

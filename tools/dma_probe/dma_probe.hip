@@ -22,7 +22,9 @@
 //   stream1   stream with one loader wave per workgroup (the guide's ldsdma-fill shape)
 //   dw2       dw with two workgroups per CU (504 workgroups, R-slot rings of 16 KiB stages:
 //             16 pixels per stage)
-// argv[2]: ring slots R (3..4 for 32 KiB stages), argv[3]: launches timed.
+// argv[2]: ring slots R (3..4 for 32 KiB stages), argv[3]: launches timed, argv[4]: 1 = write a
+// 512 MB buffer before every launch (the sources cold, the Infinity Cache full of dirty lines),
+// 2 = read it (cold sources, clean cache); each launch then timed alone.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -122,6 +124,16 @@ __global__ __launch_bounds__(512) void probe(Args a) {
   vm_wait<0>();  // no DMA may land after the workgroup ends
 }
 
+// the clean flush: reads n16 × 16 B (the sum is never stored)
+__global__ __launch_bounds__(256) void sweep(const uint4* __restrict__ p, size_t n16, int* sink) {
+  unsigned acc = 0;
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) {
+    const uint4 v = p[i];
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x12345678u) sink[0] = 1;
+}
+
 int main(int argc, char** argv) {
   const char* ms = argc > 1 ? argv[1] : "dw";
   const int R = argc > 2 ? atoi(argv[2]) : 4;
@@ -162,22 +174,47 @@ int main(int argc, char** argv) {
     else if (R == 4) hipLaunchKernelGGL((probe<16, 4>), dim3(a.nwg), dim3(512), 0, 0, a);
     else hipLaunchKernelGGL((probe<16, 3>), dim3(a.nwg), dim3(512), 0, 0, a);
   };
+  const int cold = argc > 4 ? atoi(argv[4]) : 0;
+  char* flush = nullptr;
+  const size_t flushB = 512ull << 20;
+  if (cold) {
+    CK(hipMalloc(&flush, flushB));
+    CK(hipMemset(flush, 5, flushB));
+  }
   for (int i = 0; i < 3; ++i) launch();
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  CK(hipEventRecord(e0, 0));
-  for (int i = 0; i < reps; ++i) launch();
-  CK(hipEventRecord(e1, 0));
-  CK(hipEventSynchronize(e1));
   float ms_tot = 0.f;
-  CK(hipEventElapsedTime(&ms_tot, e0, e1));
+  if (cold) {
+    for (int i = 0; i < reps; ++i) {
+      if (cold == 1)
+        CK(hipMemsetAsync(flush, i & 0xff, flushB, 0));
+      else
+        hipLaunchKernelGGL(sweep, dim3(4096), dim3(256), 0, 0,
+                           reinterpret_cast<const uint4*>(flush), flushB / 16, (int*)sink);
+      CK(hipEventRecord(e0, 0));
+      launch();
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      ms_tot += ms;
+    }
+    CK(hipFree(flush));
+  } else {
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < reps; ++i) launch();
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms_tot, e0, e1));
+  }
   const double us = 1e3 * ms_tot / reps;
   const double through = (double)a.nwg * a.spr * stageB;  // bytes moved into LDS (or regs)
-  printf("{\"mode\": \"%s\", \"ring\": %d, \"stage_px\": %d, \"workgroups\": %d, \"stages_per_wg\": %d, "
+  printf("{\"mode\": \"%s\", \"cold\": %d, \"ring\": %d, \"stage_px\": %d, \"workgroups\": %d, \"stages_per_wg\": %d, "
          "\"us\": %.2f, \"through_MB\": %.1f, \"through_TBps\": %.3f, \"per_wg_GBps\": %.2f}\n",
-         ms, R, px, a.nwg, a.spr, us, through / 1e6, through / us / 1e6,
+         ms, cold, R, px, a.nwg, a.spr, us, through / 1e6, through / us / 1e6,
          through / a.nwg / us / 1e3);
   CK(hipFree(gout));
   CK(hipFree(col));
