@@ -141,11 +141,21 @@ int dw_parts_max(const Geo& g) {
   return *std::max_element(n, n + DW_PATHS);
 }
 
+// The fp32 forward GEMM as ONE product over the batch's pixels instead of one per image when
+// an image has few output pixels (r06: BASELINE config 5, Ho·Wo = 36: the per-image GEMM's
+// 64-pixel tiles ran 1.78× the MFMA work, SQ_VALU_MFMA_BUSY 0.86 against 0.51 of useful
+// flops); its [O][B·HW] result goes to NCHW with the bias folded in (launch_permute_obp_bias)
+bool fwd_flat_gemm(const Geo& g) {
+  return g.dt == DCN_F32 && g.HW < 256 && (long)g.B * g.HW * g.K < (1l << 31) &&
+         (long)g.B * g.HW * g.O < (1l << 31);
+}
+
 struct WsLayout {
   size_t xT = 0;     // [B][H*W][C] channels-last copy of x (forward, kept for backward)
   size_t wt = 0;     // transposed w_off copy for the offset-conv kernels
   size_t part = 0;   // offset-conv channel-slice partials (forward)
   size_t col = 0;    // [B][HW][K] channels-last columns / ∂columns
+  size_t fwdT = 0;   // [O][B][HW] the flat forward GEMM's result (fwd_flat_gemm geometries)
   size_t parts = 0;  // [dw_parts_max][O*K] ∂W partials
   int parts_planes = 0;  // the [O][K] planes `parts` holds (0: forward-only layout)
   size_t goff = 0;   // [B][J][HW] ∂offset (when the caller passes none)
@@ -178,6 +188,7 @@ WsLayout ws_layout(const Geo& g, bool bwd, bool cols = true) {
   L.wt = take(dcn::offset_conv_wt_floats(g) * sizeof(float));
   L.part = take(dcn::offset_conv_fpart_floats(g) * sizeof(float));
   L.col = take(cols ? (size_t)g.B * g.HW * g.K * sizeof(float) : 0);
+  L.fwdT = take(fwd_flat_gemm(g) ? (size_t)g.B * g.O * g.HW * sizeof(float) : 0);
   const size_t f = sizeof(float);
   if (g.dt == DCN_BF16) {
     // DCN_BF16 forward copies, at the same offsets in the forward-only and the
@@ -426,7 +437,7 @@ bool use_split(dcn_handle* h, const Geo& g) {
 
 int core_forward(dcn_handle* h, const Geo& g, const float* x, const float* off, const float* w,
                  const float* b, bool has_bias, float* out, float* xT, float* colT,
-                 bool xT_ready) {
+                 bool xT_ready, float* fwdT) {
   if (!xT_ready) {
     ProfScope ps(h, DCN_K_XPOSE);
     HIP_TRY(dcn::launch_nchw_to_nhwc(x, xT, g.B, g.C, g.HWi, h->stream));
@@ -461,7 +472,23 @@ int core_forward(dcn_handle* h, const Geo& g, const float* x, const float* off, 
                                      has_bias ? b : nullptr));
       return DCN_OK;
     }
-    GEMM_TRY(h, sp, colT, w, out);
+    if (fwdT && fwd_flat_gemm(g)) {
+      // one product over all B·HW pixels, C(B·HW × O) = colTᵀ · Wf into [O][B][HW]
+      sp.m = g.B * g.HW;
+      sp.lda = g.K; sp.sa = 0;
+      sp.ldc = g.B * g.HW; sp.sc = 0;
+      sp.batch = 1;
+      GEMM_TRY(h, sp, colT, w, fwdT);
+    } else {
+      GEMM_TRY(h, sp, colT, w, out);
+      fwdT = nullptr;
+    }
+  }
+  if (fwdT) {
+    ProfScope ps(h, DCN_K_BIAS_FWD);
+    HIP_TRY(dcn::launch_permute_obp_bias(fwdT, has_bias ? b : nullptr, out, g.B, g.O, g.HW,
+                                         h->stream));
+    return DCN_OK;
   }
   if (has_bias) {
     ProfScope ps(h, DCN_K_BIAS_FWD);
@@ -1214,7 +1241,8 @@ int dcn_forward_ex(dcn_handle* h, const dcn_desc* d, const float* x, const float
                                              reinterpret_cast<float*>(base + L.wt), h->stream));
     }
     return core_forward(h, g, x, off, w, b, d->has_bias != 0, out, xT,
-                        reinterpret_cast<float*>(base + L.col), true);
+                        reinterpret_cast<float*>(base + L.col), true,
+                        reinterpret_cast<float*>(base + L.fwdT));
   }
   if (ocg_on(g)) {
     // r05: the offset conv as one GEMM over its own im2col (config 5: C = 512, J = 72,
@@ -1231,7 +1259,8 @@ int dcn_forward_ex(dcn_handle* h, const dcn_desc* d, const float* x, const float
                                    reinterpret_cast<float*>(base + L.part)));
     }
     return core_forward(h, g, x, off, w, b, d->has_bias != 0, out, xT,
-                        reinterpret_cast<float*>(base + L.col), true);
+                        reinterpret_cast<float*>(base + L.col), true,
+                        reinterpret_cast<float*>(base + L.fwdT));
   }
   // x -> channels-last on the side stream, beside the offset conv (both only read x)
   DCN_TRY(fork_aux(h));
@@ -1247,7 +1276,8 @@ int dcn_forward_ex(dcn_handle* h, const dcn_desc* d, const float* x, const float
   }
   DCN_TRY(join_aux(h));
   return core_forward(h, g, x, off, w, b, d->has_bias != 0, out, xT,
-                      reinterpret_cast<float*>(base + L.col), true);
+                      reinterpret_cast<float*>(base + L.col), true,
+                      reinterpret_cast<float*>(base + L.fwdT));
 }
 
 int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* off,

@@ -244,6 +244,9 @@ hipError_t launch_xpose_chsum(const float* in, float* out, float* tsum, float* c
                               hipEvent_t ev = nullptr);
 hipError_t launch_bias_add(const Geo& g, float* out, const float* bias, int b0, int nb,
                            hipStream_t s);
+// out[b][o][p] = src[o][b][p] (+ bias[o] when bias != NULL): the flat forward GEMM's result
+hipError_t launch_permute_obp_bias(const float* src, const float* bias, float* out, int B, int O,
+                                   int HW, hipStream_t s);
 hipError_t launch_bias_grad(const Geo& g, const float* gout, float* gb, hipStream_t s);
 hipError_t launch_sum_partials(const float* parts, int nparts, size_t n, float* dst,
                                hipStream_t s,

@@ -143,6 +143,56 @@ hipError_t launch_bias_add(const Geo& g, float* out, const float* bias, int b0, 
   return hipGetLastError();
 }
 
+// out[b][o][p] = src[o][b][p] (+ bias[o]): the flat forward GEMM's [O][B·HW] result into
+// NCHW, with the bias pass folded in (one fp32 add, launch_bias_add's op). vec4 when HW % 4 == 0.
+__global__ __launch_bounds__(256) void permute_obp_bias(const float* __restrict__ src,
+                                                        const float* __restrict__ bias,
+                                                        float* __restrict__ out, int B, int O,
+                                                        int HW, long n) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int p = (int)(i % HW);
+    const long bo = i / HW;
+    const int o = (int)(bo % O), b = (int)(bo / O);
+    const float v = src[((long)o * B + b) * HW + p];
+    out[i] = bias ? v + bias[o] : v;
+  }
+}
+__global__ __launch_bounds__(256) void permute_obp_bias4(const float4* __restrict__ src,
+                                                         const float* __restrict__ bias,
+                                                         float4* __restrict__ out, int B, int O,
+                                                         int HW4, long n4) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const int p = (int)(i % HW4);
+    const long bo = i / HW4;
+    const int o = (int)(bo % O), b = (int)(bo / O);
+    float4 v = src[((long)o * B + b) * HW4 + p];
+    if (bias) {
+      const float bv = bias[o];
+      v.x += bv;
+      v.y += bv;
+      v.z += bv;
+      v.w += bv;
+    }
+    out[i] = v;
+  }
+}
+
+hipError_t launch_permute_obp_bias(const float* src, const float* bias, float* out, int B, int O,
+                                   int HW, hipStream_t s) {
+  const long n = (long)B * O * HW;
+  if (HW % 4 == 0) {
+    const long n4 = n / 4;
+    const unsigned grid = (unsigned)min((n4 + 255) / 256, 8192L);
+    hipLaunchKernelGGL(permute_obp_bias4, dim3(grid), dim3(256), 0, s,
+                       reinterpret_cast<const float4*>(src), bias, reinterpret_cast<float4*>(out),
+                       B, O, HW / 4, n4);
+  } else {
+    const unsigned grid = (unsigned)min((n + 255) / 256, 8192L);
+    hipLaunchKernelGGL(permute_obp_bias, dim3(grid), dim3(256), 0, s, src, bias, out, B, O, HW, n);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_bias_grad(const Geo& g, const float* gout, float* gb, hipStream_t s) {
   launch_channel_sum(gout, g.B, g.O, g.HW, gb, s);
   return hipGetLastError();
