@@ -141,12 +141,14 @@ int dw_parts_max(const Geo& g) {
   return *std::max_element(n, n + DW_PATHS);
 }
 
-// The fp32 forward GEMM as ONE product over the batch's pixels instead of one per image when
-// an image has few output pixels (r06: BASELINE config 5, Ho·Wo = 36: the per-image GEMM's
-// 64-pixel tiles ran 1.78× the MFMA work, SQ_VALU_MFMA_BUSY 0.86 against 0.51 of useful
-// flops); its [O][B·HW] result goes to NCHW with the bias folded in (launch_permute_obp_bias)
+// The fp32 forward GEMM as ONE product over the batch's pixels instead of one per image
+// (r06); its [O][B·HW] result goes to NCHW with the bias folded in (launch_permute_obp_bias,
+// which replaces the bias pass at the same bytes). Config 5 (Ho·Wo = 36): the per-image GEMM's
+// 64-pixel tiles ran 1.78× the MFMA work (SQ_VALU_MFMA_BUSY 0.86 against 0.51 of useful
+// flops), forward GEMM 0.138 -> 0.091 ms; config 3: 1.650 -> 1.603-1.616 ms, step -0.04 ms;
+// config 2: no change (tools/ab.sh, one box each). Costs a [B][O][HW] fp32 workspace region.
 bool fwd_flat_gemm(const Geo& g) {
-  return g.dt == DCN_F32 && g.HW < 256 && (long)g.B * g.HW * g.K < (1l << 31) &&
+  return g.dt == DCN_F32 && g.B > 1 && (long)g.B * g.HW * g.K < (1l << 31) &&
          (long)g.B * g.HW * g.O < (1l << 31);
 }
 
