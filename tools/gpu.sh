@@ -9,7 +9,7 @@
 #   strong    rocprofv3 kernel stats of config 3 at B = 512 (the strong-scaling shard at N = 1)
 #   pmc3 / pmc4 / pmc5   FETCH_SIZE and WRITE_SIZE passes (tools/pmc_pass.sh) for that config
 #   sq4 / sq3  SQ counters (tools/pmc_sq.sh) for that config
-#   mfma3 / mfma4 / mfma5  MFMA-busy counters (tools/pmc_mfma.sh + tools/mfma_summary.py)
+#   mfma2 / mfma3 / mfma4 / mfma5  MFMA-busy counters (tools/pmc_mfma.sh + tools/mfma_summary.py)
 #   diag      tools/launch_diag.py (200 config-4 steps per schedule, 40 of config 3, bitwise)
 # Env: BENCH_EXTRA (extra bench.py flags for the prof / pmc steps).
 set -o pipefail
@@ -49,7 +49,7 @@ for S in "$@"; do
     pmc5) BENCH_ARGS="--config 5 ${BENCH_EXTRA}" bash tools/pmc_pass.sh ${T}c5 || exit 1 ;;
     sq3) bash tools/pmc_sq.sh ${T}c3 || exit 1 ;;
     sq4) BENCH_ARGS="--config 4 ${BENCH_EXTRA}" bash tools/pmc_sq.sh ${T}c4 || exit 1 ;;
-    mfma3|mfma4|mfma5)
+    mfma2|mfma3|mfma4|mfma5)
       c=${S#mfma}
       bash tools/pmc_mfma.sh ${T}c$c --config $c ${BENCH_EXTRA} || { tail -5 gpurun_out/mfma_${T}c$c.log; exit 1; }
       python3 tools/mfma_summary.py gpurun_out/mfma_${T}c$c gpurun_out/${T}_mfma_busy_config$c.json --config=$c || exit 1 ;;
