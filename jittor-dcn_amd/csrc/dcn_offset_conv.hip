@@ -912,26 +912,48 @@ __global__ __launch_bounds__(256) void offset_wgrad_mfma_m2(Geo g, const float* 
 
 // ∂w_off[j][c][tap] = Σ_chunk part[chunk][c][j·KK + tap], chunks in order: 64 elements per
 // 1024-thread block, wave w sums chunks ≡ w (mod 16), the 16 wave sums fold in order.
+// VEC (E % 4 == 0): a lane's 4 consecutive elements as one float4 (1 KiB per wave load, 256
+// elements per block); per element the same additions in the same order either way
+template <bool VEC>
 __global__ __launch_bounds__(1024) void wgrad_mfma_reduce(Geo g, const float* __restrict__ part,
                                                          int nchunk, float* __restrict__ gw) {
+  constexpr int V = VEC ? 4 : 1;
   const int KK = g.kh * g.kw, TJ = g.J * KK;
   const long E = (long)g.C * TJ;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long i = (long)blockIdx.x * 64 + lane;
-  const long ic = i < E ? i : 0;
-  float s = 0.f;
-#pragma unroll 4
-  for (int ch = w; ch < nchunk; ch += 16) s += part[(size_t)ch * E + ic];
-  __shared__ float red[16][64];
-  red[w][lane] = s;
-  __syncthreads();
-  if (w != 0 || i >= E) return;
-  s = red[0][lane];
+  const long i0 = (long)blockIdx.x * 64 * V + V * lane;
+  const long ic = i0 < E ? i0 : 0;
+  float s[V];
 #pragma unroll
-  for (int k = 1; k < 16; ++k) s += red[k][lane];
-  const int c = (int)(i / TJ), tj = (int)(i - (long)c * TJ);
-  const int j = tj / KK, t = tj - j * KK;
-  gw[((size_t)j * g.C + c) * KK + t] = s;
+  for (int e = 0; e < V; ++e) s[e] = 0.f;
+#pragma unroll 4
+  for (int ch = w; ch < nchunk; ch += 16) {
+    if constexpr (VEC) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (size_t)ch * E + ic);
+      s[0] += v.x;
+      s[1] += v.y;
+      s[2] += v.z;
+      s[3] += v.w;
+    } else {
+      s[0] += part[(size_t)ch * E + ic];
+    }
+  }
+  __shared__ float red[16][64 * V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) red[w][V * lane + e] = s[e];
+  __syncthreads();
+  if (w != 0) return;
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    const long i = i0 + e;
+    if (i >= E) break;
+    float t0 = red[0][V * lane + e];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) t0 += red[k][V * lane + e];
+    const int c = (int)(i / TJ), tj = (int)(i - (long)c * TJ);
+    const int j = tj / KK, t = tj - j * KK;
+    gw[((size_t)j * g.C + c) * KK + t] = t0;
+  }
 }
 
 // ∂x (+)= convᵀ: block = one 64-pixel strip of an image, wave w = channels 64w..64w+63
@@ -1886,36 +1908,57 @@ __global__ __launch_bounds__(256 * CGB) void offset_wgrad_bf16(Geo g, const bf16
 }
 
 // ∂w_off[j][c][t] = Σ_chunk (fragment-ordered partials of offset_wgrad_bf16), chunks in
-// order: 64 fragment elements per 1024-thread block, wave w sums chunks ≡ w (mod 16), the
-// 16 wave sums fold in order (deterministic); each element then lands at its (j, c, t).
+// order: 256 fragment elements per 1024-thread block (a lane's 4 consecutive elements as one
+// float4: 1 KiB per wave load), wave w sums chunks ≡ w (mod 16), the 16 wave sums fold in
+// order (deterministic; per element the same additions in the same order as r05's
+// one-element-per-lane form, which read 256 B per wave load and took 23 µs at config 4);
+// each element then lands at its (j, c, t).
 __global__ __launch_bounds__(1024) void wgrad_frag_reduce(Geo g, const float* __restrict__ part,
                                                          int nchunk, float* __restrict__ gw) {
   const int J8 = j8(g.J), KK = g.kh * g.kw, NT = (KK * J8 + 31) / 32;
-  const long E = (long)(g.C / 64) * NT * 2 * 1024;
+  const long E = (long)(g.C / 64) * NT * 2 * 1024;  // a multiple of 2048
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long i = (long)blockIdx.x * 64 + lane;
-  const long ic = i < E ? i : 0;
-  // padding K columns (k >= KK·J8) were never written: not read either
+  const long i0 = (long)blockIdx.x * 256 + 4 * lane;
+  const long ic = i0 < E ? i0 : 0;
+  // the 4 elements share their K column (the same 16-element register group): padding K
+  // columns (k >= KK·J8) were never written, so they are not read either
   const int kcol = 32 * (int)(((ic >> 10) >> 1) % NT) + (int)((ic >> 4) & 31);
-  float s = 0.f;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (kcol < KK * J8) {
-#pragma unroll 4
-    for (int ch = w; ch < nchunk; ch += 16) s += part[(size_t)ch * E + ic];
+#pragma unroll 8
+    for (int ch = w; ch < nchunk; ch += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (size_t)ch * E + ic);
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
   }
-  __shared__ float red[16][64];
+  __shared__ float4 red[16][64];
   red[w][lane] = s;
   __syncthreads();
-  if (w != 0 || i >= E) return;
+  if (w != 0 || i0 >= E) return;
   s = red[0][lane];
 #pragma unroll
-  for (int k = 1; k < 16; ++k) s += red[k][lane];
-  const int reg = (int)(i & 15), fl = (int)((i >> 4) & 63);
-  const long tm = i >> 10;  // ((cg·NT + tile)·2 + m)
-  const int m = (int)(tm & 1), tile = (int)((tm >> 1) % NT), cg = (int)((tm >> 1) / NT);
-  const int row = (reg & 3) + 8 * (reg >> 2) + 4 * (fl >> 5);
-  const int c = 64 * cg + 32 * m + row, k = 32 * tile + (fl & 31);
-  const int t = k / J8, j = k - t * J8;
-  if (t < KK && j < g.J) gw[((size_t)j * g.C + c) * KK + t] = s;
+  for (int k = 1; k < 16; ++k) {
+    const float4 v = red[k][lane];
+    s.x += v.x;
+    s.y += v.y;
+    s.z += v.z;
+    s.w += v.w;
+  }
+  const float sv[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const long i = i0 + e;
+    const int reg = (int)(i & 15), fl = (int)((i >> 4) & 63);
+    const long tm = i >> 10;  // ((cg·NT + tile)·2 + m)
+    const int m = (int)(tm & 1), tile = (int)((tm >> 1) % NT), cg = (int)((tm >> 1) / NT);
+    const int row = (reg & 3) + 8 * (reg >> 2) + 4 * (fl >> 5);
+    const int c = 64 * cg + 32 * m + row, k = 32 * tile + (fl & 31);
+    const int t = k / J8, j = k - t * J8;
+    if (t < KK && j < g.J) gw[((size_t)j * g.C + c) * KK + t] = sv[e];
+  }
 }
 static size_t wgrad_frag_part_floats(const Geo& g, const MfmaStage& ms) {
   const int NT = (g.kh * g.kw * j8(g.J) + 31) / 32;
@@ -1987,7 +2030,7 @@ hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16
   hipLaunchKernelGGL(offset_wgrad_bf16<1>, dim3(nblk, g.C / 64), dim3(256), lds_w, s, g, x, goff,
                      part, ms.rowsB, ms.cpi, cpb);
   const long E = (long)(g.C / 64) * ((KK * J8 + 31) / 32) * 2 * 1024;
-  hipLaunchKernelGGL(wgrad_frag_reduce, dim3((unsigned)((E + 63) / 64)), dim3(1024), 0, s, g,
+  hipLaunchKernelGGL(wgrad_frag_reduce, dim3((unsigned)((E + 255) / 256)), dim3(1024), 0, s, g,
                      part, nblk, gw_off);
 #if OFFB_CONC
   // (A/B) ∂x on the side stream, concurrent with ∂W_off + its fold on the main one
@@ -2441,8 +2484,13 @@ hipError_t launch_offset_bwd_finish(const Geo& g, const float* goff, const float
   MfmaStage ms;
   if (!mfma_stage(g, &ms)) return hipErrorInvalidValue;
   const long E = (long)g.C * g.J * g.kh * g.kw;
-  hipLaunchKernelGGL(wgrad_mfma_reduce, dim3((unsigned)((E + 63) / 64)), dim3(1024), 0, s, g,
-                     goffT, g.B * ms.cpi / wgrad_cpb(g, ms), gw_off);
+  const int nchunk = g.B * ms.cpi / wgrad_cpb(g, ms);
+  if (E % 4 == 0)
+    hipLaunchKernelGGL(wgrad_mfma_reduce<true>, dim3((unsigned)((E + 255) / 256)), dim3(1024), 0,
+                       s, g, goffT, nchunk, gw_off);
+  else
+    hipLaunchKernelGGL(wgrad_mfma_reduce<false>, dim3((unsigned)((E + 63) / 64)), dim3(1024), 0, s,
+                       g, goffT, nchunk, gw_off);
   if (gb_off) launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
   return hipGetLastError();
 }
