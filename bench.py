@@ -736,11 +736,12 @@ def main():
         # one step captured on a side stream (libdcn bound to it, its own side stream joins
         # through events); each replay is one full step of the same kernels
         try:
-            gs = torch.cuda.Stream(dev)
-            gs.wait_stream(stream)
+            # (its own name: `gs` is the gradient-exchange stream the step closes over)
+            cap = torch.cuda.Stream(dev)
+            cap.wait_stream(stream)
             graph = torch.cuda.CUDAGraph()
-            h.set_stream(gs.cuda_stream)
-            with torch.cuda.graph(graph, stream=gs):
+            h.set_stream(cap.cuda_stream)
+            with torch.cuda.graph(graph, stream=cap):
                 step()
             h.set_stream(stream.cuda_stream)
             run = graph.replay
