@@ -721,11 +721,23 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
   const bool off_mfma = dcn::offset_bwd_bf16_ok(g);
   const bool dcol_k = !h->dcol_gemm && dcn::dcol_bf16_ok(g.K, g.O, npix) &&
                       !dcn::get_force_generic();
+  // the sample bins (K5's input) on the side stream. (r06 A/B at config 4: the sort's 64
+  // workgroups hold 100 KiB of LDS each and keep ≈60 of dw_stream_bf16's 252 one-per-CU
+  // workgroups waiting ≈25 µs; launched after ∂W instead, beside the ∂col product, ∂W's scope
+  // went 0.101 -> 0.096 ms but ∂col's 0.079 -> 0.106 ms.) With the forward's columns in the
+  // workspace, its fp32 offsets are there too (every bf16 forward leaves off32 = the rounded
+  // offsets it sampled with), so the sort starts before the prep and the ∂out transpose
+  // instead of after them, and ends that much earlier into ∂W.
+  if (col_valid) {
+    DCN_TRY(fork_aux(h));
+    HIP_TRY(dcn::launch_bins(g, off32, base + L.bins, goff32, 0, g.B, h->aux));
+  }
   {
-    // one launch: the fp32 offsets (== the forward's rounded ones), and the weights in the
-    // layouts of the kernels below (fp32 w_off only for the non-MFMA offset-conv paths)
+    // one launch: the fp32 offsets (== the forward's rounded ones) unless the forward left
+    // them, and the weights in the layouts of the kernels below (fp32 w_off only for the
+    // non-MFMA offset-conv paths)
     dcn::PrepBatch pb;
-    pb.f32(off, off32, noff);
+    if (!col_valid) pb.f32(off, off32, noff);
     if (off_mfma)
       pb.add(dcn::prep_ck(g, w_off, BF(L.wb16)));
     else
@@ -733,12 +745,10 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
     if (dcol_k) pb.add(dcn::prep_dcol(g.K, w, BF(L.wz)));
     HIP_TRY(dcn::launch_prep_bf16(pb, st));
   }
-  // the sample bins (K5's input) on the side stream from here on. (r06 A/B at config 4: the
-  // sort's 64 workgroups hold 100 KiB of LDS each and keep ≈60 of dw_stream_bf16's 252
-  // one-per-CU workgroups waiting ≈25 µs; launched after ∂W instead, beside the ∂col product,
-  // ∂W's scope went 0.101 -> 0.096 ms but ∂col's 0.079 -> 0.106 ms, so they stay here.)
-  DCN_TRY(fork_aux(h));
-  HIP_TRY(dcn::launch_bins(g, off32, base + L.bins, goff32, 0, g.B, h->aux));
+  if (!col_valid) {
+    DCN_TRY(fork_aux(h));
+    HIP_TRY(dcn::launch_bins(g, off32, base + L.bins, goff32, 0, g.B, h->aux));
+  }
   // f2 without a column matrix (DCN_FWD_FUSED_NOCOL): ∂W with the columns recomputed from
   // xT inside the MFMA kernel, so the ∂columns are the only large buffer of the step
   const bool dw_fused = !col_valid && h->fwd_path == DCN_FWD_FUSED_NOCOL &&
