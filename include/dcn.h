@@ -166,7 +166,10 @@ int dcn_forward_ex(dcn_handle* h, const dcn_desc* d, const float* x,
                               pointer per workspace, at most 256, the oldest dropped first); a
                               backward on a workspace it holds no record for (a NO_COLUMNS /
                               FUSED_NOCOL forward, a dropped record) recomputes them, but the
-                              record does not notice a foreign write into a recorded ws. */
+                              record does not notice a foreign write into a recorded ws. The
+                              offsets are then also the forward's (a DCN_BF16 backward reads
+                              the fp32 offsets that forward left in ws, r06): off must be that
+                              forward's output, as the columns already assume. */
 
 /* Autodiff of DeformConv2d.execute as triggered by optimizer.backward
  * (train.py:414). Overwrites grad_x, grad_w, grad_b (if has_bias),

@@ -912,44 +912,37 @@ __global__ __launch_bounds__(256) void offset_wgrad_mfma_m2(Geo g, const float* 
 
 // ∂w_off[j][c][tap] = Σ_chunk part[chunk][c][j·KK + tap], chunks in order: 64 elements per
 // 1024-thread block, wave w sums chunks ≡ w (mod 16), the 16 wave sums fold in order.
-// VEC (E % 4 == 0): a lane's 4 consecutive elements as one float4 (1 KiB per wave load, 256
-// elements per block); per element the same additions in the same order either way
-template <bool VEC>
+// a lane's 4 consecutive elements as one float4 (1 KiB per wave load, 256 elements per block;
+// E = C·J·kh·kw is a multiple of 4 since mfma_stage requires C % 4 == 0); per element the same
+// additions in the same order as r05's one-element-per-lane form
 __global__ __launch_bounds__(1024) void wgrad_mfma_reduce(Geo g, const float* __restrict__ part,
                                                          int nchunk, float* __restrict__ gw) {
-  constexpr int V = VEC ? 4 : 1;
   const int KK = g.kh * g.kw, TJ = g.J * KK;
   const long E = (long)g.C * TJ;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long i0 = (long)blockIdx.x * 64 * V + V * lane;
+  const long i0 = (long)blockIdx.x * 256 + 4 * lane;
   const long ic = i0 < E ? i0 : 0;
-  float s[V];
-#pragma unroll
-  for (int e = 0; e < V; ++e) s[e] = 0.f;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
   for (int ch = w; ch < nchunk; ch += 16) {
-    if constexpr (VEC) {
-      const float4 v = *reinterpret_cast<const float4*>(part + (size_t)ch * E + ic);
-      s[0] += v.x;
-      s[1] += v.y;
-      s[2] += v.z;
-      s[3] += v.w;
-    } else {
-      s[0] += part[(size_t)ch * E + ic];
-    }
+    const float4 v = *reinterpret_cast<const float4*>(part + (size_t)ch * E + ic);
+    s[0] += v.x;
+    s[1] += v.y;
+    s[2] += v.z;
+    s[3] += v.w;
   }
-  __shared__ float red[16][64 * V];
+  __shared__ float red[16][256];
 #pragma unroll
-  for (int e = 0; e < V; ++e) red[w][V * lane + e] = s[e];
+  for (int e = 0; e < 4; ++e) red[w][4 * lane + e] = s[e];
   __syncthreads();
   if (w != 0) return;
 #pragma unroll
-  for (int e = 0; e < V; ++e) {
+  for (int e = 0; e < 4; ++e) {
     const long i = i0 + e;
     if (i >= E) break;
-    float t0 = red[0][V * lane + e];
+    float t0 = red[0][4 * lane + e];
 #pragma unroll
-    for (int k = 1; k < 16; ++k) t0 += red[k][V * lane + e];
+    for (int k = 1; k < 16; ++k) t0 += red[k][4 * lane + e];
     const int c = (int)(i / TJ), tj = (int)(i - (long)c * TJ);
     const int j = tj / KK, t = tj - j * KK;
     gw[((size_t)j * g.C + c) * KK + t] = t0;
@@ -2484,13 +2477,8 @@ hipError_t launch_offset_bwd_finish(const Geo& g, const float* goff, const float
   MfmaStage ms;
   if (!mfma_stage(g, &ms)) return hipErrorInvalidValue;
   const long E = (long)g.C * g.J * g.kh * g.kw;
-  const int nchunk = g.B * ms.cpi / wgrad_cpb(g, ms);
-  if (E % 4 == 0)
-    hipLaunchKernelGGL(wgrad_mfma_reduce<true>, dim3((unsigned)((E + 255) / 256)), dim3(1024), 0,
-                       s, g, goffT, nchunk, gw_off);
-  else
-    hipLaunchKernelGGL(wgrad_mfma_reduce<false>, dim3((unsigned)((E + 63) / 64)), dim3(1024), 0, s,
-                       g, goffT, nchunk, gw_off);
+  hipLaunchKernelGGL(wgrad_mfma_reduce, dim3((unsigned)((E + 255) / 256)), dim3(1024), 0, s, g,
+                     goffT, g.B * ms.cpi / wgrad_cpb(g, ms), gw_off);
   if (gb_off) launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
   return hipGetLastError();
 }
