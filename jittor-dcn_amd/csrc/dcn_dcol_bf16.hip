@@ -17,6 +17,7 @@
 //     lane holds are 16 consecutive k; a pair of row tiles (64 columns × 32 pixels) passes
 //     through a per-wave 4-KiB LDS stage, so each store instruction writes 8 whole 128-B
 //     lines (the MFMA layout alone gives 32 lines × 2 pieces of 16 B per instruction);
+//   * stores are non-temporal;
 //   * the row groups of one pixel range run on one XCD (bijective remap), so the L2 serves
 //     a tile's ∂outT rows to all of them after the first read.
 // Rounding: fp32 accumulation over o inside the MFMA, one round-to-nearest-even to bf16 per
@@ -27,6 +28,7 @@
 
 #include "dcn_device.h"
 #include "dcn_swizzle.h"
+
 
 namespace dcn {
 namespace {
@@ -46,6 +48,12 @@ constexpr int kDcLds = kDcMT * kDcKS * 64 * 16;  // the A image: 128 KiB
 // and s_setprio 1 around the MFMAs, no change)
 constexpr int kDcLA = 2;
 constexpr int kDcLdsAll = kDcLds + kDcWaves * 4096;  // + a 4-KiB output stage per wave
+// ∂col stores non-temporal (buffer cache policy bit 1, `nt`): r06 A/B at config 4, dcol
+// 0.077 -> 0.070-0.074 ms and the step -12 µs (the 231 MB leave the Infinity Cache clean for
+// K5's reads, the fused forward's column policy). A role-split form of this kernel (one
+// loader wave filling an LDS ring, compute waves that only store) measured 0.079-0.089 ms in
+// six variants and was dropped.
+constexpr int kNT = 2;
 static_assert(kDcLdsAll <= 160 * 1024, "one workgroup per CU");
 
 __device__ __forceinline__ unsigned pack_bf16(float a, float b) {
@@ -151,7 +159,7 @@ __global__ __launch_bounds__(kDcWaves * 64, 2) void dcol_bf16(const bf16_t* __re
         const u32x4 v = *reinterpret_cast<const u32x4*>(stage + r * 128 + ((c ^ (r & 7)) << 4));
         const int p = tc * 32 + r;
         const unsigned o = p < npix ? (unsigned)(p * K + kr + 64 * pr + 8 * c) * 2u : 0x80000000u;
-        __builtin_amdgcn_raw_buffer_store_b128(v, rcol, o, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rcol, o, 0, kNT);
       }
       asm volatile("" ::: "memory");  // the reads before the next pair's writes
     }
@@ -161,6 +169,7 @@ __global__ __launch_bounds__(kDcWaves * 64, 2) void dcol_bf16(const bf16_t* __re
     if (t + kDcWaves < t1) tile(t + kDcWaves, b1, b0);
   }
 }
+
 
 }  // namespace
 
