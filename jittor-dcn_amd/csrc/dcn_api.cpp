@@ -19,6 +19,9 @@
 #include "dcn_internal.h"
 
 // A/B: the bf16 offset backward's ∂x kernel on the side stream beside ∂W_off
+#ifndef DCN_EV_XFLAGS
+#define DCN_EV_XFLAGS hipEventDisableSystemFence
+#endif
 #ifndef OFFB_CONC
 #define OFFB_CONC 1
 #endif
@@ -942,10 +945,12 @@ int dcn_create(int device, dcn_handle** out) {
   }
   h->stream = h->own;
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming);
+  // stream-to-stream events on this device only: no system-scope fence at record / wait
+  const unsigned evf = hipEventDisableTiming | DCN_EV_XFLAGS;
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->fork_ev, evf);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->join_ev, evf);
   for (hipEvent_t* ev : {&h->dw_main, &h->dw_aux, &h->end_ev, &h->comm_done})
-    if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(ev, evf);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     dcn_destroy(h);
