@@ -19,6 +19,9 @@
 #include "dcn_internal.h"
 
 // A/B: the bf16 offset backward's ∂x kernel on the side stream beside ∂W_off
+#ifndef DCN_SUMP_AUX
+#define DCN_SUMP_AUX 1
+#endif
 #ifndef DCN_EV_XFLAGS
 #define DCN_EV_XFLAGS hipEventDisableSystemFence
 #endif
@@ -825,7 +828,15 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
       sp.batch = g.B;
       GEMM_TRY(h, sp, col, gout, F32(L.parts));
     }
-    HIP_TRY(dcn::launch_sum_partials(F32(L.parts), nparts, (size_t)g.K * g.O, F32(L.gw32), st,
+    // the partial-plane sum on the side stream, beside ∂col (it reads 66 MB at config 4;
+    // ∂col is bound by its stores). join_aux below (before K5) and dw_final's dw_aux event
+    // order it before everything that reads ∂W.
+    hipStream_t ss = st;
+    if (DCN_SUMP_AUX) {
+      DCN_TRY(fork_aux(h));
+      ss = h->aux;
+    }
+    HIP_TRY(dcn::launch_sum_partials(F32(L.parts), nparts, (size_t)g.K * g.O, F32(L.gw32), ss,
                                      exch ? nullptr : gw));
   }
   DCN_TRY(dw_final(h, F32(L.gw32), has_bias ? F32(L.gb32) : nullptr, g, exch ? gw : nullptr,
