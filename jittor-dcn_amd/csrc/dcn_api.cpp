@@ -19,6 +19,9 @@
 #include "dcn_internal.h"
 
 // A/B: the bf16 offset backward's ∂x kernel on the side stream beside ∂W_off
+#ifndef DCN_BSUM_AUX
+#define DCN_BSUM_AUX 1
+#endif
 #ifndef DCN_SUMP_AUX
 #define DCN_SUMP_AUX 1
 #endif
@@ -778,7 +781,8 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
     // gxT, which only K5 writes, after this)
     if (dcn::xpose_chsum_bf16_floats(g.B, g.O, g.HW) <= (size_t)g.B * g.HWi * g.C &&
         dcn::launch_xpose_chsum_bf16(gout, goutT, F32(L.gxT), F32(L.gb32), exch ? nullptr : gb,
-                                     g.B, g.O, g.HW, st)) {
+                                     g.B, g.O, g.HW, st, DCN_BSUM_AUX ? h->aux : nullptr,
+                                     h->fork_ev)) {
       HIP_TRY(hipGetLastError());
       have_goutT = true;
     } else {

@@ -236,7 +236,8 @@ bool launch_xpose_f4(const float* in, float* out, int B, int C, int P, hipStream
 bool launch_xpose_b8(const bf16_t* in, bf16_t* out, int B, int C, int P, hipStream_t s);
 size_t xpose_chsum_bf16_floats(int B, int C, int P);
 bool launch_xpose_chsum_bf16(const bf16_t* in, bf16_t* out, float* tsum, float* chsum,
-                             bf16_t* chsum_bf, int B, int C, int P, hipStream_t s);
+                             bf16_t* chsum_bf, int B, int C, int P, hipStream_t s,
+                             hipStream_t s_sum = nullptr, hipEvent_t ev = nullptr);
 // ∂out -> ∂outT with ∂b; the per-channel fold of the tile sums runs on s_sum (after event ev)
 // when given, so tsum must then stay untouched until s_sum is joined.
 hipError_t launch_xpose_chsum(const float* in, float* out, float* tsum, float* chsum, int B,

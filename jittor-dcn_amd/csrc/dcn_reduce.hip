@@ -682,10 +682,16 @@ size_t xpose_chsum_bf16_floats(int B, int C, int P) {
 }
 
 bool launch_xpose_chsum_bf16(const bf16_t* in, bf16_t* out, float* tsum, float* chsum,
-                             bf16_t* chsum_bf, int B, int C, int P, hipStream_t s) {
+                             bf16_t* chsum_bf, int B, int C, int P, hipStream_t s,
+                             hipStream_t s_sum, hipEvent_t ev) {
   if (!xpose_b8_ok(in, out, C, P)) return false;
   dim3 grid(xpose_b8_blocks_x(P), C / 64, B);
   hipLaunchKernelGGL(xpose_b8<true>, grid, dim3(256), 0, s, in, out, tsum, C, P);
+  // the fold only feeds ∂b: off the main stream's critical path when given a side stream
+  // (a failed record / wait leaves it on s)
+  if (s_sum && s_sum != s && hipEventRecord(ev, s) == hipSuccess &&
+      hipStreamWaitEvent(s_sum, ev, 0) == hipSuccess)
+    s = s_sum;
   hipLaunchKernelGGL(tile_sum_to_channels, dim3(C), dim3(64), 0, s, tsum, B * (int)grid.x, C,
                      chsum, chsum_bf);
   return true;
