@@ -19,6 +19,9 @@
 #include "dcn_internal.h"
 
 // A/B: the bf16 offset backward's ∂x kernel on the side stream beside ∂W_off
+#ifndef OCG_REUSE
+#define OCG_REUSE 1
+#endif
 #ifndef DCN_BSUM_AUX
 #define DCN_BSUM_AUX 1
 #endif
@@ -167,6 +170,8 @@ struct WsLayout {
   size_t part = 0;   // offset-conv channel-slice partials (forward)
   size_t col = 0;    // [B][HW][K] channels-last columns / ∂columns
   size_t fwdT = 0;   // [O][B][HW] the flat forward GEMM's result (fwd_flat_gemm geometries)
+  size_t ocol = 0;   // [B][HW][C·kh·kw] the offset conv's im2col (fp32 GEMM route, ocol_ws)
+  bool has_ocol = false;
   size_t parts = 0;  // [dw_parts_max][O*K] ∂W partials
   int parts_planes = 0;  // the [O][K] planes `parts` holds (0: forward-only layout)
   size_t goff = 0;   // [B][J][HW] ∂offset (when the caller passes none)
@@ -200,6 +205,12 @@ WsLayout ws_layout(const Geo& g, bool bwd, bool cols = true) {
   L.part = take(dcn::offset_conv_fpart_floats(g) * sizeof(float));
   L.col = take(cols ? (size_t)g.B * g.HW * g.K * sizeof(float) : 0);
   L.fwdT = take(fwd_flat_gemm(g) ? (size_t)g.B * g.O * g.HW * sizeof(float) : 0);
+  // r06: the forward's offset-conv im2col kept for the backward's ∂W' GEMM (geometries of
+  // the fp32 offset-conv GEMM route, whatever dcn_debug_offset_gemm says: the layout depends
+  // on the geometry alone), in the prefix the forward-only and backward layouts share
+  L.has_ocol = g.dt == DCN_F32 && dcn::offset_conv_gemm_ok(g) && !dcn::offset_fwd_mfma_xt_ok(g) &&
+               !dcn::offset_bwd_chunkable(g);
+  L.ocol = take(L.has_ocol ? (size_t)g.B * g.HW * g.C * g.kh * g.kw * sizeof(float) : 0);
   const size_t f = sizeof(float);
   if (g.dt == DCN_BF16) {
     // DCN_BF16 forward copies, at the same offsets in the forward-only and the
@@ -273,6 +284,9 @@ struct dcn_handle {
   // Guarded by col_ws_mu: concurrent forwards / backwards on one handle may touch it.
   static constexpr size_t kColWsCap = 256;
   std::vector<const void*> col_ws;
+  // the same record (same cap, same mutex) for the fp32 offset-conv GEMM route: workspaces
+  // whose last forward on this handle left the offset conv's im2col (`ocol`) and W' there
+  std::vector<const void*> ocol_ws;
   std::mutex col_ws_mu;
   // data-parallel gradient exchange (dcn_set_comm / dcn_set_grad_stream): the ∂W/∂b
   // all-reduce runs on comm_stream as soon as they are final (dw_main / dw_aux), beside the
@@ -350,18 +364,23 @@ int set_device(dcn_handle* h) {
   return DCN_OK;
 }
 
-// Does this workspace hold the columns of the last DCN_BF16 forward that used it?
-bool ws_has_columns(dcn_handle* h, const void* ws) {
+// per-workspace records (dcn_handle::col_ws, ocol_ws)
+bool ws_rec_has(dcn_handle* h, const std::vector<const void*>& rec, const void* ws) {
   std::lock_guard<std::mutex> lk(h->col_ws_mu);
-  return std::find(h->col_ws.begin(), h->col_ws.end(), ws) != h->col_ws.end();
+  return std::find(rec.begin(), rec.end(), ws) != rec.end();
 }
-void ws_mark_columns(dcn_handle* h, const void* ws, bool has) {
+void ws_rec_mark(dcn_handle* h, std::vector<const void*>& rec, const void* ws, bool has) {
   std::lock_guard<std::mutex> lk(h->col_ws_mu);
-  auto it = std::find(h->col_ws.begin(), h->col_ws.end(), ws);
-  if (it != h->col_ws.end()) h->col_ws.erase(it);
+  auto it = std::find(rec.begin(), rec.end(), ws);
+  if (it != rec.end()) rec.erase(it);
   if (!has) return;
-  if (h->col_ws.size() >= dcn_handle::kColWsCap) h->col_ws.erase(h->col_ws.begin());
-  h->col_ws.push_back(ws);
+  if (rec.size() >= dcn_handle::kColWsCap) rec.erase(rec.begin());
+  rec.push_back(ws);
+}
+// Does this workspace hold the columns of the last DCN_BF16 forward that used it?
+bool ws_has_columns(dcn_handle* h, const void* ws) { return ws_rec_has(h, h->col_ws, ws); }
+void ws_mark_columns(dcn_handle* h, const void* ws, bool has) {
+  ws_rec_mark(h, h->col_ws, ws, has);
 }
 
 // Can the DCN_BF16 forward of this geometry skip the column matrix (the fused forward
@@ -1208,12 +1227,17 @@ int offset_conv_fwd_gemm(dcn_handle* h, const Geo& g, const float* xT, const flo
 }
 // ∂w_off and ∂x (= transpose(gxT_in) + the offset route) from ∂off; wp: J·K floats,
 // ocol: B·HW·K floats (ocol, then ∂ocol), goffT: B·HW·J floats, gwp: J·K floats
+// ocol_fwd: the forward's im2col (and its W' in wp) when still in the workspace, else null
+// (both recomputed, the im2col into ocol)
 int offset_conv_bwd_gemm(dcn_handle* h, const Geo& g, const float* xT, const float* w_off,
                          const float* goff, float* wp, float* ocol, float* goffT, float* gwp,
-                         const float* gxT_in, float* gx, float* gw_off) {
+                         const float* gxT_in, float* gx, float* gw_off, const float* ocol_fwd) {
   const int K = g.C * g.kh * g.kw, P = g.B * g.HW;
-  HIP_TRY(dcn::launch_ocg_wprime(g, w_off, wp, h->stream));
-  HIP_TRY(dcn::launch_ocg_im2col(g, xT, ocol, h->stream));
+  if (!ocol_fwd) {
+    HIP_TRY(dcn::launch_ocg_wprime(g, w_off, wp, h->stream));
+    HIP_TRY(dcn::launch_ocg_im2col(g, xT, ocol, h->stream));
+  }
+  const float* ocol_in = ocol_fwd ? ocol_fwd : ocol;
   HIP_TRY(dcn::launch_ocg_goff_to_pj(g, goff, goffT, h->stream));
   {
     // column-major ∂W'(K × J) = ocol(K × P) · ∂offT(P × J)   (∂offT = [P][J])
@@ -1222,7 +1246,7 @@ int offset_conv_bwd_gemm(dcn_handle* h, const Geo& g, const float* xT, const flo
     sp.m = K; sp.n = g.J; sp.k = P;
     sp.lda = K; sp.ldb = g.J; sp.ldc = K;
     sp.native_f32 = true;
-    GEMM_TRY(h, sp, ocol, goffT, gwp);
+    GEMM_TRY(h, sp, ocol_in, goffT, gwp);
   }
   HIP_TRY(dcn::launch_ocg_wgrad_out(g, gwp, gw_off, h->stream));
   {
@@ -1256,6 +1280,8 @@ int dcn_forward_ex(dcn_handle* h, const dcn_desc* d, const float* x, const float
   if (!ws || ws_bytes < L.total) return fail(DCN_ERR_WORKSPACE, "workspace too small for dcn_forward");
   if (d->has_bias && !b) return fail(DCN_ERR_INVALID, "has_bias set but bias is NULL");
   char* base = static_cast<char*>(ws);
+  // this forward overwrites whatever offset-conv im2col an earlier one left in ws
+  ws_rec_mark(h, h->ocol_ws, ws, false);
   if (g.dt == DCN_BF16) {
     using dcn::bf16_t;
     return forward_bf16(h, g, d->has_bias != 0, reinterpret_cast<const bf16_t*>(x),
@@ -1285,10 +1311,13 @@ int dcn_forward_ex(dcn_handle* h, const dcn_desc* d, const float* x, const float
     }
     {
       ProfScope ps(h, DCN_K_OFFSET_FWD);
+      // ocol in its own region when the layout has one (kept for the backward), else in
+      // the columns region, which K1 overwrites next
       DCN_TRY(offset_conv_fwd_gemm(h, g, xT, w_off, b_off, off,
                                    reinterpret_cast<float*>(base + L.wt),
-                                   reinterpret_cast<float*>(base + L.col),
+                                   reinterpret_cast<float*>(base + (L.has_ocol ? L.ocol : L.col)),
                                    reinterpret_cast<float*>(base + L.part)));
+      if (L.has_ocol) ws_rec_mark(h, h->ocol_ws, ws, true);
     }
     return core_forward(h, g, x, off, w, b, d->has_bias != 0, out, xT,
                         reinterpret_cast<float*>(base + L.col), true,
@@ -1349,8 +1378,13 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
     if (ocg_on(g) && (size_t)g.J * g.K <= (size_t)g.B * g.HW * g.O) {
       // r05: ∂W_off and the offset route of ∂x as GEMMs over the offset conv's im2col (the
       // columns region is free after K5; ∂W' [J][K] in the ∂outT region, free after ∂col)
+      // with the forward's im2col and W' still in ws (DCN_BWD_COL_IN_WS and this handle's
+      // record), ∂W' reads them and the ∂ocol product goes to the free columns region
+      const bool reuse = L.has_ocol && (flags & DCN_BWD_COL_IN_WS) != 0 &&
+                         ws_rec_has(h, h->ocol_ws, ws) && OCG_REUSE;
       DCN_TRY(offset_conv_bwd_gemm(h, g, F(L.xT), w_off, goff, F(L.wt), F(L.col), F(L.goffT),
-                                   F(L.goutT), F(L.gxT), grad_x, grad_w_off));
+                                   F(L.goutT), F(L.gxT), grad_x, grad_w_off,
+                                   reuse ? F(L.ocol) : nullptr));
     } else {
       HIP_TRY(dcn::launch_offset_conv_bwd(g, x, F(L.xT), w_off, goff, F(L.goffT), F(L.wt), grad_x,
                                           grad_w_off, nullptr,

@@ -185,6 +185,36 @@ def test_offset_conv_gemm_vs_valu_kernels(gpu_handle, geo):
     _check_all(out1, off1, g1, ro, roff, rg, "offset-conv GEMM path")
 
 
+def _bitwise_equal(r1, r0, what):
+    np.testing.assert_array_equal(r1[0].view(np.uint32), r0[0].view(np.uint32), err_msg=f"{what} out")
+    np.testing.assert_array_equal(r1[1].view(np.uint32), r0[1].view(np.uint32), err_msg=f"{what} off")
+    for k in r0[2]:
+        np.testing.assert_array_equal(r1[2][k].view(np.uint32), r0[2][k].view(np.uint32),
+                                      err_msg=f"{what} {k}")
+
+
+def test_offset_conv_gemm_backward_reuses_forward_im2col(gpu_handle):
+    """r06: on the offset-conv GEMM route the forward keeps its offset-conv im2col (and W') in
+    the workspace, and a DCN_BWD_COL_IN_WS backward reads them instead of recomputing. A
+    backward without the flag recomputes everything: every output bit for bit the same. A
+    forward that took the VALU offset conv (dcn_debug_offset_gemm(0)) leaves no im2col, and
+    the handle's per-workspace record makes the GEMM-route backward after it recompute: the
+    gradients stay the oracle's."""
+    c = _rand_case(513, B=4, C=512, O_=64, H=14, W=14, s=(2, 2), p=(1, 1), dil=(2, 2), G=4)
+    h = gpu_handle
+    r1 = _device_fwd_bwd(h, c)
+    r0 = _device_fwd_bwd(h, c, bwd_flags=0)
+    _bitwise_equal(r1, r0, "reuse vs recompute")
+    L = h.lib
+    rt.check(L.dcn_debug_offset_gemm(0))
+    try:
+        out, off, g = _device_fwd_bwd(h, c, between=lambda: rt.check(L.dcn_debug_offset_gemm(1)))
+    finally:
+        rt.check(L.dcn_debug_offset_gemm(1))
+    ro, roff, rg = _c_oracle_all(c, off)
+    _check_all(out, off, g, ro, roff, rg, "VALU forward, GEMM-route backward")
+
+
 @pytest.mark.parametrize("math", [3, 6])
 def test_offset_conv_gemm_native_under_split_math(gpu_handle, math):
     """dcn_set_math covers the op's three GEMMs only (include/dcn.h). The offset

@@ -88,8 +88,11 @@ class Dev:
         self.ptrs = []
 
 
-def _device_fwd_bwd(h, c):
-    """dcn_forward + dcn_backward on device buffers, columns reused (DCN_BWD_COL_IN_WS)."""
+def _device_fwd_bwd(h, c, bwd_flags=None, between=None):
+    """dcn_forward + dcn_backward on device buffers, columns reused (DCN_BWD_COL_IN_WS unless
+    bwd_flags says otherwise); `between()` runs after the forward, before the backward."""
+    if bwd_flags is None:
+        bwd_flags = rt.DCN_BWD_COL_IN_WS
     x, wo, bo, w, b, gout = c["x"], c["w_off"], c["b_off"], c["w"], c["b"], c["grad_out"]
     B, C, H, W = x.shape
     O_, _, kh, kw = w.shape
@@ -107,13 +110,15 @@ def _device_fwd_bwd(h, c):
         vp = ctypes.c_void_p
         rt.check(h.lib.dcn_forward(h.h, desc, vp(px), vp(pwo), vp(pbo), vp(pw), vp(pb), vp(pout),
                                    vp(poff), vp(ws), wsb), "dcn_forward")
+        if between is not None:
+            between()
         pgo = D.up(gout)
         pgx, pgw = D.zeros(x.nbytes), D.zeros(w.nbytes)
         pgb = D.zeros(O_ * 4) if b is not None else None
         pgwo, pgbo, pgoff = D.zeros(wo.nbytes), D.zeros(J * 4), D.zeros(B * J * Ho * Wo * 4)
         rt.check(h.lib.dcn_backward(h.h, desc, vp(px), vp(poff), vp(pwo), vp(pw), vp(pgo), vp(pgx),
                                     vp(pgw), vp(pgb), vp(pgwo), vp(pgbo), vp(pgoff), vp(ws), wsb,
-                                    rt.DCN_BWD_COL_IN_WS), "dcn_backward")
+                                    bwd_flags), "dcn_backward")
         out, off = D.down(pout, (B, O_, Ho, Wo)), D.down(poff, (B, J, Ho, Wo))
         g = {"x": D.down(pgx, x.shape), "weight": D.down(pgw, w.shape),
              "offset_conv.weight": D.down(pgwo, wo.shape), "offset_conv.bias": D.down(pgbo, (J,)),
