@@ -19,6 +19,9 @@
 #include "dcn_internal.h"
 
 // A/B: the bf16 offset backward's ∂x kernel on the side stream beside ∂W_off
+#ifndef DCN_K5_EV
+#define DCN_K5_EV 1
+#endif
 #ifndef OCG_REUSE
 #define OCG_REUSE 1
 #endif
@@ -295,6 +298,7 @@ struct dcn_handle {
   hipStream_t comm_stream = nullptr;
   hipStream_t grad_stream = nullptr;  // caller's stream to release at ∂W/∂b-final
   hipEvent_t dw_main = nullptr, dw_aux = nullptr, end_ev = nullptr, comm_done = nullptr;
+  hipEvent_t k5_ev = nullptr;  // bf16 backward: the side-stream work K5 depends on is done
   // host-pointer API: device copies of the tensors no module state keeps (outputs and
   // gradients, grow-only, one per role), the pinned staging ring, the per-module states
   // (dcn_host_state, hs0 = the one dcn_forward_host / dcn_backward_host[_ex] use), and the
@@ -808,6 +812,8 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
       dcn::launch_channel_sum_bf16(gout, g.B, g.O, g.HW, F32(L.gb32), st, exch ? nullptr : gb);
     }
   }
+  // what K5 waits for on the side stream: the bins and the ∂b fold (issued above)
+  if (DCN_K5_EV) HIP_TRY(hipEventRecord(h->k5_ev, h->aux));
   // ∂W over the stored (or just recomputed) columns: the streaming MFMA kernel where it
   // applies (O = 256, K % 256 == 0: config 4), else the vendor GEMM (grouped where B allows)
   const bool dw_stream = !dw_fused && !h->dw_gemm && dw_stream_applies(g) &&
@@ -879,7 +885,14 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
       GEMM_TRY(h, sp, w, goutT, col);
     }
   }
-  DCN_TRY(join_aux(h));
+  // K5 needs the bins (and the ∂b fold done reading its tile sums in gxT, which K5
+  // overwrites): wait for the side-stream work up to k5_ev only. The ∂W partial sum issued
+  // after it is joined at the end; it has long finished by then, while a join here waited
+  // for it to end beside dcol_bf16 and then ≈11 µs more (r06 kernel trace at config 4).
+  if (DCN_K5_EV)
+    HIP_TRY(hipStreamWaitEvent(st, h->k5_ev, 0));
+  else
+    DCN_TRY(join_aux(h));
   {
     ProfScope ps(h, DCN_K_COL2IM);
     HIP_TRY(dcn::launch_col2im_bf16(g, xT, off32, col, nullptr, F32(L.gxT), goff32, base + L.bins, 0,
@@ -914,6 +927,9 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
                                         F32(L.wt), gx32, F32(L.gwo32), F32(L.gbo32), F32(L.gxT),
                                         st));
   }
+  // everything on the side stream before the results (the MFMA offset backward with its
+  // side stream already ends with that join)
+  if (DCN_K5_EV && !(off_mfma && OFFB_CONC)) DCN_TRY(join_aux(h));
   // the bf16 results, one launch (the offset-conv parameter grads after the exchange when
   // there is one)
   dcn::ConvBatch cb;
@@ -983,7 +999,7 @@ int dcn_create(int device, dcn_handle** out) {
   const unsigned evf = hipEventDisableTiming | DCN_EV_XFLAGS;
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->fork_ev, evf);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->join_ev, evf);
-  for (hipEvent_t* ev : {&h->dw_main, &h->dw_aux, &h->end_ev, &h->comm_done})
+  for (hipEvent_t* ev : {&h->dw_main, &h->dw_aux, &h->end_ev, &h->comm_done, &h->k5_ev})
     if (e == hipSuccess) e = hipEventCreateWithFlags(ev, evf);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
@@ -1029,7 +1045,7 @@ int dcn_destroy(dcn_handle* h) {
   dcn::gemm_engine_destroy(h->gemm);
   if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
   if (h->join_ev) (void)hipEventDestroy(h->join_ev);
-  for (hipEvent_t ev : {h->dw_main, h->dw_aux, h->end_ev, h->comm_done})
+  for (hipEvent_t ev : {h->dw_main, h->dw_aux, h->end_ev, h->comm_done, h->k5_ev})
     if (ev) (void)hipEventDestroy(ev);
   if (h->comm_stream) {
     (void)hipStreamSynchronize(h->comm_stream);
