@@ -19,6 +19,9 @@
 #include "dcn_internal.h"
 
 // A/B: the bf16 offset backward's ∂x kernel on the side stream beside ∂W_off
+#ifndef BOFF_MAIN_F32
+#define BOFF_MAIN_F32 1
+#endif
 #ifndef DCN_K5_EV
 #define DCN_K5_EV 1
 #endif
@@ -1386,12 +1389,19 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
                         (flags & DCN_BWD_COL_IN_WS) != 0));
   {
     ProfScope ps(h, DCN_K_OFFSET_BWD);
-    // ∂b_off = Σ ∂offset (18 channels: a latency-bound reduction) on the side stream, beside
-    // the offset-conv ∂W / ∂x kernels
-    DCN_TRY(fork_aux(h));
-    // two-level over (channel, image) blocks (one block per channel held 18 CUs for 0.11 ms)
-    dcn::launch_channel_sum_2l(goff, g.B, g.J, g.HW, F(L.part), grad_b_off, h->aux);
-    if (ocg_on(g) && (size_t)g.J * g.K <= (size_t)g.B * g.HW * g.O) {
+    const bool ocg = ocg_on(g) && (size_t)g.J * g.K <= (size_t)g.B * g.HW * g.O;
+    // ∂b_off = Σ ∂offset (18 channels: a latency-bound reduction), two-level over (channel,
+    // image) blocks (one block per channel held 18 CUs for 0.11 ms). On the GEMM route it
+    // runs on the side stream beside the offset-conv GEMMs. On the MFMA route (r06) it runs
+    // on the main stream after ∂W_off: there the side stream carries the ∂x kernel, and with
+    // the sum queued ahead of it, ∂x ended 13 µs after ∂W_off's fold, and the join then
+    // waited ≈15 µs more (config 3 kernel trace, profiles/r06i_timeline_config3.txt).
+    const bool bsum_side = ocg || !BOFF_MAIN_F32;
+    if (bsum_side) {
+      DCN_TRY(fork_aux(h));
+      dcn::launch_channel_sum_2l(goff, g.B, g.J, g.HW, F(L.part), grad_b_off, h->aux);
+    }
+    if (ocg) {
       // r05: ∂W_off and the offset route of ∂x as GEMMs over the offset conv's im2col (the
       // columns region is free after K5; ∂W' [J][K] in the ∂outT region, free after ∂col)
       // with the forward's im2col and W' still in ws (DCN_BWD_COL_IN_WS and this handle's
@@ -1408,7 +1418,10 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
                                           h->stream, OFFB_CONC_F32 ? h->aux : nullptr,
                                           h->fork_ev, h->join_ev));
     }
-    DCN_TRY(join_aux(h));
+    if (bsum_side)
+      DCN_TRY(join_aux(h));
+    else
+      dcn::launch_channel_sum_2l(goff, g.B, g.J, g.HW, F(L.part), grad_b_off, h->stream);
   }
   return grads_final(h, grad_w_off, grad_b_off, g);
 }
