@@ -19,6 +19,9 @@
 #include "dcn_internal.h"
 
 // A/B: the bf16 offset backward's ∂x kernel on the side stream beside ∂W_off
+#ifndef BOFF_MAIN_BF16
+#define BOFF_MAIN_BF16 1
+#endif
 #ifndef BOFF_MAIN_F32
 #define BOFF_MAIN_F32 1
 #endif
@@ -912,7 +915,7 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
 #else
                                              nullptr, nullptr, nullptr,
 #endif
-                                             true));
+                                             true, BOFF_MAIN_BF16 ? F32(L.part) : nullptr));
     // (r02: the Wc swizzle and ∂b_off sums on the side stream beside ∂W_off measured slower,
     // offset bwd 0.115 -> 0.121 ms at config 4: concurrent kernels slow each other; r05: the
     // ∂x kernel there beside ∂W_off is faster, 0.0914-0.092 -> 0.0896-0.0901 ms, OFFB_CONC)

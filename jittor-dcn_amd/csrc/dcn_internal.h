@@ -119,7 +119,7 @@ hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16
                                        float* part, bf16_t* gx, float* gw_off, float* gb_off,
                                        hipStream_t s, hipStream_t aux = nullptr,
                                        hipEvent_t fork = nullptr, hipEvent_t join = nullptr,
-                                       bool wc_ready = false);
+                                       bool wc_ready = false, float* bsum_part = nullptr);
 // xT: channels-last x; goffT: scratch of offset_conv_goffT_floats(g). gxT_in == NULL:
 // grad_x is accumulated; else grad_x = transpose(gxT_in) + the offset-conv route, written
 // once (gxT_in: the sampling-route ∂x left channels-last by launch_col2im_*).

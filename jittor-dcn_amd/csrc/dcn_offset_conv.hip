@@ -1992,7 +1992,7 @@ hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16
                                        const float* goff, const float* gxT_in, bf16_t* wc,
                                        float* part, bf16_t* gx, float* gw_off, float* gb_off,
                                        hipStream_t s, hipStream_t aux, hipEvent_t fork,
-                                       hipEvent_t join, bool wc_ready) {
+                                       hipEvent_t join, bool wc_ready, float* bsum_part) {
   MfmaStage ms;
   if (!offset_bwd_bf16_ok(g) || !mfma_stage(g, &ms)) return hipErrorInvalidValue;
   const int KK = g.kh * g.kw, J8 = j8(g.J), KT16 = kt16(g);
@@ -2010,7 +2010,9 @@ hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16
                        J8, g.C, KK, KT16);
   // ∂b_off: one block per channel (r02, config 4: the two-level (channel, image) sum that the
   // fp32 path runs on its side stream measured 0.122 against 0.112 ms for this scope here)
-  if (gb_off) launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s2);
+  // bsum_part (B·J floats): ∂b_off as the two-level (channel, image) sum on the main stream
+  // after ∂W_off's fold instead (A/B knob of the caller)
+  if (gb_off && !bsum_part) launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s2);
   size_t lds_w, lds_x;
   bwd_bf16_lds(g, ms, &lds_w, &lds_x);
   // chunks per workgroup (config 4: 1 -> 48 + 11 us, 2 -> 42 + 7, 4 -> 53 + 6 for ∂W_off + fold)
@@ -2025,6 +2027,7 @@ hipError_t launch_offset_conv_bwd_bf16(const Geo& g, const bf16_t* x, const bf16
   const long E = (long)(g.C / 64) * ((KK * J8 + 31) / 32) * 2 * 1024;
   hipLaunchKernelGGL(wgrad_frag_reduce, dim3((unsigned)((E + 255) / 256)), dim3(1024), 0, s, g,
                      part, nblk, gw_off);
+  if (gb_off && bsum_part) launch_channel_sum_2l(goff, g.B, g.J, g.HW, bsum_part, gb_off, s);
 #if OFFB_CONC
   // (A/B) ∂x on the side stream, concurrent with ∂W_off + its fold on the main one
   if (aux)
