@@ -1396,9 +1396,9 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
     // ∂b_off = Σ ∂offset (18 channels: a latency-bound reduction), two-level over (channel,
     // image) blocks (one block per channel held 18 CUs for 0.11 ms). On the GEMM route it
     // runs on the side stream beside the offset-conv GEMMs. On the MFMA route (r06) it runs
-    // on the main stream after ∂W_off: there the side stream carries the ∂x kernel, and with
-    // the sum queued ahead of it, ∂x ended 13 µs after ∂W_off's fold, and the join then
-    // waited ≈15 µs more (config 3 kernel trace, profiles/r06i_timeline_config3.txt).
+    // on the main stream after ∂W_off's fold, before the ∂x join: there the side stream
+    // carries the ∂x kernel, and with the sum queued ahead of it, ∂x ended 13 µs after the
+    // fold, and the join then waited ≈15 µs more (profiles/r06i_timeline_config3.txt).
     const bool bsum_side = ocg || !BOFF_MAIN_F32;
     if (bsum_side) {
       DCN_TRY(fork_aux(h));
@@ -1415,16 +1415,14 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
                                    F(L.goutT), F(L.gxT), grad_x, grad_w_off,
                                    reuse ? F(L.ocol) : nullptr));
     } else {
+      // (∂b_off inside, on the main stream before its join, unless on the side stream above)
       HIP_TRY(dcn::launch_offset_conv_bwd(g, x, F(L.xT), w_off, goff, F(L.goffT), F(L.wt), grad_x,
-                                          grad_w_off, nullptr,
+                                          grad_w_off, bsum_side ? nullptr : grad_b_off,
                                           dcn::get_force_generic() ? nullptr : F(L.gxT),
                                           h->stream, OFFB_CONC_F32 ? h->aux : nullptr,
-                                          h->fork_ev, h->join_ev));
+                                          h->fork_ev, h->join_ev, F(L.part)));
     }
-    if (bsum_side)
-      DCN_TRY(join_aux(h));
-    else
-      dcn::launch_channel_sum_2l(goff, g.B, g.J, g.HW, F(L.part), grad_b_off, h->stream);
+    if (bsum_side) DCN_TRY(join_aux(h));
   }
   return grads_final(h, grad_w_off, grad_b_off, g);
 }

@@ -128,7 +128,8 @@ hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
                                   const float* w_off, const float* goff, float* goffT, float* wt2,
                                   float* gx, float* gw_off, float* gb_off, const float* gxT_in,
                                   hipStream_t s, hipStream_t aux = nullptr,
-                                  hipEvent_t fork = nullptr, hipEvent_t join = nullptr);
+                                  hipEvent_t fork = nullptr, hipEvent_t join = nullptr,
+                                  float* bsum_part = nullptr);  // B·J floats: two-level ∂b_off
 // The MFMA offset-conv backward (stride 1) in pieces, so that batch chunk k's ∂W_off / ∂x
 // can run on a side stream beside chunk k+1's col2im: prep (w_off transpose) once,
 // chunk(b0, nb) per image range (after that range's ∂offset exists), finish once (∂W_off
@@ -154,7 +155,8 @@ hipError_t launch_offset_bwd_chunk(const Geo& g, const void* xT, bool xT_bf16, c
                                    const float* gxT_in, int b0, int nb, hipStream_t s,
                                    hipStream_t s_dx = nullptr);
 hipError_t launch_offset_bwd_finish(const Geo& g, const float* goff, const float* goffT,
-                                    float* gw_off, float* gb_off, hipStream_t s);
+                                    float* gw_off, float* gb_off, hipStream_t s,
+                                    float* bsum_part = nullptr);
 // dcn_reduce.hip conversions: bf16 <-> f32 (RNE), and the bf16 rounding of a f32 tensor
 // in place (out = bf16(v), v = f32(out)) so later f32 work sees exactly the bf16 value.
 hipError_t launch_bf16_to_f32(const bf16_t* in, float* out, size_t n, hipStream_t s);

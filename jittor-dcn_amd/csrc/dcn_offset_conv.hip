@@ -2476,13 +2476,15 @@ hipError_t launch_offset_bwd_chunk(const Geo& g, const void* xT, bool xT_bf16, c
 }
 
 hipError_t launch_offset_bwd_finish(const Geo& g, const float* goff, const float* goffT,
-                                    float* gw_off, float* gb_off, hipStream_t s) {
+                                    float* gw_off, float* gb_off, hipStream_t s,
+                                    float* bsum_part) {
   MfmaStage ms;
   if (!mfma_stage(g, &ms)) return hipErrorInvalidValue;
   const long E = (long)g.C * g.J * g.kh * g.kw;
   hipLaunchKernelGGL(wgrad_mfma_reduce, dim3((unsigned)((E + 255) / 256)), dim3(1024), 0, s, g,
                      goffT, g.B * ms.cpi / wgrad_cpb(g, ms), gw_off);
-  if (gb_off) launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
+  if (gb_off && bsum_part) launch_channel_sum_2l(goff, g.B, g.J, g.HW, bsum_part, gb_off, s);
+  else if (gb_off) launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
   return hipGetLastError();
 }
 
@@ -2492,7 +2494,7 @@ hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
                                   const float* w_off, const float* goff, float* goffT, float* wt2,
                                   float* gx, float* gw_off, float* gb_off, const float* gxT_in,
                                   hipStream_t s, hipStream_t aux, hipEvent_t fork,
-                                  hipEvent_t join) {
+                                  hipEvent_t join, float* bsum_part) {
   const int KK = g.kh * g.kw;
   bool generic = false;
   DCN_KK_DISPATCH(KK, (void)KKc);
@@ -2507,14 +2509,17 @@ hipError_t launch_offset_conv_bwd(const Geo& g, const float* x, const float* xT,
     }
     if (e == hipSuccess)
       e = launch_offset_bwd_chunk(g, xT, false, goff, goffT, wt2, gx, gxT_in, 0, g.B, s, aux);
-    if (e == hipSuccess) e = launch_offset_bwd_finish(g, goff, goffT, gw_off, gb_off, s);
+    // (∂b_off, when asked for, on the main stream after the ∂W_off fold and before the join:
+    // the ∂x kernel on the side stream is the longer branch, r06)
+    if (e == hipSuccess) e = launch_offset_bwd_finish(g, goff, goffT, gw_off, gb_off, s, bsum_part);
     if (e == hipSuccess && aux) {
       e = hipEventRecord(join, aux);
       if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
     }
     return e;
   }
-  if (gb_off) launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
+  if (gb_off && bsum_part) launch_channel_sum_2l(goff, g.B, g.J, g.HW, bsum_part, gb_off, s);
+  else if (gb_off) launch_channel_sum(goff, g.B, g.J, g.HW, gb_off, s);
   if (generic) {
     hipError_t e = hipMemsetAsync(gw_off, 0, (size_t)g.J * g.C * KK * sizeof(float), s);
     if (e != hipSuccess) return e;
