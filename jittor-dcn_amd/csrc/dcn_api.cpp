@@ -25,6 +25,9 @@
 #ifndef BOFF_MAIN_F32
 #define BOFF_MAIN_F32 1
 #endif
+#ifndef BSUM_F32_AUX
+#define BSUM_F32_AUX 0
+#endif
 #ifndef DCN_K5_EV
 #define DCN_K5_EV 1
 #endif
@@ -570,8 +573,8 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
         dcn::xpose_chsum_floats(g.B, g.O, g.HW) <= (size_t)g.B * g.HWi * g.C)
       // tile sums in gxT (written only by K5, after the join), the fold on the side stream
       // beside the ∂W GEMM (it only feeds ∂b)
-      HIP_TRY(dcn::launch_xpose_chsum(gout, goutT, gxT, gb, g.B, g.O, g.HW, h->stream, h->aux,
-                                      h->fork_ev));
+      HIP_TRY(dcn::launch_xpose_chsum(gout, goutT, gxT, gb, g.B, g.O, g.HW, h->stream,
+                                      BSUM_F32_AUX ? h->aux : nullptr, h->fork_ev));
     else if (flat && has_bias)
       HIP_TRY(dcn::launch_xpose_chsum(gout, goutT, parts, gb, g.B, g.O, g.HW, h->stream));
     else if (flat)
