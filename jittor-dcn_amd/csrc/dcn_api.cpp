@@ -19,30 +19,6 @@
 #include "dcn_internal.h"
 
 // A/B: the bf16 offset backward's ∂x kernel on the side stream beside ∂W_off
-#ifndef BOFF_MAIN_BF16
-#define BOFF_MAIN_BF16 1
-#endif
-#ifndef BOFF_MAIN_F32
-#define BOFF_MAIN_F32 1
-#endif
-#ifndef BSUM_F32_AUX
-#define BSUM_F32_AUX 0
-#endif
-#ifndef DCN_K5_EV
-#define DCN_K5_EV 1
-#endif
-#ifndef OCG_REUSE
-#define OCG_REUSE 1
-#endif
-#ifndef DCN_BSUM_AUX
-#define DCN_BSUM_AUX 1
-#endif
-#ifndef DCN_SUMP_AUX
-#define DCN_SUMP_AUX 1
-#endif
-#ifndef DCN_EV_XFLAGS
-#define DCN_EV_XFLAGS hipEventDisableSystemFence
-#endif
 #ifndef OFFB_CONC
 #define OFFB_CONC 1
 #endif
@@ -571,10 +547,10 @@ int core_backward(dcn_handle* h, const Geo& g, const float* x, const float* off,
     ProfScope ps(h, DCN_K_BWD_BIAS);
     if (flat && has_bias &&
         dcn::xpose_chsum_floats(g.B, g.O, g.HW) <= (size_t)g.B * g.HWi * g.C)
-      // tile sums in gxT (written only by K5, after the join), the fold on the side stream
-      // beside the ∂W GEMM (it only feeds ∂b)
-      HIP_TRY(dcn::launch_xpose_chsum(gout, goutT, gxT, gb, g.B, g.O, g.HW, h->stream,
-                                      BSUM_F32_AUX ? h->aux : nullptr, h->fork_ev));
+      // tile sums in gxT (written only by K5, later on this stream), their fold right after
+      // on this stream too (r06: on the side stream it queued behind the bin sort, and K5
+      // waited for both; config 5, DESIGN.md "r06: the fp32 ∂b fold on the main stream")
+      HIP_TRY(dcn::launch_xpose_chsum(gout, goutT, gxT, gb, g.B, g.O, g.HW, h->stream));
     else if (flat && has_bias)
       HIP_TRY(dcn::launch_xpose_chsum(gout, goutT, parts, gb, g.B, g.O, g.HW, h->stream));
     else if (flat)
@@ -813,7 +789,7 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
     // gxT, which only K5 writes, after this)
     if (dcn::xpose_chsum_bf16_floats(g.B, g.O, g.HW) <= (size_t)g.B * g.HWi * g.C &&
         dcn::launch_xpose_chsum_bf16(gout, goutT, F32(L.gxT), F32(L.gb32), exch ? nullptr : gb,
-                                     g.B, g.O, g.HW, st, DCN_BSUM_AUX ? h->aux : nullptr,
+                                     g.B, g.O, g.HW, st, h->aux,
                                      h->fork_ev)) {
       HIP_TRY(hipGetLastError());
       have_goutT = true;
@@ -822,7 +798,7 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
     }
   }
   // what K5 waits for on the side stream: the bins and the ∂b fold (issued above)
-  if (DCN_K5_EV) HIP_TRY(hipEventRecord(h->k5_ev, h->aux));
+  HIP_TRY(hipEventRecord(h->k5_ev, h->aux));
   // ∂W over the stored (or just recomputed) columns: the streaming MFMA kernel where it
   // applies (O = 256, K % 256 == 0: config 4), else the vendor GEMM (grouped where B allows)
   const bool dw_stream = !dw_fused && !h->dw_gemm && dw_stream_applies(g) &&
@@ -869,12 +845,8 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
     // the partial-plane sum on the side stream, beside ∂col (it reads 66 MB at config 4;
     // ∂col is bound by its stores). join_aux below (before K5) and dw_final's dw_aux event
     // order it before everything that reads ∂W.
-    hipStream_t ss = st;
-    if (DCN_SUMP_AUX) {
-      DCN_TRY(fork_aux(h));
-      ss = h->aux;
-    }
-    HIP_TRY(dcn::launch_sum_partials(F32(L.parts), nparts, (size_t)g.K * g.O, F32(L.gw32), ss,
+    DCN_TRY(fork_aux(h));
+    HIP_TRY(dcn::launch_sum_partials(F32(L.parts), nparts, (size_t)g.K * g.O, F32(L.gw32), h->aux,
                                      exch ? nullptr : gw));
   }
   DCN_TRY(dw_final(h, F32(L.gw32), has_bias ? F32(L.gb32) : nullptr, g, exch ? gw : nullptr,
@@ -898,10 +870,7 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
   // overwrites): wait for the side-stream work up to k5_ev only. The ∂W partial sum issued
   // after it is joined at the end; it has long finished by then, while a join here waited
   // for it to end beside dcol_bf16 and then ≈11 µs more (r06 kernel trace at config 4).
-  if (DCN_K5_EV)
-    HIP_TRY(hipStreamWaitEvent(st, h->k5_ev, 0));
-  else
-    DCN_TRY(join_aux(h));
+  HIP_TRY(hipStreamWaitEvent(st, h->k5_ev, 0));
   {
     ProfScope ps(h, DCN_K_COL2IM);
     HIP_TRY(dcn::launch_col2im_bf16(g, xT, off32, col, nullptr, F32(L.gxT), goff32, base + L.bins, 0,
@@ -918,7 +887,7 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
 #else
                                              nullptr, nullptr, nullptr,
 #endif
-                                             true, BOFF_MAIN_BF16 ? F32(L.part) : nullptr));
+                                             true, F32(L.part)));
     // (r02: the Wc swizzle and ∂b_off sums on the side stream beside ∂W_off measured slower,
     // offset bwd 0.115 -> 0.121 ms at config 4: concurrent kernels slow each other; r05: the
     // ∂x kernel there beside ∂W_off is faster, 0.0914-0.092 -> 0.0896-0.0901 ms, OFFB_CONC)
@@ -938,7 +907,7 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
   }
   // everything on the side stream before the results (the MFMA offset backward with its
   // side stream already ends with that join)
-  if (DCN_K5_EV && !(off_mfma && OFFB_CONC)) DCN_TRY(join_aux(h));
+  if (!(off_mfma && OFFB_CONC)) DCN_TRY(join_aux(h));
   // the bf16 results, one launch (the offset-conv parameter grads after the exchange when
   // there is one)
   dcn::ConvBatch cb;
@@ -1005,7 +974,7 @@ int dcn_create(int device, dcn_handle** out) {
   h->stream = h->own;
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking);
   // stream-to-stream events on this device only: no system-scope fence at record / wait
-  const unsigned evf = hipEventDisableTiming | DCN_EV_XFLAGS;
+  const unsigned evf = hipEventDisableTiming | hipEventDisableSystemFence;
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->fork_ev, evf);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->join_ev, evf);
   for (hipEvent_t* ev : {&h->dw_main, &h->dw_aux, &h->end_ev, &h->comm_done, &h->k5_ev})
@@ -1402,7 +1371,7 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
     // on the main stream after ∂W_off's fold, before the ∂x join: there the side stream
     // carries the ∂x kernel, and with the sum queued ahead of it, ∂x ended 13 µs after the
     // fold, and the join then waited ≈15 µs more (profiles/r06i_timeline_config3.txt).
-    const bool bsum_side = ocg || !BOFF_MAIN_F32;
+    const bool bsum_side = ocg;
     if (bsum_side) {
       DCN_TRY(fork_aux(h));
       dcn::launch_channel_sum_2l(goff, g.B, g.J, g.HW, F(L.part), grad_b_off, h->aux);
@@ -1413,7 +1382,7 @@ int dcn_backward(dcn_handle* h, const dcn_desc* d, const float* x, const float* 
       // with the forward's im2col and W' still in ws (DCN_BWD_COL_IN_WS and this handle's
       // record), ∂W' reads them and the ∂ocol product goes to the free columns region
       const bool reuse = L.has_ocol && (flags & DCN_BWD_COL_IN_WS) != 0 &&
-                         ws_rec_has(h, h->ocol_ws, ws) && OCG_REUSE;
+                         ws_rec_has(h, h->ocol_ws, ws);
       DCN_TRY(offset_conv_bwd_gemm(h, g, F(L.xT), w_off, goff, F(L.wt), F(L.col), F(L.goffT),
                                    F(L.goutT), F(L.gxT), grad_x, grad_w_off,
                                    reuse ? F(L.ocol) : nullptr));
