@@ -843,8 +843,8 @@ int backward_bf16(dcn_handle* h, const Geo& g, bool has_bias, const bf16_t* x, c
       GEMM_TRY(h, sp, col, gout, F32(L.parts));
     }
     // the partial-plane sum on the side stream, beside ∂col (it reads 66 MB at config 4;
-    // ∂col is bound by its stores). join_aux below (before K5) and dw_final's dw_aux event
-    // order it before everything that reads ∂W.
+    // ∂col is bound by its stores). The side stream's join at the end of the backward and
+    // dw_final's dw_aux event order it before everything that reads ∂W.
     DCN_TRY(fork_aux(h));
     HIP_TRY(dcn::launch_sum_partials(F32(L.parts), nparts, (size_t)g.K * g.O, F32(L.gw32), h->aux,
                                      exch ? nullptr : gw));
