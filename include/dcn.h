@@ -169,7 +169,11 @@ int dcn_forward_ex(dcn_handle* h, const dcn_desc* d, const float* x,
                               record does not notice a foreign write into a recorded ws. The
                               offsets are then also the forward's (a DCN_BF16 backward reads
                               the fp32 offsets that forward left in ws, r06): off must be that
-                              forward's output, as the columns already assume. */
+                              forward's output, as the columns already assume. On the DCN_F32
+                              offset-conv GEMM route (stride / dilation != 1, e.g. BASELINE
+                              config 5) the backward also reads the offset conv's im2col and
+                              reshaped w_off that forward left in ws (r06), tracked per
+                              workspace the same way: w_off must be that forward's too. */
 
 /* Autodiff of DeformConv2d.execute as triggered by optimizer.backward
  * (train.py:414). Overwrites grad_x, grad_w, grad_b (if has_bias),
